@@ -1,0 +1,43 @@
+# Top-level build.  `make` builds the product library and the CPU oracle;
+# `make ref` additionally builds the reference harness from /root/reference
+# (test infrastructure, see oracle/Makefile).
+#
+#   p64_amd/libp64gpu.so   HIP kernels (gfx950) + C ABI (include/p64gpu.h)
+#   p64_amd/p64gpu_enc     C host encoder driver over the C ABI
+#   oracle/liboracle.so    CPU restatement used as the parity checker
+
+HIPCC   ?= /opt/rocm/bin/hipcc
+CC      ?= gcc
+ARCH    ?= gfx950
+HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Wall -Wno-unused-function
+LIB     := p64_amd/libp64gpu.so
+
+all: $(LIB) p64_amd/p64gpu_enc oracle
+
+p64_amd/csrc/synth.o: p64_amd/csrc/synth.c include/p64gpu.h
+	$(CC) -O2 -fPIC -Wall -c $< -o $@
+
+p64_amd/csrc/p64gpu.o: p64_amd/csrc/p64gpu.hip include/p64gpu.h
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(LIB): p64_amd/csrc/p64gpu.o p64_amd/csrc/synth.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $^
+
+p64_amd/p64gpu_enc: p64_amd/host/p64gpu_enc.c $(LIB) include/p64gpu.h
+	$(CC) -O2 -Wall -o $@ $< -Lp64_amd -lp64gpu -Wl,-rpath,'$$ORIGIN'
+
+oracle:
+	$(MAKE) -C oracle
+
+ref:
+	$(MAKE) -C oracle ref
+
+# ISA listing of the kernels for inspection (not part of the build)
+asm: p64_amd/csrc/p64gpu.hip
+	$(HIPCC) $(HIPFLAGS) --offload-arch=$(ARCH) -S --cuda-device-only -o build/p64gpu.s $<
+
+clean:
+	rm -f p64_amd/csrc/*.o $(LIB) p64_amd/p64gpu_enc
+	$(MAKE) -C oracle clean
+
+.PHONY: all oracle ref asm clean

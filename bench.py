@@ -1,0 +1,285 @@
+#!/usr/bin/env python3
+"""bench.py -- macroblocks/s of the fused MI355X encode hot path (BASELINE.json).
+
+Workload (BASELINE.json configs[2], the metric's config): CIF 352x288 inter
+pictures, brute-force FastBME search at SearchLimit 31 ([-15,14]^2, 900
+candidates, me.c:206) + MTYPE decision + prediction/loop filter + ChenDct +
+quantisation + zigzag + CBP + IQ/ChenIDct reconstruction, bit-exact with the
+reference.  Each GPU encodes S independent closed-loop sequences (the chunks
+`p64 -a first -b last` would encode); one STEP = one picture of
+every sequence = ONE launch of the fused kernel over S*396 macroblocks.  The
+intra first picture and W warmup steps run untimed; K steps are timed with
+inputs resident in HBM (generated on the device by the same integer generator
+the CPU legs use).
+
+Multi-GPU: one process per GPU (torch.distributed, RCCL); rank r encodes its
+own S sequences (weak scaling, no data-path collective).  The timed region is
+bracketed by barrier + synchronize; the max over ranks is reported.
+
+Extra objects on the JSON line:
+  roofline      HBM roofline of the fused kernel (algorithmic bytes)
+  roofline_sad  VALU v_sad_u8 roofline (the binding one for FULL search)
+  cpu_baseline  the reference encoder (oracle/_ref, built from /root/reference
+                sources) timed on this host's cores on a bounded sample
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import shutil
+import subprocess
+import sys
+import tempfile
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+METRIC = "macroblocks/s (full-search ME+DCT+quant), CIF inter; % HBM roofline"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
+# v_sad_u8: 4 byte-absolute-differences per lane; 256 CUs x 4 SIMD32 x 32 lanes
+# per clock at 2.4 GHz (MI355X_MICROARCH.md: 4 SIMD-32 per CU, 2400 MHz)
+SAD_PEAK = 256 * 4 * 32 * 4 * 2.4e9
+# algorithmic HBM bytes per macroblock of the fused kernel:
+#   read  cur 384 + previous recon 384 + last_intra 1
+#   write coef 768 + recon 384 + p64_mb_rec 4 + p64_me_rec 28 + last_intra 1
+BYTES_PER_MB = 384 + 384 + 1 + 768 + 384 + 4 + 28 + 1
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--mode", choices=("full", "tss"), default="full")
+    p.add_argument("--search-limit", type=int, default=31)
+    p.add_argument("--quant", type=int, default=8)
+    p.add_argument("--width", type=int, default=352)
+    p.add_argument("--height", type=int, default=288)
+    p.add_argument("--streams", type=int, default=256, help="sequences per GPU")
+    p.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    p.add_argument("--cpu-procs", type=int, default=8)
+    p.add_argument("--cpu-frames", type=int, default=120)
+    p.add_argument("--no-verify", action="store_true")
+    p.add_argument("--pmc-json", default=os.path.join(REPO, "profiles", "pmc_traffic.json"))
+    return p.parse_args()
+
+
+def shard_seeds(rank: int, streams: int) -> tuple[int, int]:
+    """Weak scaling: rank r owns sequences seed0 .. seed0+streams-1."""
+    return 1 + rank * streams, streams
+
+
+# ---------------------------------------------------------------------------
+# CPU baseline (rank 0, N = 1 only; runs before the GPU is touched)
+
+def write_y4m(path, frames, w, h):
+    with open(path, "wb") as f:
+        f.write(b"YUV4MPEG2 W%d H%d F30000:1001 Ip A0:0 C420jpeg\n" % (w, h))
+        for fr in frames:
+            f.write(b"FRAME\n")
+            f.write(fr.tobytes())
+
+
+def cpu_baseline(args):
+    import p64_amd  # host-only synth (no GPU use)
+
+    w, h = args.width, args.height
+    fmt = {(352, 288): "-CIF", (176, 144): "-QCIF", (352, 240): "-NTSC"}.get((w, h))
+    nmb = (w // 16) * (h // 16)
+    procs = max(1, min(args.cpu_procs, os.cpu_count() or 1))
+    nfr = args.cpu_frames
+    refbin = os.path.join(REPO, "oracle", "_ref", "p64hook")
+    with tempfile.TemporaryDirectory() as td:
+        for k in range(procs):
+            frames = [p64_amd.synth_frame(1 + k, t, w, h) for t in range(nfr)]
+            write_y4m(os.path.join(td, f"s{k}.y4m"), frames, w, h)
+        if fmt and os.access(refbin, os.X_OK):
+            env = dict(os.environ)
+            if args.mode == "full":
+                env["P64REF_ME"] = "full"
+            env.pop("P64REF_DUMP", None)
+            cmds = [[refbin, fmt, "-y4m", "-a", "0", "-b", str(nfr - 1), "-q", str(args.quant),
+                     "-i", str(args.search_limit), os.path.join(td, f"s{k}"), "-z", ".y4m",
+                     "-s", os.path.join(td, f"s{k}.p64")] for k in range(procs)]
+            t0 = time.perf_counter()
+            ps = [subprocess.Popen(c, env=env, stdout=subprocess.DEVNULL) for c in cmds]
+            rc = [p.wait() for p in ps]
+            dt = time.perf_counter() - t0
+            if any(rc):
+                raise RuntimeError(f"reference encoder failed: {rc}")
+            mbs = procs * nfr * nmb
+            me = "FastBME SL=%d" % args.search_limit if args.mode == "full" else "StepBME (TSS)"
+            return {"value": round(mbs / dt, 1), "unit": "macroblocks/s", "cores": procs,
+                    "kind": "reference",
+                    "sample": f"{procs} concurrent reference encoder processes (oracle/_ref/p64hook, "
+                              f"unmodified reference objects, {me}), each a {nfr}-picture "
+                              f"{w}x{h} y4m sequence (first intra), q={args.quant}; "
+                              f"{mbs} MBs in {dt:.2f} s wall incl. VLC and file I/O"}
+        # fallback: the clean-room port (single core)
+        sys.path.insert(0, os.path.join(REPO, "oracle"))
+        import oracle
+
+        frames = [p64_amd.synth_frame(1, t, w, h) for t in range(min(nfr, 12))]
+        t0 = time.perf_counter()
+        oracle.encode_sequence(frames, w, h, quant=args.quant,
+                               me_mode=1 if args.mode == "full" else 0,
+                               search_limit=args.search_limit)
+        dt = time.perf_counter() - t0
+        mbs = len(frames) * nmb
+        return {"value": round(mbs / dt, 1), "unit": "macroblocks/s", "cores": 1, "kind": "port",
+                "sample": f"oracle/p64_oracle.c (scalar, no early exit) on {len(frames)} pictures "
+                          f"of one {w}x{h} sequence; {mbs} MBs in {dt:.2f} s"}
+
+
+# ---------------------------------------------------------------------------
+
+def load_pmc(path, workload_key):
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        e = d.get(workload_key)
+        return e if e else None
+    except (OSError, ValueError):
+        return None
+
+
+def main():
+    args = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        world = max(world, 1)
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        cpu = cpu_baseline(args)
+
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    import p64_amd
+
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    w, h = args.width, args.height
+    nmb = (w // 16) * (h // 16)
+    pic = w * h * 3 // 2
+    seed0, S = shard_seeds(rank, args.streams)
+    nslots = 1 + args.warmup + args.steps
+    mode = p64_amd.ME_FULL if args.mode == "full" else p64_amd.ME_TSS
+
+    frames = p64_amd.synth_frames_device(w, h, seed0, S, 0, nslots)  # [slot][stream][pic]
+    rec = [torch.zeros(S * pic, dtype=torch.uint8, device="cuda") for _ in range(2)]
+    li = torch.zeros(S * nmb, dtype=torch.uint8, device="cuda")
+    out = p64_amd.FrameBatchOut(
+        coef=torch.empty((S, nmb, 6, 64), dtype=torch.int16, device="cuda"),
+        mb=torch.empty((S, nmb, 4), dtype=torch.int8, device="cuda"),
+        me=torch.empty((S, nmb, 7), dtype=torch.int32, device="cuda"))
+
+    def step(t):
+        return p64_amd.encode_frames(frames[t].reshape(-1), rec[(t + 1) % 2], rec[t % 2], li,
+                                     width=w, height=h, intra=(t == 0), quant=args.quant,
+                                     me_mode=mode, search_limit=args.search_limit, out=out)
+
+    for t in range(1 + args.warmup):  # intra picture + warmup, untimed
+        step(t)
+    torch.cuda.synchronize()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    ev[0].record()
+    for k in range(args.steps):
+        step(1 + args.warmup + k)
+        ev[k + 1].record()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kern = [ev[k].elapsed_time(ev[k + 1]) * 1e-3 for k in range(args.steps)]
+    kavg = sum(kern) / len(kern)
+    tmax = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+    if world > 1:
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+    tmax = float(tmax.item())
+
+    verified = None
+    if rank == 0 and not args.no_verify:
+        # closed-loop check of sequence 0 against the CPU oracle: every picture
+        # feeds the next, so matching the last picture's outputs and
+        # reconstruction pins the whole chain (outside the timed region)
+        sys.path.insert(0, os.path.join(REPO, "oracle"))
+        import oracle
+
+        fr0 = [frames[t, 0].cpu().numpy() for t in range(nslots)]
+        o = oracle.encode_sequence(fr0, w, h, quant=args.quant, me_mode=mode,
+                                   search_limit=args.search_limit)
+        last = nslots - 1
+        coef, mb, me, recon = o[last]
+        verified = bool(
+            np.array_equal(out.coef[0].cpu().numpy(), coef)
+            and np.array_equal(out.mb[0].cpu().numpy().view(p64_amd.MB_DTYPE).reshape(nmb), mb)
+            and np.array_equal(out.me[0].cpu().numpy().view(p64_amd.ME_DTYPE).reshape(nmb), me)
+            and np.array_equal(rec[last % 2][:pic].cpu().numpy(), recon))
+        if not verified:
+            raise SystemExit("bench: GPU output differs from the oracle -- refusing to report")
+
+    if world > 1:
+        dist.destroy_process_group()
+    if rank != 0:
+        return
+
+    mbs_launch = S * nmb
+    value = world * mbs_launch * args.steps / tmax
+    bytes_launch = mbs_launch * BYTES_PER_MB
+    hbm_gbs = bytes_launch / kavg / 1e9
+    cand = 900 if args.mode == "full" else 33
+    if args.mode == "full":
+        hl = args.search_limit // 2
+        cand = (2 * hl) * (2 * hl)
+    sad_rate = mbs_launch * cand * 256 / kavg
+    workload = (f"{w}x{h} inter, {'FULL FastBME SL=%d' % args.search_limit if args.mode == 'full' else 'TSS StepBME'}, "
+                f"q={args.quant}, closed loop, {S} sequences/GPU")
+    key = f"{w}x{h}_{args.mode}{args.search_limit}_q{args.quant}_S{S}"
+    pmc = load_pmc(args.pmc_json, key)
+    line = {
+        "metric": METRIC,
+        "value": round(value, 1),
+        "unit": "macroblocks/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(tmax / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic (seeded integer generator, generated on device)",
+        "config": {"workload": workload, "width": w, "height": h, "me": args.mode,
+                   "search_limit": args.search_limit, "quant": args.quant,
+                   "sequences_per_gpu": S, "macroblocks_per_step_per_gpu": mbs_launch,
+                   "parallelism": f"dp{world} (independent sequences per GPU, no data-path collective)"},
+        "roofline": {"bound": "hbm", "achieved": round(hbm_gbs, 1), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(hbm_gbs / HBM_PEAK_GBS, 5),
+                     "traffic": (pmc or {}).get("hbm_bytes_per_launch"),
+                     "kernel": "k_encode<%d>" % (2 if args.mode == "full" else 1),
+                     "kernel_avg_us": round(kavg * 1e6, 2),
+                     "algorithmic_bytes_per_mb": BYTES_PER_MB},
+        "roofline_sad": {"bound": "valu", "achieved": round(sad_rate / 1e12, 3),
+                         "peak": round(SAD_PEAK / 1e12, 3), "unit": "T byte-absdiff/s",
+                         "frac": round(sad_rate / SAD_PEAK, 4), "candidates_per_mb": cand},
+        "cpu_baseline": cpu,
+        "verified_vs_oracle": verified,
+    }
+    print(json.dumps(line), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,194 @@
+/*
+ * p64gpu.h -- C ABI of the MI355X-native PVRG-P64 macroblock encode hot path.
+ *
+ * Plain C, plain pointers and sizes; no HIP or torch types cross this header
+ * (streams are passed as `void *` = hipStream_t, NULL = the default stream).
+ * Every entry point returns P64GPU_OK (0) or a negative P64GPU_E_* status and
+ * never calls exit(); p64gpu_last_error() gives the text of the last failure
+ * on the calling thread.
+ *
+ * What each entry point replaces in the reference (/root/reference, PVRG-P64
+ * v1.2 + maikmerten fork); INTEGRATION.md shows the host-side re-plumbing:
+ *
+ *   p64gpu_block_op            ChenDct chendct.c:97, ChenIDct chendct.c:217,
+ *                              CCITTQuantize transform.c:271, CCITTFlatQuantize
+ *                              :317, ICCITTFlatQuantize :359, ICCITTQuantize :400,
+ *                              BoundDctMatrix :460, BoundIDctMatrix :483,
+ *                              FlatBoundQuantizeMatrix :502, BoundQuantizeMatrix
+ *                              :526, IZigzagMatrix :546, ZigzagMatrix :561
+ *                              (the `vFunc *UseDct/UseIDct` plug-in, p64.c:227-231,
+ *                              batched over blocks)
+ *   p64gpu_motion_estimation   MotionEstimation(MEM*,MEM*) me.c:340 (TSS StepBME
+ *                              me.c:255 as shipped, or brute-force FastBME me.c:187)
+ *                              writing the MeX/MeY/MeVal/MeOVal/MeVAR/MeVAROR/MeMWOR
+ *                              arrays (me.c:49-60) as p64_me_rec records
+ *   p64gpu_encode_frames       GlobalMC io.c:129 + the per-MDU compute of
+ *                              p64EncodeGOB p64.c:692-786 (MTYPE decision),
+ *                              ReadCompressMDU p64.c:823, the reconstruction half
+ *                              of WriteMDU p64.c:945-959 and DecodeSaveMDU p64.c:971,
+ *                              for a batch of independent pictures
+ *   p64gpu_encoder_*           host-buffer, state-keeping form of the above for a C
+ *                              host loop: p64EncodeFrame p64.c:622 keeps CFS/OFS
+ *                              (previous/new reconstruction) device resident and
+ *                              swaps them (SwapFS p64.c:661)
+ *   p64gpu_decode_recon        DecompressMDU p64.c:1179 (IZigzag/IQ/IDCT) +
+ *                              DecodeSaveMDU p64.c:971 for decoded pictures
+ *
+ * Layouts.  A picture is planar 4:2:0: Y (w*h bytes) then U then V
+ * ((w/2)*(h/2) bytes each), stride = plane width (MEM, mem.h:37-42).  w and h
+ * are multiples of 16; batched pictures sit `frame_stride` bytes apart
+ * (multiple of 16).  Macroblocks are in RASTER order mb = mby*(w/16)+mbx (the
+ * index Bpos() yields in the MDU loop, io.c:757-783); GOB order is the host
+ * writer's business.  Per macroblock, blocks c = 0..3 are luma
+ * (h,v) = (0,0),(1,0),(0,1),(1,1), c = 4 is U, c = 5 is V (p64.c:77-79).
+ * Coefficients are int16 levels in zigzag order, [mb][6][64], exactly as
+ * ReadCompressMDU leaves inputbuf (p64.c:885) -- i.e. before CBP zeroing.
+ */
+#ifndef P64GPU_H
+#define P64GPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define P64GPU_ABI_VERSION 1
+
+enum p64gpu_status {
+  P64GPU_OK = 0,
+  P64GPU_E_INVALID = -1,  /* bad argument: shape, range, alignment or NULL */
+  P64GPU_E_NODEVICE = -2, /* no usable HIP device */
+  P64GPU_E_HIP = -3,      /* a HIP runtime call failed */
+  P64GPU_E_NOMEM = -4     /* device or host allocation failed */
+};
+
+/* Motion search (me.c).  TSS is what the reference ships (me.c:352); FULL is
+ * the dormant brute-force FastBME over [-sl/2, sl/2)^2 (me.c:206-208). */
+enum p64gpu_me_mode { P64GPU_ME_TSS = 0, P64GPU_ME_FULL = 1 };
+
+/* One macroblock's motion-estimation record (me.c:49-60, 353-359). */
+typedef struct {
+  int32_t mx, my; /* MeX, MeY: chosen vector                          */
+  int32_t sad;    /* MeVal  = MV, SAD of the chosen vector             */
+  int32_t sad0;   /* MeOVal = OMV, SAD of the (0,0) vector             */
+  int32_t var;    /* MeVAR   = sum((ref-cur)^2)/256 at the vector      */
+  int32_t varor;  /* MeVAROR = sum(ref^2)/256 - (sum(ref)/256)^2       */
+  int32_t mwor;   /* MeMWOR  = sum(ref)                                */
+} p64_me_rec;
+
+/* One coded macroblock's header fields (marker.c:288 WriteMBHeader inputs). */
+typedef struct {
+  int8_t mtype; /* MType 0..9 after the CBP fallback (p64.c:899-906)     */
+  int8_t cbp;   /* CBP (0x3f for types without CBP)                      */
+  int8_t mvx;   /* MVDH transmitted: the ME vector for MC types, else 0 */
+  int8_t mvy;   /* MVDV transmitted                                      */
+} p64_mb_rec;
+
+int p64gpu_abi_version(void);
+const char *p64gpu_strerror(int status);
+const char *p64gpu_last_error(void);
+
+/* ---- device selection / stream helpers (for C hosts without a runtime) ---- */
+int p64gpu_device_count(int *count);
+int p64gpu_set_device(int device);
+int p64gpu_synchronize(void *stream);
+
+/* ---- 8x8 block operations, batched (device pointers) -------------------- */
+enum p64gpu_block_op {
+  P64GPU_OP_DCT = 0,           /* ChenDct(in,out)                         */
+  P64GPU_OP_IDCT = 1,          /* ChenIDct(in,out)                        */
+  P64GPU_OP_QUANT_INTRA = 2,   /* CCITTFlatQuantize(m, dcq, acq)          */
+  P64GPU_OP_QUANT_INTER = 3,   /* CCITTQuantize(m, dcq, acq)              */
+  P64GPU_OP_IQUANT_INTRA = 4,  /* ICCITTFlatQuantize(m, dcq, acq)         */
+  P64GPU_OP_IQUANT_INTER = 5,  /* ICCITTQuantize(m, dcq, acq)             */
+  P64GPU_OP_BOUND_DCT = 6,     /* BoundDctMatrix(m)                       */
+  P64GPU_OP_BOUND_IDCT = 7,    /* BoundIDctMatrix(m)                      */
+  P64GPU_OP_BOUND_QFLAT = 8,   /* FlatBoundQuantizeMatrix(m)              */
+  P64GPU_OP_BOUND_QUANT = 9,   /* BoundQuantizeMatrix(m)                  */
+  P64GPU_OP_ZIGZAG = 10,       /* ZigzagMatrix(in,out)                    */
+  P64GPU_OP_IZIGZAG = 11,      /* IZigzagMatrix(in,out)                   */
+  P64GPU_OP_COUNT = 12
+};
+/* in/out: nblocks * 64 int32, row-major 8x8 blocks, device memory; in may
+ * equal out (in-place ops).  dcq/acq are only read by the quantiser ops
+ * (1..31; the intra DC step is normally 8, p64.c:874). */
+int p64gpu_block_op(int op, const int32_t *in, int32_t *out, int64_t nblocks,
+                    int dcq, int acq, void *stream);
+
+/* ---- motion estimation over a batch of pictures (device pointers) ------- */
+/* ref_y/cur_y: luma planes of nframes pictures, frame_stride apart.
+ * out: nframes * nmb records. search_limit in 1..31 (FULL only; TSS is +-15). */
+int p64gpu_motion_estimation(int width, int height, int nframes,
+                             int64_t frame_stride, const uint8_t *ref_y,
+                             const uint8_t *cur_y, int mode, int search_limit,
+                             p64_me_rec *out, void *stream);
+
+/* ---- the fused per-macroblock encode (device pointers) ------------------ */
+typedef struct {
+  int32_t width, height;  /* picture size, multiples of 16, 32..4096         */
+  int32_t nframes;        /* independent pictures in this launch (>= 1)      */
+  int32_t intra;          /* 1: first picture of a sequence -> all MTYPE 0,
+                             no ME (p64.c:635, 770-771)                      */
+  int32_t quant;          /* GQuant 1..31 (UseQuant without -r)              */
+  int32_t me_mode;        /* P64GPU_ME_TSS | P64GPU_ME_FULL                  */
+  int32_t search_limit;   /* FULL: 1..31 (SearchLimit, me.c:62, -i flag)     */
+  int32_t reserved;       /* must be 0                                       */
+  int64_t frame_stride;   /* bytes between pictures in cur/ref/recon        */
+  const uint8_t *cur;     /* [nframes] current pictures                       */
+  const uint8_t *ref;     /* [nframes] previous reconstructions (CFS);
+                             unused when intra                               */
+  uint8_t *recon;         /* [nframes] new reconstructions (OFS), written    */
+  uint8_t *last_intra;    /* [nframes][nmb] intra-refresh counters, in/out
+                             (LastIntra, p64.c:213, 772, 909-910)            */
+  const uint8_t *quant_mb;      /* NULL or [nframes][nmb] UseQuant per MB    */
+  const int8_t *mtype_override; /* NULL or [nframes][nmb]; < 0 = no override
+                                   (-o interpreter program 0, p64.c:761-768) */
+  int16_t *coef;          /* [nframes][nmb][6][64] zigzag levels, written    */
+  p64_mb_rec *mb;         /* [nframes][nmb], written                         */
+  p64_me_rec *me;         /* NULL or [nframes][nmb], written (inter only)    */
+} p64gpu_encode_args;
+
+int p64gpu_encode_frames(const p64gpu_encode_args *args, void *stream);
+
+/* ---- decoder-side reconstruction (device pointers) ---------------------- */
+/* recon must already hold the previous picture where MBs are not coded
+ * (p64DecodeGOB leaves untransmitted MBs untouched); coded_mask
+ * ([nmb] bytes, nonzero = MB present in the stream) selects the MBs written.
+ * mb[].mtype/cbp/mvx/mvy and quant_mb (UseQuant per MB) come from the host
+ * VLC decoder.  Pictures are independent within the call (nframes >= 1). */
+int p64gpu_decode_recon(int width, int height, int nframes, int64_t frame_stride,
+                        const uint8_t *ref, uint8_t *recon, const int16_t *coef,
+                        const p64_mb_rec *mb, const uint8_t *quant_mb,
+                        const uint8_t *coded_mask, void *stream);
+
+/* ---- host-buffer encoder context (drop-in for a C host loop) ------------ */
+typedef struct p64gpu_encoder p64gpu_encoder;
+int p64gpu_encoder_open(int device, int width, int height, int me_mode,
+                        int search_limit, p64gpu_encoder **out);
+/* Encodes one picture (host Y|U|V, w*h*3/2 bytes).  intra=1 starts a new
+ * sequence.  mtype_override may be NULL.  coef/mb are host outputs sized for
+ * nmb macroblocks; me and recon may be NULL.  The reconstruction stays on the
+ * device as the reference for the next call. */
+int p64gpu_encoder_frame(p64gpu_encoder *enc, const uint8_t *picture, int intra,
+                         int quant, const int8_t *mtype_override, int16_t *coef,
+                         p64_mb_rec *mb, p64_me_rec *me, uint8_t *recon);
+void p64gpu_encoder_close(p64gpu_encoder *enc);
+
+/* ---- deterministic synthetic input (integer only) ----------------------- */
+/* Host: picture `frame` of stream `seed` (Y|U|V, w*h*3/2 bytes). */
+void p64_synth_motion(uint32_t seed, int *mvx, int *mvy);
+void p64_synth_frame(uint32_t seed, int frame, int width, int height,
+                     uint8_t *out);
+/* Device: the same bytes for nslots x nseeds pictures, slot-major: picture
+ * (t, s) = p64_synth_frame(seed0 + s, frame0 + t) at out + (t*nseeds + s)*stride.
+ * nseeds*nslots <= 65535. */
+int p64gpu_synth_frames(int width, int height, uint32_t seed0, int nseeds,
+                        int frame0, int nslots, int64_t frame_stride,
+                        uint8_t *out, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* P64GPU_H */

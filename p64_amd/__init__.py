@@ -1,0 +1,364 @@
+"""p64_amd -- MI355X-native PVRG-P64 macroblock encode hot path.
+
+Python mirror of the reference's hot-path interface over the C ABI in
+include/p64gpu.h (libp64gpu.so, hand-written HIP for gfx950).  Names follow the
+reference (/root/reference):
+
+    ChenDct / ChenIDct                       chendct.c:97 / :217
+    CCITTQuantize / CCITTFlatQuantize        transform.c:271 / :317
+    ICCITTQuantize / ICCITTFlatQuantize      transform.c:400 / :359
+    BoundDctMatrix / BoundIDctMatrix         transform.c:460 / :483
+    FlatBoundQuantizeMatrix / BoundQuantizeMatrix   transform.c:502 / :526
+    ZigzagMatrix / IZigzagMatrix             transform.c:561 / :546
+    MotionEstimation                         me.c:340 (StepBME :255 / FastBME :187)
+    encode_frames                            p64.c:622-1013 per-MB compute, batched
+    Encoder                                  p64EncodeSequence/p64EncodeFrame loop
+                                             (closed loop, reconstruction on device)
+
+Block functions take/return int32 tensors of shape [..., 64] (row-major 8x8
+blocks) on a CUDA(HIP) device; the reference works on one `int[64]` at a time,
+these work on a batch.  There is no CPU fallback: if the HIP library is missing
+or no device is present the calls raise.  PyTorch is used only for device
+memory and the stream handle.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from dataclasses import dataclass
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libp64gpu.so")
+
+ME_TSS = 0
+ME_FULL = 1
+
+OP_DCT, OP_IDCT, OP_QUANT_INTRA, OP_QUANT_INTER, OP_IQUANT_INTRA, OP_IQUANT_INTER = range(6)
+OP_BOUND_DCT, OP_BOUND_IDCT, OP_BOUND_QFLAT, OP_BOUND_QUANT, OP_ZIGZAG, OP_IZIGZAG = range(6, 12)
+
+# coding-control tables, p64.c:217-222
+QUANT_MTYPE = (0, 1, 0, 1, 0, 0, 1, 0, 0, 1)
+CBP_MTYPE = (0, 0, 1, 1, 0, 1, 1, 0, 1, 1)
+INTRA_MTYPE = (1, 1, 0, 0, 0, 0, 0, 0, 0, 0)
+MF_MTYPE = (0, 0, 0, 0, 1, 1, 1, 1, 1, 1)
+FILTER_MTYPE = (0, 0, 0, 0, 0, 0, 0, 1, 1, 1)
+TCOEFF_MTYPE = (1, 1, 1, 1, 0, 1, 1, 0, 1, 1)
+
+
+class P64GpuError(RuntimeError):
+    pass
+
+
+class MeRec(ctypes.Structure):
+    """p64_me_rec: one MB of MeX/MeY/MeVal/MeOVal/MeVAR/MeVAROR/MeMWOR (me.c:49-60)."""
+    _fields_ = [(n, ctypes.c_int32) for n in ("mx", "my", "sad", "sad0", "var", "varor", "mwor")]
+
+
+class MbRec(ctypes.Structure):
+    """p64_mb_rec: MType, CBP, MVDH, MVDV as written by WriteMBHeader (marker.c:288)."""
+    _fields_ = [(n, ctypes.c_int8) for n in ("mtype", "cbp", "mvx", "mvy")]
+
+
+class EncodeArgs(ctypes.Structure):
+    _fields_ = [
+        ("width", ctypes.c_int32), ("height", ctypes.c_int32), ("nframes", ctypes.c_int32),
+        ("intra", ctypes.c_int32), ("quant", ctypes.c_int32), ("me_mode", ctypes.c_int32),
+        ("search_limit", ctypes.c_int32), ("reserved", ctypes.c_int32),
+        ("frame_stride", ctypes.c_int64),
+        ("cur", ctypes.c_void_p), ("ref", ctypes.c_void_p), ("recon", ctypes.c_void_p),
+        ("last_intra", ctypes.c_void_p), ("quant_mb", ctypes.c_void_p),
+        ("mtype_override", ctypes.c_void_p), ("coef", ctypes.c_void_p),
+        ("mb", ctypes.c_void_p), ("me", ctypes.c_void_p),
+    ]
+
+
+# numpy views of the record arrays (field order matches include/p64gpu.h)
+ME_DTYPE = np.dtype([(n, "<i4") for n in ("mx", "my", "sad", "sad0", "var", "varor", "mwor")])
+MB_DTYPE = np.dtype([(n, "i1") for n in ("mtype", "cbp", "mvx", "mvy")])
+
+_lib = None
+
+
+def lib() -> ctypes.CDLL:
+    """Load libp64gpu.so (built by `make` / __graft_entry__.build()); raise if absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise P64GpuError(f"{LIB_PATH} not built: run `make` (or __graft_entry__.build())")
+    L = ctypes.CDLL(LIB_PATH)
+    vp, i32, i64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64
+    L.p64gpu_abi_version.restype = i32
+    L.p64gpu_strerror.restype = ctypes.c_char_p
+    L.p64gpu_strerror.argtypes = [i32]
+    L.p64gpu_last_error.restype = ctypes.c_char_p
+    L.p64gpu_device_count.argtypes = [ctypes.POINTER(i32)]
+    L.p64gpu_set_device.argtypes = [i32]
+    L.p64gpu_synchronize.argtypes = [vp]
+    L.p64gpu_block_op.argtypes = [i32, vp, vp, i64, i32, i32, vp]
+    L.p64gpu_motion_estimation.argtypes = [i32, i32, i32, i64, vp, vp, i32, i32, vp, vp]
+    L.p64gpu_encode_frames.argtypes = [ctypes.POINTER(EncodeArgs), vp]
+    L.p64gpu_decode_recon.argtypes = [i32, i32, i32, i64, vp, vp, vp, vp, vp, vp, vp]
+    L.p64gpu_encoder_open.argtypes = [i32, i32, i32, i32, i32, ctypes.POINTER(vp)]
+    L.p64gpu_encoder_frame.argtypes = [vp, vp, i32, i32, vp, vp, vp, vp, vp]
+    L.p64gpu_encoder_close.argtypes = [vp]
+    L.p64gpu_encoder_close.restype = None
+    L.p64gpu_synth_frames.argtypes = [i32, i32, ctypes.c_uint32, i32, i32, i32, i64, vp, vp]
+    L.p64_synth_frame.argtypes = [ctypes.c_uint32, i32, i32, i32, vp]
+    L.p64_synth_frame.restype = None
+    L.p64_synth_motion.argtypes = [ctypes.c_uint32, ctypes.POINTER(i32), ctypes.POINTER(i32)]
+    L.p64_synth_motion.restype = None
+    if L.p64gpu_abi_version() != 1:
+        raise P64GpuError("libp64gpu.so ABI version mismatch")
+    _lib = L
+    return L
+
+
+def _check(status: int) -> None:
+    if status != 0:
+        L = lib()
+        raise P64GpuError(f"{L.p64gpu_strerror(status).decode()}: {L.p64gpu_last_error().decode()}")
+
+
+# ---------------------------------------------------------------------------
+# synthetic input (host, integer-only; identical bytes for GPU and CPU legs)
+
+def picture_bytes(width: int, height: int) -> int:
+    return width * height * 3 // 2
+
+
+def synth_frame(seed: int, frame: int, width: int, height: int) -> np.ndarray:
+    out = np.empty(picture_bytes(width, height), np.uint8)
+    lib().p64_synth_frame(seed, frame, width, height, out.ctypes.data)
+    return out
+
+
+def synth_motion(seed: int) -> tuple[int, int]:
+    x, y = ctypes.c_int(), ctypes.c_int()
+    lib().p64_synth_motion(seed, ctypes.byref(x), ctypes.byref(y))
+    return x.value, y.value
+
+
+# ---------------------------------------------------------------------------
+# device-tensor API (torch tensors on a HIP device)
+
+def synth_frames_device(width: int, height: int, seed0: int, nseeds: int, frame0: int,
+                        nslots: int, out=None):
+    """Device copy of synth_frame for nslots x nseeds pictures, slot-major:
+    out[t, s] = synth_frame(seed0 + s, frame0 + t)."""
+    torch = _torch()
+    pic = picture_bytes(width, height)
+    if out is None:
+        out = torch.empty((nslots, nseeds, pic), dtype=torch.uint8, device="cuda")
+    _dev_check(out, torch.uint8, "out")
+    if out.numel() < nslots * nseeds * pic:
+        raise P64GpuError("out too small")
+    _check(lib().p64gpu_synth_frames(width, height, seed0, nseeds, frame0, nslots, pic,
+                                     out.data_ptr(), _stream(torch)))
+    return out
+
+def _torch():
+    import torch
+    if not torch.cuda.is_available():
+        raise P64GpuError("no HIP device visible: the p64_amd hot path has no CPU fallback")
+    return torch
+
+
+def _stream(torch):
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def _dev_check(t, dtype, name):
+    torch = _torch()
+    if not isinstance(t, torch.Tensor) or not t.is_cuda:
+        raise P64GpuError(f"{name} must be a device tensor")
+    if t.dtype != dtype or not t.is_contiguous():
+        raise P64GpuError(f"{name} must be contiguous {dtype}")
+
+
+def block_op(op: int, blocks, dcq: int = 8, acq: int = 8, out=None):
+    """Run one reference block routine over a batch of int32 [..., 64] device blocks."""
+    torch = _torch()
+    _dev_check(blocks, torch.int32, "blocks")
+    if blocks.shape[-1] != 64:
+        raise P64GpuError("blocks must have a trailing dimension of 64")
+    if out is None:
+        out = torch.empty_like(blocks)
+    n = blocks.numel() // 64
+    _check(lib().p64gpu_block_op(op, blocks.data_ptr(), out.data_ptr(), n, dcq, acq, _stream(torch)))
+    return out
+
+
+def ChenDct(x):  # chendct.c:97
+    return block_op(OP_DCT, x)
+
+
+def ChenIDct(x):  # chendct.c:217
+    return block_op(OP_IDCT, x)
+
+
+def CCITTQuantize(m, dcq, acq):  # transform.c:271 (returns a new tensor)
+    return block_op(OP_QUANT_INTER, m, dcq, acq)
+
+
+def CCITTFlatQuantize(m, dcq, acq):  # transform.c:317
+    return block_op(OP_QUANT_INTRA, m, dcq, acq)
+
+
+def ICCITTQuantize(m, dcq, acq):  # transform.c:400
+    return block_op(OP_IQUANT_INTER, m, dcq, acq)
+
+
+def ICCITTFlatQuantize(m, dcq, acq):  # transform.c:359
+    return block_op(OP_IQUANT_INTRA, m, dcq, acq)
+
+
+def BoundDctMatrix(m):  # transform.c:460
+    return block_op(OP_BOUND_DCT, m)
+
+
+def BoundIDctMatrix(m):  # transform.c:483
+    return block_op(OP_BOUND_IDCT, m)
+
+
+def FlatBoundQuantizeMatrix(m):  # transform.c:502
+    return block_op(OP_BOUND_QFLAT, m)
+
+
+def BoundQuantizeMatrix(m):  # transform.c:526
+    return block_op(OP_BOUND_QUANT, m)
+
+
+def ZigzagMatrix(m):  # transform.c:561
+    return block_op(OP_ZIGZAG, m)
+
+
+def IZigzagMatrix(m):  # transform.c:546
+    return block_op(OP_IZIGZAG, m)
+
+
+def MotionEstimation(ref, cur, width: int, height: int, mode: int = ME_TSS,
+                     search_limit: int = 15, frame_stride: int | None = None):
+    """me.c:340 over a batch: ref/cur are uint8 device tensors holding nframes
+    pictures (or luma planes) `frame_stride` bytes apart.  Returns an int32
+    tensor [nframes, nmb, 7] = (MeX, MeY, MeVal, MeOVal, MeVAR, MeVAROR, MeMWOR)."""
+    torch = _torch()
+    _dev_check(ref, torch.uint8, "ref")
+    _dev_check(cur, torch.uint8, "cur")
+    stride = frame_stride or picture_bytes(width, height)
+    nframes = cur.numel() // stride
+    if nframes < 1 or ref.numel() < (nframes - 1) * stride + width * height:
+        raise P64GpuError("ref/cur hold fewer pictures than the geometry needs")
+    nmb = (width // 16) * (height // 16)
+    out = torch.empty((nframes, nmb, 7), dtype=torch.int32, device=cur.device)
+    _check(lib().p64gpu_motion_estimation(width, height, nframes, stride, ref.data_ptr(),
+                                          cur.data_ptr(), mode, search_limit, out.data_ptr(),
+                                          _stream(torch)))
+    return out
+
+
+@dataclass
+class FrameBatchOut:
+    coef: object        # int16 [nframes, nmb, 6, 64]
+    mb: object          # int8  [nframes, nmb, 4]  (mtype, cbp, mvx, mvy)
+    me: object          # int32 [nframes, nmb, 7] or None
+
+
+def encode_frames(cur, ref, recon, last_intra, *, width: int, height: int, intra: bool,
+                  quant: int = 8, me_mode: int = ME_TSS, search_limit: int = 15,
+                  quant_mb=None, mtype_override=None, out: FrameBatchOut | None = None,
+                  want_me: bool = True) -> FrameBatchOut:
+    """One picture of each of `nframes` independent sequences (p64.c:622-1013)."""
+    torch = _torch()
+    stride = picture_bytes(width, height)
+    nframes = cur.numel() // stride
+    nmb = (width // 16) * (height // 16)
+    dev = cur.device
+    _dev_check(cur, torch.uint8, "cur")
+    _dev_check(recon, torch.uint8, "recon")
+    _dev_check(last_intra, torch.uint8, "last_intra")
+    if not intra:
+        _dev_check(ref, torch.uint8, "ref")
+    need = nframes * stride
+    nmb_all = nframes * nmb
+    if nframes < 1 or recon.numel() < need or last_intra.numel() < nmb_all or \
+            (not intra and ref.numel() < need) or \
+            (quant_mb is not None and quant_mb.numel() < nmb_all) or \
+            (mtype_override is not None and mtype_override.numel() < nmb_all):
+        raise P64GpuError("buffer sizes do not match nframes x picture geometry")
+    if out is None:
+        out = FrameBatchOut(
+            coef=torch.empty((nframes, nmb, 6, 64), dtype=torch.int16, device=dev),
+            mb=torch.empty((nframes, nmb, 4), dtype=torch.int8, device=dev),
+            me=torch.empty((nframes, nmb, 7), dtype=torch.int32, device=dev) if want_me else None)
+    a = EncodeArgs(width=width, height=height, nframes=nframes, intra=int(bool(intra)),
+                   quant=quant, me_mode=me_mode, search_limit=search_limit, reserved=0,
+                   frame_stride=stride, cur=cur.data_ptr(),
+                   ref=(ref.data_ptr() if ref is not None else None), recon=recon.data_ptr(),
+                   last_intra=last_intra.data_ptr(),
+                   quant_mb=(quant_mb.data_ptr() if quant_mb is not None else None),
+                   mtype_override=(mtype_override.data_ptr() if mtype_override is not None else None),
+                   coef=out.coef.data_ptr(), mb=out.mb.data_ptr(),
+                   me=(out.me.data_ptr() if out.me is not None else None))
+    _check(lib().p64gpu_encode_frames(ctypes.byref(a), _stream(torch)))
+    return out
+
+
+def decode_recon(ref, recon, coef, mb, quant_mb, coded_mask, *, width: int, height: int):
+    """Decoder reconstruction (p64.c:1179-1237 + 971-1013) of coded MBs into recon."""
+    torch = _torch()
+    stride = picture_bytes(width, height)
+    nframes = recon.numel() // stride
+    nmb_all = nframes * (width // 16) * (height // 16)
+    if nframes < 1 or ref.numel() < nframes * stride or coef.numel() < nmb_all * 384 or \
+            mb.numel() < nmb_all * 4 or quant_mb.numel() < nmb_all or coded_mask.numel() < nmb_all:
+        raise P64GpuError("buffer sizes do not match nframes x picture geometry")
+    _check(lib().p64gpu_decode_recon(width, height, nframes, stride, ref.data_ptr(),
+                                     recon.data_ptr(), coef.data_ptr(), mb.data_ptr(),
+                                     quant_mb.data_ptr(), coded_mask.data_ptr(), _stream(torch)))
+    return recon
+
+
+class Encoder:
+    """Host-buffer closed-loop encoder (p64EncodeSequence/p64EncodeFrame,
+    p64.c:524-683) through the C ABI's p64gpu_encoder_* context: numpy in,
+    numpy out, reconstruction kept on the device between pictures."""
+
+    def __init__(self, width: int, height: int, me_mode: int = ME_TSS, search_limit: int = 15,
+                 device: int = 0):
+        self.width, self.height = width, height
+        self.nmb = (width // 16) * (height // 16)
+        self._h = ctypes.c_void_p()
+        _check(lib().p64gpu_encoder_open(device, width, height, me_mode, search_limit,
+                                         ctypes.byref(self._h)))
+
+    def frame(self, picture: np.ndarray, *, intra: bool, quant: int = 8, mtype_override=None,
+              want_recon: bool = False):
+        pic = np.ascontiguousarray(picture, dtype=np.uint8)
+        if pic.size != picture_bytes(self.width, self.height):
+            raise P64GpuError("picture has the wrong size")
+        coef = np.empty((self.nmb, 6, 64), np.int16)
+        mb = np.empty(self.nmb, MB_DTYPE)
+        me = np.zeros(self.nmb, ME_DTYPE)
+        recon = np.empty_like(pic) if want_recon else None
+        ov = None
+        if mtype_override is not None:
+            ov = np.ascontiguousarray(mtype_override, dtype=np.int8)
+        _check(lib().p64gpu_encoder_frame(self._h, pic.ctypes.data, int(bool(intra)), quant,
+                                          ov.ctypes.data if ov is not None else None,
+                                          coef.ctypes.data, mb.ctypes.data, me.ctypes.data,
+                                          recon.ctypes.data if recon is not None else None))
+        return coef, mb, me, recon
+
+    def close(self):
+        if self._h:
+            lib().p64gpu_encoder_close(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -1,0 +1,1158 @@
+// p64gpu.hip -- MI355X (gfx950) kernels and C ABI for the PVRG-P64 macroblock
+// encode hot path.  See include/p64gpu.h for the interface and DESIGN.md for
+// the data layout and rooflines.
+//
+// Execution model: one 64-lane wavefront (one workgroup) per macroblock.
+//   * the 16x16 current luma block and a 46x48-byte window of the previous
+//     reconstruction around it are staged in LDS with 16-byte loads;
+//   * FULL search: lane = (dx, dy-half); each lane slides its column of the
+//     window past the 16 current rows (held in SGPRs) with v_sad_u8, keeping 15
+//     SAD accumulators; the argmin is one wave-wide min over packed
+//     (SAD, scan-order) keys, reproducing FastBME's first-minimum rule;
+//   * TSS: lane = (candidate, row pair); four dependent steps of 8 candidates;
+//   * encode: lane = (block, row) for 6 blocks; the Chen DCT/IDCT row and
+//     column passes exchange through LDS; quantisation, zigzag, CBP and the
+//     reconstruction are fused into the same wave.
+// All arithmetic is integer except the MTYPE decision, which is evaluated in
+// IEEE binary64 exactly as p64.c:745-756 writes it.
+
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+
+#include "../../include/p64gpu.h"
+
+#define SYNTH_FN __host__ __device__ static inline
+#include "synth_impl.h"
+
+namespace {
+
+// ---------------------------------------------------------------------------
+// error reporting
+
+thread_local char g_err[512];
+
+int fail(int status, const char *fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof g_err, fmt, ap);
+  va_end(ap);
+  return status;
+}
+
+#define HIP_TRY(expr)                                                        \
+  do {                                                                       \
+    hipError_t e_ = (expr);                                                  \
+    if (e_ != hipSuccess)                                                    \
+      return fail(P64GPU_E_HIP, "%s: %s", #expr, hipGetErrorString(e_));     \
+  } while (0)
+
+// ---------------------------------------------------------------------------
+// coding-control tables (p64.c:217-222) as predicates on MTYPE 0..9
+
+__host__ __device__ constexpr bool mt_intra(int m) { return m < 2; }
+__host__ __device__ constexpr bool mt_cbp(int m) {
+  return m == 2 || m == 3 || m == 5 || m == 6 || m == 8 || m == 9;
+}
+__host__ __device__ constexpr bool mt_mf(int m) { return m >= 4; }
+__host__ __device__ constexpr bool mt_filter(int m) { return m >= 7; }
+__host__ __device__ constexpr bool mt_tcoeff(int m) { return m != 4 && m != 7; }
+
+// zigzag scan position of natural index n (transform.c:67-75), generated
+struct ZigZag {
+  uint8_t pos[64];
+};
+constexpr ZigZag make_zigzag() {
+  ZigZag z{};
+  int k = 0;
+  for (int s = 0; s < 15; s++) {
+    int lo = s < 8 ? 0 : s - 7, hi = s < 8 ? s : 7;
+    if (s & 1)
+      for (int r = lo; r <= hi; r++) z.pos[8 * r + s - r] = (uint8_t)k++;
+    else
+      for (int r = hi; r >= lo; r--) z.pos[8 * r + s - r] = (uint8_t)k++;
+  }
+  return z;
+}
+__constant__ ZigZag c_zz = make_zigzag();
+
+// ---------------------------------------------------------------------------
+// Chen integer DCT kernels of one 8-point line (chendct.c:97-375)
+
+constexpr int C1D4 = 362, C1D8 = 473, C3D8 = 196, C1D16 = 502, C3D16 = 426,
+              C5D16 = 284, C7D16 = 100;
+
+__device__ __forceinline__ int ms9(int v) { return v >> 9; }  // MSCALE, arithmetic
+
+// forward butterfly on scaled sums s[k] and differences d[k] (chendct.c:135-159)
+__device__ __forceinline__ void fwd8(const int s[4], const int d[4], int o[8]) {
+  const int e0 = s[0] + s[3], e1 = s[1] + s[2], e2 = s[1] - s[2], e3 = s[0] - s[3];
+  o[0] = ms9(C1D4 * (e0 + e1));
+  o[4] = ms9(C1D4 * (e0 - e1));
+  o[2] = ms9(C3D8 * e2 + C1D8 * e3);
+  o[6] = ms9(C3D8 * e3 - C1D8 * e2);
+  const int r0 = ms9(C1D4 * (d[1] - d[2])), r1 = ms9(C1D4 * (d[1] + d[2]));
+  const int u0 = d[3] + r0, u1 = d[3] - r0, u2 = d[0] - r1, u3 = d[0] + r1;
+  o[1] = ms9(C7D16 * u0 + C1D16 * u3);
+  o[3] = ms9(C3D16 * u2 - C5D16 * u1);
+  o[5] = ms9(C3D16 * u1 + C5D16 * u2);
+  o[7] = ms9(C7D16 * u3 - C1D16 * u0);
+}
+
+// column pass: sums/differences scaled <<2 (chendct.c:120-133)
+__device__ __forceinline__ void fwd_col(const int x[8], int o[8]) {
+  int s[4], d[4];
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    s[k] = (x[k] + x[7 - k]) << 2;
+    d[k] = (x[k] - x[7 - k]) << 2;
+  }
+  fwd8(s, d, o);
+}
+// row pass: sums/differences >>1 (chendct.c:167-174)
+__device__ __forceinline__ void fwd_row(const int x[8], int o[8]) {
+  int s[4], d[4];
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    s[k] = (x[k] + x[7 - k]) >> 1;
+    d[k] = (x[k] - x[7 - k]) >> 1;
+  }
+  fwd8(s, d, o);
+}
+
+// inverse butterfly (chendct.c:254-303 == 320-365)
+__device__ __forceinline__ void inv8(const int x[8], int o[8]) {
+  const int p0 = ms9(C7D16 * x[1] - C1D16 * x[7]);
+  const int p1 = ms9(C3D16 * x[5] - C5D16 * x[3]);
+  const int p2 = ms9(C3D16 * x[3] + C5D16 * x[5]);
+  const int p3 = ms9(C1D16 * x[1] + C7D16 * x[7]);
+  const int q0 = ms9(C1D4 * (x[0] + x[4])), q1 = ms9(C1D4 * (x[0] - x[4]));
+  const int q2 = ms9(C3D8 * x[2] - C1D8 * x[6]), q3 = ms9(C1D8 * x[2] + C3D8 * x[6]);
+  const int e0 = q0 + q3, e1 = q1 + q2, e2 = q1 - q2, e3 = q0 - q3;
+  const int f0 = p0 + p1, f1 = p0 - p1, f2 = p3 - p2, f3 = p3 + p2;
+  const int g1 = ms9(C1D4 * (f2 - f1)), g2 = ms9(C1D4 * (f2 + f1));
+  o[0] = e0 + f3;
+  o[1] = e1 + g2;
+  o[2] = e2 + g1;
+  o[3] = e3 + f0;
+  o[4] = e3 - f0;
+  o[5] = e2 - g1;
+  o[6] = e1 - g2;
+  o[7] = e0 - f3;
+}
+
+__device__ __forceinline__ int dct_final(int v) { return (v < 0 ? v - 4 : v + 4) / 8; }
+__device__ __forceinline__ int idct_final(int v) { return (v < 0 ? v - 8 : v + 8) / 16; }
+__device__ __forceinline__ int clampi(int v, int lo, int hi) { return min(max(v, lo), hi); }
+
+// ---------------------------------------------------------------------------
+// quantisers (transform.c:271-451, non-VERSION_1_0)
+
+// Truncating c / d for d = 2q.  In the fused kernel |c| <= 2048 (BoundDctMatrix
+// plus the +-1 of even q), where the 20-bit reciprocal is exact for every
+// d <= 62 (tests/test_quant_magic.py checks it exhaustively); the block-op path
+// handles arbitrary int32 with a true division.
+template <bool BOUNDED>
+__device__ __forceinline__ int div_trunc(int c, int d, unsigned magic) {
+  if (BOUNDED) {
+    const unsigned a = (unsigned)abs(c);
+    const int qq = (int)((a * magic) >> 20);
+    return c < 0 ? -qq : qq;
+  }
+  return c / d;
+}
+
+// H.261 level: odd q -> c/(2q); even q -> (c + sign(c))/(2q), sign(0) = -1
+// (transform.c:283-306, 339-347)
+template <bool BOUNDED>
+__device__ __forceinline__ int qlevel(int c, int q, unsigned magic) {
+  if (!(q & 1)) c += c > 0 ? 1 : -1;
+  return div_trunc<BOUNDED>(c, 2 * q, magic);
+}
+// intra DC (transform.c:321-325): (DC +- dcq/2) / dcq, sign by DC > 0
+__device__ __forceinline__ int qdc_intra(int c, int dcq) {
+  return c > 0 ? (c + dcq / 2) / dcq : (c - dcq / 2) / dcq;
+}
+// reconstruction level (transform.c:376-389, 436-448)
+__device__ __forceinline__ int rlevel(int l, int q) {
+  if (l == 0) return 0;
+  const int sg = l > 0 ? 1 : -1;
+  int v = (2 * l + sg) * q;
+  if (!(q & 1)) v -= sg;
+  return v;
+}
+
+__host__ __device__ constexpr unsigned quant_magic(int q) { return (1u << 20) / (2u * (unsigned)q) + 1u; }
+
+// ---------------------------------------------------------------------------
+// wave helpers
+
+__device__ __forceinline__ unsigned wave_min(unsigned v) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) v = min(v, (unsigned)__shfl_xor((int)v, m));
+  return v;
+}
+__device__ __forceinline__ int wave_sum(int v) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m);
+  return v;
+}
+__device__ __forceinline__ uint32_t sad4(uint32_t a, uint32_t b, uint32_t acc) {
+  return __builtin_amdgcn_sad_u8(a, b, acc);
+}
+__device__ __forceinline__ uint32_t align4(uint32_t hi, uint32_t lo, int shift) {
+  return __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)shift);
+}
+
+// ---------------------------------------------------------------------------
+// per-macroblock LDS image
+
+constexpr int WIN_ROWS = 46;   // y0-15 .. y0+30 (TSS reaches dy=+15)
+constexpr int WIN_BYTES = 48;  // x0-16 .. x0+31 (16-byte aligned loads)
+constexpr int WIN_WORDS = WIN_BYTES / 4;
+constexpr int WIN_OY = 15, WIN_OX = 16;  // window coordinates of (x0, y0)
+constexpr int BLK_STRIDE = 72, ROW_STRIDE = 9;  // padded DCT scratch
+
+struct __align__(16) MbLds {
+  uint32_t win[WIN_ROWS * WIN_WORDS];  // previous reconstruction, luma
+  uint32_t cur[64];                    // current 16x16 luma
+  int blk[6 * BLK_STRIDE];             // row/column exchange for DCT/IDCT
+  int16_t zz[6 * 64];                  // zigzagged levels for the store
+};
+
+struct Picture {  // one planar 4:2:0 picture
+  const uint8_t *y, *u, *v;
+};
+__device__ __forceinline__ Picture picture_at(const uint8_t *base, int w, int h) {
+  Picture p;
+  p.y = base;
+  p.u = base + (size_t)w * h;
+  p.v = p.u + (size_t)(w / 2) * (h / 2);
+  return p;
+}
+
+// stage the search window (zero outside the picture: such candidates are
+// never valid, me.c:212/292) and the current luma block
+__device__ __forceinline__ void stage_luma(MbLds &L, const uint8_t *ref_y, const uint8_t *cur_y,
+                                           int w, int h, int x0, int y0, int lane) {
+  for (int t = lane; t < WIN_ROWS * 3; t += 64) {
+    const int row = t / 3, seg = t - row * 3;
+    const int gy = y0 - WIN_OY + row, gx = x0 - WIN_OX + seg * 16;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (gy >= 0 && gy < h && gx >= 0 && gx < w)
+      v = *reinterpret_cast<const uint4 *>(ref_y + (size_t)gy * w + gx);
+    reinterpret_cast<uint4 *>(L.win)[t] = v;
+  }
+  L.cur[lane] = *reinterpret_cast<const uint32_t *>(cur_y + (size_t)(y0 + (lane >> 2)) * w + x0 +
+                                                    4 * (lane & 3));
+}
+
+struct MeOut {
+  int mx, my, sad, sad0, var, varor, mwor;
+};
+
+// SAD of the zero vector (OMV, me.c:203/271): one dword per lane
+__device__ __forceinline__ int sad_zero(const MbLds &L, int lane) {
+  const uint32_t r = L.win[(WIN_OY + (lane >> 2)) * WIN_WORDS + WIN_OX / 4 + (lane & 3)];
+  return wave_sum((int)sad4(r, L.cur[lane], 0));
+}
+
+// FastBME (me.c:187-227) over [-sl/2, sl/2)^2.  Returns the packed winner key.
+__device__ __forceinline__ void me_full(const MbLds &L, int w, int h, int x0, int y0, int sl,
+                                        int lane, int sad0, int &mx, int &my, int &best) {
+  const int half = lane >> 5, dxi = lane & 31;
+  const bool lane_ok = dxi < 30;
+  const int colb = (lane_ok ? dxi : 29) + 1;  // window byte column of dx = dxi-15
+  const int w0 = colb >> 2, sh = colb & 3;
+
+  uint32_t cs[64];  // current block, wave-uniform -> SGPR operands of v_sad_u8
+#pragma unroll
+  for (int k = 0; k < 64; k++) cs[k] = __builtin_amdgcn_readfirstlane(L.cur[k]);
+
+  uint32_t acc[15];
+#pragma unroll
+  for (int d = 0; d < 15; d++) acc[d] = 0;
+
+  const uint32_t *wrow = L.win + (15 * half) * WIN_WORDS + w0;
+#pragma unroll
+  for (int i = 0; i < 30; i++) {  // window row of this lane's dy-half
+    const uint32_t *p = wrow + i * WIN_WORDS;
+    const uint32_t a0 = p[0], a1 = p[1], a2 = p[2], a3 = p[3], a4 = p[4];
+    const uint32_t r0 = align4(a1, a0, sh), r1 = align4(a2, a1, sh);
+    const uint32_t r2 = align4(a3, a2, sh), r3 = align4(a4, a3, sh);
+#pragma unroll
+    for (int r = 0; r < 16; r++) {  // current row r meets candidate dy-index d = i - r
+      const int d = i - r;
+      if (d >= 0 && d < 15) {
+        uint32_t a = acc[d];
+        a = sad4(r0, cs[4 * r + 0], a);
+        a = sad4(r1, cs[4 * r + 1], a);
+        a = sad4(r2, cs[4 * r + 2], a);
+        a = sad4(r3, cs[4 * r + 3], a);
+        acc[d] = a;
+      }
+    }
+  }
+
+  // key = SAD<<11 | (1 + scan order); scan order (dx+15)*30+(dy+15) is
+  // FastBME's dx-major order; key 0-order (0) is reserved for the (0,0) vector,
+  // which wins every tie because it is evaluated first (me.c:203, 220).
+  const int hl = sl >> 1;
+  const int dx = dxi - 15, px = x0 + dx;
+  const bool col_ok = lane_ok && dx >= -hl && dx < hl && px >= 0 && px < w - 16;
+  unsigned bk = 0xFFFFFFFFu;
+#pragma unroll
+  for (int d = 0; d < 15; d++) {
+    const int dy = -15 + 15 * half + d, py = y0 + dy;
+    const bool ok = col_ok && dy >= -hl && dy < hl && py >= 0 && py < h - 16;
+    const unsigned key = (acc[d] << 11) | (unsigned)(dxi * 30 + 15 * half + d + 1);
+    if (ok && key < bk) bk = key;
+  }
+  bk = min(wave_min(bk), (unsigned)sad0 << 11);
+  const int ord = (int)(bk & 2047u);
+  best = (int)(bk >> 11);
+  if (ord == 0) {
+    mx = my = 0;
+  } else {
+    mx = (ord - 1) / 30 - 15;
+    my = (ord - 1) % 30 - 15;
+  }
+}
+
+// StepBME (me.c:255-311): steps 8,4,2,1, 8 neighbours each in (diry, dirx)
+// raster order, strict '<' against the running best.
+__device__ __forceinline__ void me_tss(const MbLds &L, int w, int h, int x0, int y0, int lane,
+                                       int sad0, int &mx, int &my, int &best) {
+  const int k = lane >> 3, rg = lane & 7;
+  const int kk = k < 4 ? k : k + 1;  // skip the centre of the 3x3
+  const int dirx = kk % 3 - 1, diry = kk / 3 - 1;
+  uint32_t c[8];
+#pragma unroll
+  for (int j = 0; j < 8; j++) c[j] = L.cur[8 * rg + j];  // rows 2rg, 2rg+1
+  int bx = 0, by = 0;
+  unsigned bsad = (unsigned)sad0;
+#pragma unroll
+  for (int step = 8; step >= 1; step >>= 1) {
+    const int dx = bx + dirx * step, dy = by + diry * step;
+    const int px = x0 + dx, py = y0 + dy;
+    const bool ok = px >= 0 && px < w - 16 && py >= 0 && py < h - 16 && dx >= -15 &&
+                    dx <= 15 && dy >= -15 && dy <= 15;
+    uint32_t s = 0;
+    if (ok) {
+      const int colb = WIN_OX + dx, sh = colb & 3;
+      const uint32_t *p = L.win + (WIN_OY + dy + 2 * rg) * WIN_WORDS + (colb >> 2);
+#pragma unroll
+      for (int rr = 0; rr < 2; rr++) {
+        const uint32_t *q = p + rr * WIN_WORDS;
+        const uint32_t a0 = q[0], a1 = q[1], a2 = q[2], a3 = q[3], a4 = q[4];
+        s = sad4(align4(a1, a0, sh), c[4 * rr + 0], s);
+        s = sad4(align4(a2, a1, sh), c[4 * rr + 1], s);
+        s = sad4(align4(a3, a2, sh), c[4 * rr + 2], s);
+        s = sad4(align4(a4, a3, sh), c[4 * rr + 3], s);
+      }
+    }
+    s += (uint32_t)__shfl_xor((int)s, 1);
+    s += (uint32_t)__shfl_xor((int)s, 2);
+    s += (uint32_t)__shfl_xor((int)s, 4);
+    const uint64_t okmask = __ballot(ok);
+    int nbx = bx, nby = by;
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      const unsigned sj = (unsigned)__shfl((int)s, 8 * j);
+      const int jj = j < 4 ? j : j + 1;
+      if (((okmask >> (8 * j)) & 1) && sj < bsad) {
+        bsad = sj;
+        nbx = bx + (jj % 3 - 1) * step;
+        nby = by + (jj / 3 - 1) * step;
+      }
+    }
+    bx = nbx;
+    by = nby;
+  }
+  mx = bx;
+  my = by;
+  best = (int)bsad;
+}
+
+// decision statistics on the chosen block (me.c:229-245 == 313-329)
+__device__ __forceinline__ void me_stats(const MbLds &L, int lane, MeOut &o) {
+  const int colb = WIN_OX + o.mx + 4 * (lane & 3);
+  const uint32_t *p = L.win + (WIN_OY + o.my + (lane >> 2)) * WIN_WORDS + (colb >> 2);
+  const uint32_t rw = align4(p[1], p[0], colb & 3), cw = L.cur[lane];
+  int var = 0, sq = 0, sum = 0;
+#pragma unroll
+  for (int j = 0; j < 4; j++) {
+    const int rb = (rw >> (8 * j)) & 255, cb = (cw >> (8 * j)) & 255, d = rb - cb;
+    var += d * d;
+    sq += rb * rb;
+    sum += rb;
+  }
+  var = wave_sum(var);
+  sq = wave_sum(sq);
+  sum = wave_sum(sum);
+  o.var = var / 256;
+  o.varor = sq / 256 - (sum / 256) * (sum / 256);
+  o.mwor = sum;
+}
+
+template <int MODE>  // 1 = TSS, 2 = FULL
+__device__ __forceinline__ MeOut motion_estimate(MbLds &L, int w, int h, int x0, int y0, int sl,
+                                                 int lane) {
+  MeOut o;
+  o.sad0 = sad_zero(L, lane);
+  if (MODE == 2)
+    me_full(L, w, h, x0, y0, sl, lane, o.sad0, o.mx, o.my, o.sad);
+  else
+    me_tss(L, w, h, x0, y0, lane, o.sad0, o.mx, o.my, o.sad);
+  me_stats(L, lane, o);
+  return o;
+}
+
+// MTYPE decision (p64.c:734-756) in binary64, as written.
+__device__ __forceinline__ int decide_mtype(const MeOut &m) {
+  double xv = (double)m.sad0, yv = (double)m.sad;
+  xv = xv / 256;
+  yv = yv / 256;
+  if (m.var < 64 || m.varor > m.var) {
+    if (xv < 1.0 || (xv < 3.0 && yv > xv * 0.5) || yv > xv / 1.1) return 2;
+    if (m.var < 6.0) return 5;
+    return 8;
+  }
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
+// prediction of row r of block b (io.c:142-496).  SRC(rr, k) returns the
+// reference byte at row rr, column k relative to the block's compensated origin.
+
+template <typename Src>
+__device__ __forceinline__ void pred_row(Src src, bool filter, int r, int p[8]) {
+  if (!filter) {
+#pragma unroll
+    for (int k = 0; k < 8; k++) p[k] = src(r, k);
+    return;
+  }
+  // LoadFilterMatrix (io.c:323-372)
+  int hz[3][8];
+#pragma unroll
+  for (int t = 0; t < 3; t++) {
+    const int rr = min(max(r - 1 + t, 0), 7);
+    int s[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) s[k] = src(rr, k);
+    hz[t][0] = s[0] << 2;
+#pragma unroll
+    for (int k = 1; k < 7; k++) hz[t][k] = s[k - 1] + 2 * s[k] + s[k + 1];
+    hz[t][7] = s[7] << 2;
+  }
+  const bool edge = r == 0 || r == 7;
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    const int v = edge ? hz[1][k] : (hz[0][k] + 2 * hz[1][k] + hz[2][k]) >> 2;
+    p[k] = (v & 2) ? (v >> 2) + 1 : (v >> 2);
+  }
+}
+
+// compensated origin of block b for MTYPE mt (MoveTo io.c:719-747; luma MV,
+// chroma MV/2 with C truncation io.c:268-270; zero vector for non-MC types)
+struct BlockGeom {
+  int plane;  // 0 Y, 1 U, 2 V
+  int x, y;   // block origin in its plane
+};
+__device__ __forceinline__ BlockGeom block_geom(int b, int mbx, int mby) {
+  BlockGeom g;
+  if (b < 4) {
+    g.plane = 0;
+    g.x = 16 * mbx + 8 * (b & 1);
+    g.y = 16 * mby + 8 * (b >> 1);
+  } else {
+    g.plane = b - 3;
+    g.x = 8 * mbx;
+    g.y = 8 * mby;
+  }
+  return g;
+}
+
+__device__ __forceinline__ void read_row8(const uint8_t *p, int v[8]) {
+  const uint2 q = *reinterpret_cast<const uint2 *>(p);
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    v[k] = (q.x >> (8 * k)) & 255;
+    v[4 + k] = (q.y >> (8 * k)) & 255;
+  }
+}
+__device__ __forceinline__ void write_row8(uint8_t *p, const int v[8]) {
+  uint2 q;
+  q.x = (uint32_t)v[0] | ((uint32_t)v[1] << 8) | ((uint32_t)v[2] << 16) | ((uint32_t)v[3] << 24);
+  q.y = (uint32_t)v[4] | ((uint32_t)v[5] << 8) | ((uint32_t)v[6] << 16) | ((uint32_t)v[7] << 24);
+  *reinterpret_cast<uint2 *>(p) = q;
+}
+
+// Prediction from LDS (luma) / global (chroma) for the encoder.
+__device__ __forceinline__ void predict_enc(const MbLds &L, const Picture &ref, int w, int b,
+                                            int mbx, int mby, int r, int mt, int mvx, int mvy,
+                                            int p[8]) {
+  const bool mf = mt_mf(mt), filt = mt_filter(mt);
+  if (b < 4) {
+    const uint8_t *wb = reinterpret_cast<const uint8_t *>(L.win);
+    const int ox = WIN_OX + 8 * (b & 1) + (mf ? mvx : 0);
+    const int oy = WIN_OY + 8 * (b >> 1) + (mf ? mvy : 0);
+    pred_row([&](int rr, int k) { return (int)wb[(oy + rr) * WIN_BYTES + ox + k]; }, filt, r, p);
+  } else {
+    const int cw = w / 2;
+    const uint8_t *pl = b == 4 ? ref.u : ref.v;
+    const int ox = 8 * mbx + (mf ? mvx / 2 : 0), oy = 8 * mby + (mf ? mvy / 2 : 0);
+    const uint8_t *base = pl + (size_t)oy * cw + ox;
+    pred_row([&](int rr, int k) { return (int)base[(size_t)rr * cw + k]; }, filt, r, p);
+  }
+}
+
+// Prediction straight from global memory (decoder recon).
+__device__ __forceinline__ void predict_glb(const Picture &ref, int w, int b, int mbx, int mby,
+                                            int r, int mt, int mvx, int mvy, int p[8]) {
+  const bool mf = mt_mf(mt), filt = mt_filter(mt);
+  const BlockGeom g = block_geom(b, mbx, mby);
+  const int pw = g.plane ? w / 2 : w;
+  const uint8_t *pl = g.plane == 0 ? ref.y : (g.plane == 1 ? ref.u : ref.v);
+  const int dx = mf ? (g.plane ? mvx / 2 : mvx) : 0, dy = mf ? (g.plane ? mvy / 2 : mvy) : 0;
+  const uint8_t *base = pl + (size_t)(g.y + dy) * pw + g.x + dx;
+  pred_row([&](int rr, int k) { return (int)base[(size_t)rr * pw + k]; }, filt, r, p);
+}
+
+// ---------------------------------------------------------------------------
+// forward transform + quantisation of row r of block b (lanes 0..47 active)
+
+__device__ __forceinline__ void dct_quant_rows(MbLds &L, bool act, int b, int r, const int res[8],
+                                               bool intra, int q, unsigned magic, int lev[8]) {
+  int *B = L.blk + b * BLK_STRIDE;
+  if (act) {
+#pragma unroll
+    for (int k = 0; k < 8; k++) B[r * ROW_STRIDE + k] = res[k];
+  }
+  __syncthreads();
+  if (act) {  // column pass, lane owns column c = r
+    int x[8], o[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) x[k] = B[k * ROW_STRIDE + r];
+    fwd_col(x, o);
+#pragma unroll
+    for (int k = 0; k < 8; k++) B[k * ROW_STRIDE + r] = o[k];
+  }
+  __syncthreads();
+  int x[8], o[8];
+#pragma unroll
+  for (int k = 0; k < 8; k++) x[k] = act ? B[r * ROW_STRIDE + k] : 0;
+  fwd_row(x, o);
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    int v = dct_final(o[k]);
+    const bool dc = (r == 0 && k == 0);
+    v = dc ? min(v, 2047) : clampi(v, -1023, 1023);  // BoundDctMatrix
+    if (intra) {
+      v = dc ? clampi(qdc_intra(v, 8), 1, 254) : clampi(qlevel<true>(v, q, magic), -127, 127);
+    } else {
+      v = clampi(qlevel<true>(v, q, magic), -127, 127);
+    }
+    lev[k] = act ? v : 0;
+  }
+}
+
+// dequantisation + inverse transform of row r of block b -> residual res[8]
+__device__ __forceinline__ void iq_idct_rows(MbLds &L, bool act, bool coded, int b, int r,
+                                             const int lev[8], bool intra, int q, int res[8]) {
+  int *B = L.blk + b * BLK_STRIDE;
+  __syncthreads();  // previous users of blk are done
+  if (act) {
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      const bool dc = (r == 0 && k == 0);
+      B[r * ROW_STRIDE + k] = (intra && dc) ? lev[k] * 8 : rlevel(lev[k], q);
+    }
+  }
+  __syncthreads();
+  if (act) {  // column pass: inputs <<2
+    int x[8], o[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) x[k] = B[k * ROW_STRIDE + r] << 2;
+    inv8(x, o);
+#pragma unroll
+    for (int k = 0; k < 8; k++) B[k * ROW_STRIDE + r] = o[k];
+  }
+  __syncthreads();
+  int x[8], o[8];
+#pragma unroll
+  for (int k = 0; k < 8; k++) x[k] = act ? B[r * ROW_STRIDE + k] : 0;
+  inv8(x, o);
+#pragma unroll
+  for (int k = 0; k < 8; k++) res[k] = (act && coded) ? idct_final(o[k]) : 0;
+}
+
+// ---------------------------------------------------------------------------
+// the fused encode kernel: ME -> decision -> prediction -> DCT -> quant ->
+// zigzag -> CBP -> IQ -> IDCT -> reconstruction, one wave per macroblock.
+// MODE: 0 intra picture, 1 TSS, 2 FULL.
+
+template <int MODE>
+__global__ __launch_bounds__(64) void k_encode(p64gpu_encode_args a) {
+  __shared__ MbLds L;
+  const int lane = threadIdx.x;
+  const int w = a.width, h = a.height, mbw = w >> 4, nmb = mbw * (h >> 4);
+  const int fi = blockIdx.x / nmb, mb = blockIdx.x - fi * nmb;
+  const int mbx = mb % mbw, mby = mb / mbw, x0 = 16 * mbx, y0 = 16 * mby;
+  const size_t gmb = (size_t)fi * nmb + mb;
+  const Picture cur = picture_at(a.cur + (size_t)fi * a.frame_stride, w, h);
+  const Picture ref = picture_at(a.ref + (size_t)fi * a.frame_stride, w, h);
+  uint8_t *rec = a.recon + (size_t)fi * a.frame_stride;
+
+  int mt = 0, mvx = 0, mvy = 0;
+  if (MODE != 0) {
+    stage_luma(L, ref.y, cur.y, w, h, x0, y0, lane);
+    __syncthreads();
+    const MeOut me = motion_estimate<MODE>(L, w, h, x0, y0, a.search_limit, lane);
+    if (a.me && lane == 0) {
+      p64_me_rec r;
+      r.mx = me.mx;
+      r.my = me.my;
+      r.sad = me.sad;
+      r.sad0 = me.sad0;
+      r.var = me.var;
+      r.varor = me.varor;
+      r.mwor = me.mwor;
+      a.me[gmb] = r;
+    }
+    mt = decide_mtype(me);
+    if (a.mtype_override) {
+      const int ov = a.mtype_override[gmb];
+      if (ov >= 0) mt = ov;
+    }
+    mvx = me.mx;
+    mvy = me.my;
+  }
+  const uint8_t li = a.last_intra[gmb];
+  if (li > 131) mt = 0;  // SEQUENCE_INTRA_THRESHOLD (p64.c:159, 772)
+  const int q = a.quant_mb ? a.quant_mb[gmb] : a.quant;
+  const unsigned magic = quant_magic(q);
+
+  const int b = lane >> 3, r = lane & 7;
+  const bool act = b < 6;
+  const BlockGeom g = block_geom(act ? b : 0, mbx, mby);
+  const int pw = g.plane ? w / 2 : w;
+
+  int pred[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (!mt_intra(mt) && act) predict_enc(L, ref, w, b, mbx, mby, r, mt, mvx, mvy, pred);
+
+  // ReadCompressMDU (p64.c:830-912)
+  int lev[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const bool intra = mt_intra(mt);
+  if (mt_tcoeff(mt)) {
+    int res[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (act) {
+      const uint8_t *pl = g.plane == 0 ? cur.y : (g.plane == 1 ? cur.u : cur.v);
+      read_row8(pl + (size_t)(g.y + r) * pw + g.x, res);
+      if (!intra) {
+#pragma unroll
+        for (int k = 0; k < 8; k++) res[k] -= pred[k];
+      }
+    }
+    dct_quant_rows(L, act, b, r, res, intra, q, magic, lev);
+  }
+  int cbp = 0x3f;
+  if (mt_cbp(mt)) {
+    int acc = 0;
+#pragma unroll
+    for (int k = 0; k < 8; k++) acc += abs(lev[k]);
+    acc += __shfl_xor(acc, 1);
+    acc += __shfl_xor(acc, 2);
+    acc += __shfl_xor(acc, 4);
+    int pmask = 0;
+    cbp = 0;
+#pragma unroll
+    for (int c = 0; c < 6; c++) {
+      const int s = __shfl(acc, 8 * c);
+      if (s && !pmask) pmask = 1 << (5 - c);
+      if (s > 1) cbp |= 1 << (5 - c);  // CBPThreshold = 1 (p64.c:151)
+    }
+    if (!cbp) {
+      if (pmask) {
+        cbp = pmask;
+      } else {  // no coefficients: MC without coefficients, ME vector kept
+        const int old = mt;
+        mt = mt_filter(mt) ? 7 : 4;
+        cbp = 0x3f;
+#pragma unroll
+        for (int k = 0; k < 8; k++) lev[k] = 0;
+        if (!mt_mf(old) && act) predict_enc(L, ref, w, b, mbx, mby, r, mt, mvx, mvy, pred);
+      }
+    }
+  }
+
+  // levels -> LDS in zigzag order -> global (768 B per MB)
+  if (act) {
+#pragma unroll
+    for (int k = 0; k < 8; k++) L.zz[b * 64 + c_zz.pos[r * 8 + k]] = (int16_t)lev[k];
+  }
+  __syncthreads();
+  if (lane < 48)
+    reinterpret_cast<uint4 *>(a.coef + gmb * 384)[lane] = reinterpret_cast<const uint4 *>(L.zz)[lane];
+
+  // reconstruction (p64.c:945-959, 971-1013)
+  const bool coded = act && ((cbp >> (5 - b)) & 1) && mt_tcoeff(mt);
+  int res[8];
+  iq_idct_rows(L, act, coded, b, r, lev, mt_intra(mt), q, res);
+  if (act) {
+    const bool add = !mt_intra(mt);
+#pragma unroll
+    for (int k = 0; k < 8; k++) res[k] = clampi(res[k] + (add ? pred[k] : 0), 0, 255);
+    uint8_t *pl = rec + (g.plane == 0 ? 0 : (size_t)w * h + (size_t)(g.plane - 1) * (w / 2) * (h / 2));
+    write_row8(pl + (size_t)(g.y + r) * pw + g.x, res);
+  }
+  if (lane == 0) {
+    p64_mb_rec o;
+    o.mtype = (int8_t)mt;
+    o.cbp = (int8_t)cbp;
+    o.mvx = (int8_t)(mt_mf(mt) ? mvx : 0);
+    o.mvy = (int8_t)(mt_mf(mt) ? mvy : 0);
+    a.mb[gmb] = o;
+    a.last_intra[gmb] = mt_intra(mt) ? 0 : (uint8_t)(li + 1);
+  }
+}
+
+// ME only (MotionEstimation me.c:340-363 over a batch of luma planes)
+template <int MODE>
+__global__ __launch_bounds__(64) void k_motion(int w, int h, int64_t stride, const uint8_t *ref_y,
+                                               const uint8_t *cur_y, int sl, p64_me_rec *out) {
+  __shared__ MbLds L;
+  const int lane = threadIdx.x;
+  const int mbw = w >> 4, nmb = mbw * (h >> 4);
+  const int fi = blockIdx.x / nmb, mb = blockIdx.x - fi * nmb;
+  const int x0 = 16 * (mb % mbw), y0 = 16 * (mb / mbw);
+  stage_luma(L, ref_y + (size_t)fi * stride, cur_y + (size_t)fi * stride, w, h, x0, y0, lane);
+  __syncthreads();
+  const MeOut me = motion_estimate<MODE>(L, w, h, x0, y0, sl, lane);
+  if (lane == 0) {
+    p64_me_rec r;
+    r.mx = me.mx;
+    r.my = me.my;
+    r.sad = me.sad;
+    r.sad0 = me.sad0;
+    r.var = me.var;
+    r.varor = me.varor;
+    r.mwor = me.mwor;
+    out[(size_t)fi * nmb + mb] = r;
+  }
+}
+
+// decoder-side reconstruction of coded macroblocks
+__global__ __launch_bounds__(64) void k_decode_recon(int w, int h, int64_t stride,
+                                                     const uint8_t *refp, uint8_t *recp,
+                                                     const int16_t *coef, const p64_mb_rec *mbr,
+                                                     const uint8_t *quant_mb,
+                                                     const uint8_t *coded_mask) {
+  __shared__ MbLds L;
+  const int lane = threadIdx.x;
+  const int mbw = w >> 4, nmb = mbw * (h >> 4);
+  const int fi = blockIdx.x / nmb, mb = blockIdx.x - fi * nmb;
+  const size_t gmb = (size_t)fi * nmb + mb;
+  if (!coded_mask[gmb]) return;  // whole workgroup exits together
+  const int mbx = mb % mbw, mby = mb / mbw;
+  const Picture ref = picture_at(refp + (size_t)fi * stride, w, h);
+  uint8_t *rec = recp + (size_t)fi * stride;
+  const p64_mb_rec m = mbr[gmb];
+  const int mt = m.mtype, q = quant_mb[gmb];
+  const int cbp = mt_cbp(mt) ? m.cbp : 0x3f;  // p64.c:1200
+  const int b = lane >> 3, r = lane & 7;
+  const bool act = b < 6;
+  const BlockGeom g = block_geom(act ? b : 0, mbx, mby);
+  const int pw = g.plane ? w / 2 : w;
+  int lev[8];
+#pragma unroll
+  for (int k = 0; k < 8; k++) lev[k] = act ? coef[gmb * 384 + b * 64 + c_zz.pos[r * 8 + k]] : 0;
+  const bool coded = act && ((cbp >> (5 - b)) & 1) && mt_tcoeff(mt);
+  int res[8];
+  iq_idct_rows(L, act, coded, b, r, lev, mt_intra(mt), q, res);
+  if (act) {
+    int pred[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (!mt_intra(mt)) predict_glb(ref, w, b, mbx, mby, r, mt, m.mvx, m.mvy, pred);
+#pragma unroll
+    for (int k = 0; k < 8; k++) res[k] = clampi(res[k] + pred[k], 0, 255);
+    uint8_t *pl = rec + (g.plane == 0 ? 0 : (size_t)w * h + (size_t)(g.plane - 1) * (w / 2) * (h / 2));
+    write_row8(pl + (size_t)(g.y + r) * pw + g.x, res);
+  }
+}
+
+// batched 8x8 block operations (one thread per block; shares the device
+// functions of the fused kernel)
+__global__ void k_block_op(int op, const int32_t *in, int32_t *out, int64_t nblocks, int dcq,
+                           int acq) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nblocks) return;
+  int m[64], t[64];
+  const int32_t *src = in + i * 64;
+  int32_t *dst = out + i * 64;
+  for (int n = 0; n < 64; n++) m[n] = src[n];
+  switch (op) {
+    case P64GPU_OP_DCT: {
+      int x[8], o[8];
+      for (int c = 0; c < 8; c++) {
+        for (int k = 0; k < 8; k++) x[k] = m[8 * k + c];
+        fwd_col(x, o);
+        for (int k = 0; k < 8; k++) t[8 * k + c] = o[k];
+      }
+      for (int rr = 0; rr < 8; rr++) {
+        for (int k = 0; k < 8; k++) x[k] = t[8 * rr + k];
+        fwd_row(x, o);
+        for (int k = 0; k < 8; k++) m[8 * rr + k] = dct_final(o[k]);
+      }
+      break;
+    }
+    case P64GPU_OP_IDCT: {
+      int x[8], o[8];
+      for (int c = 0; c < 8; c++) {
+        for (int k = 0; k < 8; k++) x[k] = m[8 * k + c] << 2;
+        inv8(x, o);
+        for (int k = 0; k < 8; k++) t[8 * k + c] = o[k];
+      }
+      for (int rr = 0; rr < 8; rr++) {
+        for (int k = 0; k < 8; k++) x[k] = t[8 * rr + k];
+        inv8(x, o);
+        for (int k = 0; k < 8; k++) m[8 * rr + k] = idct_final(o[k]);
+      }
+      break;
+    }
+    case P64GPU_OP_QUANT_INTRA:
+      m[0] = qdc_intra(m[0], dcq);
+      for (int n = 1; n < 64; n++) m[n] = qlevel<false>(m[n], acq, 0);
+      break;
+    case P64GPU_OP_QUANT_INTER:
+      m[0] = qlevel<false>(m[0], dcq, 0);
+      for (int n = 1; n < 64; n++) m[n] = qlevel<false>(m[n], acq, 0);
+      break;
+    case P64GPU_OP_IQUANT_INTRA:
+      m[0] = m[0] * dcq;
+      for (int n = 1; n < 64; n++) m[n] = rlevel(m[n], acq);
+      break;
+    case P64GPU_OP_IQUANT_INTER:
+      m[0] = rlevel(m[0], dcq);
+      for (int n = 1; n < 64; n++) m[n] = rlevel(m[n], acq);
+      break;
+    case P64GPU_OP_BOUND_DCT:
+      m[0] = min(m[0], 2047);
+      for (int n = 1; n < 64; n++) m[n] = clampi(m[n], -1023, 1023);
+      break;
+    case P64GPU_OP_BOUND_IDCT:
+      for (int n = 0; n < 64; n++) m[n] = clampi(m[n], 0, 255);
+      break;
+    case P64GPU_OP_BOUND_QFLAT:
+      m[0] = clampi(m[0], 1, 254);
+      for (int n = 1; n < 64; n++) m[n] = clampi(m[n], -127, 127);
+      break;
+    case P64GPU_OP_BOUND_QUANT:
+      for (int n = 0; n < 64; n++) m[n] = clampi(m[n], -127, 127);
+      break;
+    case P64GPU_OP_ZIGZAG:
+      for (int n = 0; n < 64; n++) t[c_zz.pos[n]] = m[n];
+      for (int n = 0; n < 64; n++) m[n] = t[n];
+      break;
+    case P64GPU_OP_IZIGZAG:
+      for (int n = 0; n < 64; n++) t[n] = m[c_zz.pos[n]];
+      for (int n = 0; n < 64; n++) m[n] = t[n];
+      break;
+    default:
+      break;
+  }
+  for (int n = 0; n < 64; n++) dst[n] = m[n];
+}
+
+// deterministic synthetic pictures on the device (same bytes as synth.c):
+// picture (t, s) = stream seed0+s, frame frame0+t, at out + (t*nseeds+s)*stride
+__global__ __launch_bounds__(256) void k_synth(int w, int h, uint32_t seed0, int nseeds,
+                                               int frame0, int64_t stride, uint8_t *out) {
+  const int pic = blockIdx.y;
+  const int t = pic / nseeds, sidx = pic - t * nseeds;
+  const uint32_t seed = seed0 + (uint32_t)sidx;
+  const int frame = frame0 + t;
+  uint8_t *y = out + (size_t)pic * stride;
+  uint8_t *u = y + (size_t)w * h, *v = u + (size_t)(w / 2) * (h / 2);
+  const int nl = w * h, nc = (w / 2) * (h / 2);
+  for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < nl + nc; k += gridDim.x * blockDim.x) {
+    if (k < nl) {
+      y[k] = p64s_luma(seed, frame, k % w, k / w);
+    } else {
+      const int c = k - nl;
+      p64s_chroma(seed, frame, c % (w / 2), c / (w / 2), &u[c], &v[c]);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// host-side validation
+
+int check_geometry(int w, int h, int nframes, int64_t stride, bool luma_only = false) {
+  if (w < 32 || h < 32 || w > 4096 || h > 4096 || (w & 15) || (h & 15))
+    return fail(P64GPU_E_INVALID, "picture %dx%d: need multiples of 16 in 32..4096", w, h);
+  if (nframes < 1) return fail(P64GPU_E_INVALID, "nframes %d < 1", nframes);
+  const int64_t need = luma_only ? (int64_t)w * h : (int64_t)w * h * 3 / 2;
+  if (stride < need || (stride & 15))
+    return fail(P64GPU_E_INVALID, "frame_stride %lld: need >= %lld and a multiple of 16",
+                (long long)stride, (long long)need);
+  const int64_t blocks = (int64_t)nframes * (w / 16) * (h / 16);
+  if (blocks > 0x7fffffffLL) return fail(P64GPU_E_INVALID, "too many macroblocks in one call");
+  return P64GPU_OK;
+}
+
+bool aligned16(const void *p) { return ((uintptr_t)p & 15) == 0; }
+
+}  // namespace
+
+// ===========================================================================
+// C ABI
+
+extern "C" {
+
+int p64gpu_abi_version(void) { return P64GPU_ABI_VERSION; }
+
+const char *p64gpu_strerror(int s) {
+  switch (s) {
+    case P64GPU_OK: return "ok";
+    case P64GPU_E_INVALID: return "invalid argument";
+    case P64GPU_E_NODEVICE: return "no HIP device";
+    case P64GPU_E_HIP: return "HIP runtime error";
+    case P64GPU_E_NOMEM: return "out of memory";
+    default: return "unknown status";
+  }
+}
+
+const char *p64gpu_last_error(void) { return g_err; }
+
+int p64gpu_device_count(int *count) {
+  if (!count) return fail(P64GPU_E_INVALID, "count is NULL");
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+  *count = n;
+  return P64GPU_OK;
+}
+
+int p64gpu_set_device(int device) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n == 0)
+    return fail(P64GPU_E_NODEVICE, "no HIP device visible");
+  if (device < 0 || device >= n) return fail(P64GPU_E_INVALID, "device %d of %d", device, n);
+  HIP_TRY(hipSetDevice(device));
+  return P64GPU_OK;
+}
+
+int p64gpu_synchronize(void *stream) {
+  HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
+  return P64GPU_OK;
+}
+
+int p64gpu_block_op(int op, const int32_t *in, int32_t *out, int64_t nblocks, int dcq, int acq,
+                    void *stream) {
+  if (op < 0 || op >= P64GPU_OP_COUNT) return fail(P64GPU_E_INVALID, "block op %d", op);
+  if (nblocks < 0) return fail(P64GPU_E_INVALID, "nblocks %lld", (long long)nblocks);
+  if (nblocks == 0) return P64GPU_OK;
+  if (!in || !out) return fail(P64GPU_E_INVALID, "NULL block buffer");
+  const bool q = op >= P64GPU_OP_QUANT_INTRA && op <= P64GPU_OP_IQUANT_INTER;
+  if (q && (dcq < 1 || acq < 1 || dcq > 255 || acq > 31))
+    return fail(P64GPU_E_INVALID, "quantiser steps dcq=%d acq=%d", dcq, acq);
+  const int threads = 64;
+  const int64_t grid = (nblocks + threads - 1) / threads;
+  if (grid > 0x7fffffffLL) return fail(P64GPU_E_INVALID, "nblocks too large");
+  hipLaunchKernelGGL(k_block_op, dim3((unsigned)grid), dim3(threads), 0, (hipStream_t)stream, op,
+                     in, out, nblocks, dcq, acq);
+  HIP_TRY(hipGetLastError());
+  return P64GPU_OK;
+}
+
+int p64gpu_motion_estimation(int w, int h, int nframes, int64_t stride, const uint8_t *ref_y,
+                             const uint8_t *cur_y, int mode, int sl, p64_me_rec *out,
+                             void *stream) {
+  int s = check_geometry(w, h, nframes, stride, true);
+  if (s) return s;
+  if (!ref_y || !cur_y || !out) return fail(P64GPU_E_INVALID, "NULL buffer");
+  if (!aligned16(ref_y) || !aligned16(cur_y)) return fail(P64GPU_E_INVALID, "planes must be 16-byte aligned");
+  if (mode != P64GPU_ME_TSS && mode != P64GPU_ME_FULL) return fail(P64GPU_E_INVALID, "me mode %d", mode);
+  if (sl < 1 || sl > 31) return fail(P64GPU_E_INVALID, "search_limit %d not in 1..31", sl);
+  const unsigned grid = (unsigned)((int64_t)nframes * (w / 16) * (h / 16));
+  if (mode == P64GPU_ME_FULL)
+    hipLaunchKernelGGL(k_motion<2>, dim3(grid), dim3(64), 0, (hipStream_t)stream, w, h, stride,
+                       ref_y, cur_y, sl, out);
+  else
+    hipLaunchKernelGGL(k_motion<1>, dim3(grid), dim3(64), 0, (hipStream_t)stream, w, h, stride,
+                       ref_y, cur_y, sl, out);
+  HIP_TRY(hipGetLastError());
+  return P64GPU_OK;
+}
+
+int p64gpu_encode_frames(const p64gpu_encode_args *a, void *stream) {
+  if (!a) return fail(P64GPU_E_INVALID, "args is NULL");
+  int s = check_geometry(a->width, a->height, a->nframes, a->frame_stride);
+  if (s) return s;
+  if (!a->cur || !a->recon || !a->last_intra || !a->coef || !a->mb)
+    return fail(P64GPU_E_INVALID, "NULL required buffer");
+  if (!a->intra && !a->ref) return fail(P64GPU_E_INVALID, "inter picture needs ref");
+  if (!aligned16(a->cur) || !aligned16(a->recon) || !aligned16(a->coef) ||
+      (!a->intra && !aligned16(a->ref)))
+    return fail(P64GPU_E_INVALID, "cur/ref/recon/coef must be 16-byte aligned");
+  if (a->quant < 1 || a->quant > 31) return fail(P64GPU_E_INVALID, "quant %d not in 1..31", a->quant);
+  if (a->me_mode != P64GPU_ME_TSS && a->me_mode != P64GPU_ME_FULL)
+    return fail(P64GPU_E_INVALID, "me mode %d", a->me_mode);
+  if (a->search_limit < 1 || a->search_limit > 31)
+    return fail(P64GPU_E_INVALID, "search_limit %d not in 1..31", a->search_limit);
+  if (a->reserved != 0) return fail(P64GPU_E_INVALID, "reserved must be 0");
+  const unsigned grid = (unsigned)((int64_t)a->nframes * (a->width / 16) * (a->height / 16));
+  hipStream_t st = (hipStream_t)stream;
+  if (a->intra)
+    hipLaunchKernelGGL(k_encode<0>, dim3(grid), dim3(64), 0, st, *a);
+  else if (a->me_mode == P64GPU_ME_FULL)
+    hipLaunchKernelGGL(k_encode<2>, dim3(grid), dim3(64), 0, st, *a);
+  else
+    hipLaunchKernelGGL(k_encode<1>, dim3(grid), dim3(64), 0, st, *a);
+  HIP_TRY(hipGetLastError());
+  return P64GPU_OK;
+}
+
+int p64gpu_decode_recon(int w, int h, int nframes, int64_t stride, const uint8_t *ref,
+                        uint8_t *recon, const int16_t *coef, const p64_mb_rec *mb,
+                        const uint8_t *quant_mb, const uint8_t *coded_mask, void *stream) {
+  int s = check_geometry(w, h, nframes, stride);
+  if (s) return s;
+  if (!ref || !recon || !coef || !mb || !quant_mb || !coded_mask)
+    return fail(P64GPU_E_INVALID, "NULL buffer");
+  const unsigned grid = (unsigned)((int64_t)nframes * (w / 16) * (h / 16));
+  hipLaunchKernelGGL(k_decode_recon, dim3(grid), dim3(64), 0, (hipStream_t)stream, w, h, stride,
+                     ref, recon, coef, mb, quant_mb, coded_mask);
+  HIP_TRY(hipGetLastError());
+  return P64GPU_OK;
+}
+
+int p64gpu_synth_frames(int w, int h, uint32_t seed0, int nseeds, int frame0, int nslots,
+                        int64_t stride, uint8_t *out, void *stream) {
+  int s = check_geometry(w, h, 1, stride);
+  if (s) return s;
+  if (!out || nseeds < 1 || nslots < 1 || frame0 < 0 || (int64_t)nseeds * nslots > 65535)
+    return fail(P64GPU_E_INVALID, "synth: out=%p nseeds=%d nslots=%d frame0=%d", (void *)out,
+                nseeds, nslots, frame0);
+  hipLaunchKernelGGL(k_synth, dim3(64, (unsigned)(nseeds * nslots)), dim3(256), 0,
+                     (hipStream_t)stream, w, h, seed0, nseeds, frame0, stride, out);
+  HIP_TRY(hipGetLastError());
+  return P64GPU_OK;
+}
+
+// ---- host-buffer encoder context ------------------------------------------
+
+struct p64gpu_encoder {
+  int device, w, h, nmb, me_mode, sl;
+  size_t pic;
+  uint8_t *d_cur, *d_rec[2], *d_li;
+  int8_t *d_ov;
+  int16_t *d_coef;
+  p64_mb_rec *d_mb;
+  p64_me_rec *d_me;
+  int cur_ref;  // index of the buffer holding the previous reconstruction
+  hipStream_t stream;
+};
+
+static void enc_free(p64gpu_encoder *e) {
+  if (!e) return;
+  (void)hipFree(e->d_cur);
+  (void)hipFree(e->d_rec[0]);
+  (void)hipFree(e->d_rec[1]);
+  (void)hipFree(e->d_li);
+  (void)hipFree(e->d_ov);
+  (void)hipFree(e->d_coef);
+  (void)hipFree(e->d_mb);
+  (void)hipFree(e->d_me);
+  if (e->stream) (void)hipStreamDestroy(e->stream);
+  free(e);
+}
+
+int p64gpu_encoder_open(int device, int w, int h, int me_mode, int sl, p64gpu_encoder **out) {
+  if (!out) return fail(P64GPU_E_INVALID, "out is NULL");
+  *out = nullptr;
+  int s = check_geometry(w, h, 1, (int64_t)w * h * 3 / 2);
+  if (s) return s;
+  if (me_mode != P64GPU_ME_TSS && me_mode != P64GPU_ME_FULL)
+    return fail(P64GPU_E_INVALID, "me mode %d", me_mode);
+  if (sl < 1 || sl > 31) return fail(P64GPU_E_INVALID, "search_limit %d", sl);
+  s = p64gpu_set_device(device);
+  if (s) return s;
+  p64gpu_encoder *e = (p64gpu_encoder *)calloc(1, sizeof *e);
+  if (!e) return fail(P64GPU_E_NOMEM, "host allocation");
+  e->device = device;
+  e->w = w;
+  e->h = h;
+  e->nmb = (w / 16) * (h / 16);
+  e->me_mode = me_mode;
+  e->sl = sl;
+  e->pic = (size_t)w * h * 3 / 2;
+  bool ok = hipMalloc(&e->d_cur, e->pic) == hipSuccess &&
+            hipMalloc(&e->d_rec[0], e->pic) == hipSuccess &&
+            hipMalloc(&e->d_rec[1], e->pic) == hipSuccess &&
+            hipMalloc(&e->d_li, e->nmb) == hipSuccess &&
+            hipMalloc(&e->d_ov, e->nmb) == hipSuccess &&
+            hipMalloc(&e->d_coef, (size_t)e->nmb * 384 * sizeof(int16_t)) == hipSuccess &&
+            hipMalloc(&e->d_mb, (size_t)e->nmb * sizeof(p64_mb_rec)) == hipSuccess &&
+            hipMalloc(&e->d_me, (size_t)e->nmb * sizeof(p64_me_rec)) == hipSuccess &&
+            hipStreamCreate(&e->stream) == hipSuccess;
+  if (!ok) {
+    enc_free(e);
+    return fail(P64GPU_E_NOMEM, "device allocation for %dx%d encoder", w, h);
+  }
+  (void)hipMemset(e->d_rec[0], 0, e->pic);  // InitFS/ClearFS (p64.c:533-536)
+  (void)hipMemset(e->d_rec[1], 0, e->pic);
+  (void)hipMemset(e->d_li, 0, e->nmb);
+  *out = e;
+  return P64GPU_OK;
+}
+
+int p64gpu_encoder_frame(p64gpu_encoder *e, const uint8_t *picture, int intra, int quant,
+                         const int8_t *mtype_override, int16_t *coef, p64_mb_rec *mb,
+                         p64_me_rec *me, uint8_t *recon) {
+  if (!e || !picture || !coef || !mb) return fail(P64GPU_E_INVALID, "NULL argument");
+  HIP_TRY(hipSetDevice(e->device));
+  HIP_TRY(hipMemcpyAsync(e->d_cur, picture, e->pic, hipMemcpyHostToDevice, e->stream));
+  if (intra) HIP_TRY(hipMemsetAsync(e->d_li, 0, e->nmb, e->stream));
+  if (mtype_override)
+    HIP_TRY(hipMemcpyAsync(e->d_ov, mtype_override, e->nmb, hipMemcpyHostToDevice, e->stream));
+  p64gpu_encode_args a;
+  memset(&a, 0, sizeof a);
+  a.width = e->w;
+  a.height = e->h;
+  a.nframes = 1;
+  a.intra = intra ? 1 : 0;
+  a.quant = quant;
+  a.me_mode = e->me_mode;
+  a.search_limit = e->sl;
+  a.frame_stride = (int64_t)e->pic;
+  a.cur = e->d_cur;
+  a.ref = e->d_rec[e->cur_ref];
+  a.recon = e->d_rec[e->cur_ref ^ 1];
+  a.last_intra = e->d_li;
+  a.mtype_override = mtype_override ? e->d_ov : nullptr;
+  a.coef = e->d_coef;
+  a.mb = e->d_mb;
+  a.me = e->d_me;
+  int s = p64gpu_encode_frames(&a, e->stream);
+  if (s) return s;
+  HIP_TRY(hipMemcpyAsync(coef, e->d_coef, (size_t)e->nmb * 384 * sizeof(int16_t),
+                         hipMemcpyDeviceToHost, e->stream));
+  HIP_TRY(hipMemcpyAsync(mb, e->d_mb, (size_t)e->nmb * sizeof(p64_mb_rec), hipMemcpyDeviceToHost,
+                         e->stream));
+  if (me && !intra)
+    HIP_TRY(hipMemcpyAsync(me, e->d_me, (size_t)e->nmb * sizeof(p64_me_rec),
+                           hipMemcpyDeviceToHost, e->stream));
+  if (recon)
+    HIP_TRY(hipMemcpyAsync(recon, a.recon, e->pic, hipMemcpyDeviceToHost, e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  e->cur_ref ^= 1;  // SwapFS(CFS, OFS), p64.c:661
+  return P64GPU_OK;
+}
+
+void p64gpu_encoder_close(p64gpu_encoder *e) { enc_free(e); }
+
+}  // extern "C"

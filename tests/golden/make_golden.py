@@ -1,0 +1,340 @@
+"""Generate the golden fixtures in tests/golden/ from the UNMODIFIED reference.
+
+Runs only in the development container, where /root/reference exists: it needs
+oracle/_ref/ (built by `make -C oracle ref`) and p64_amd/libp64gpu.so (for the
+synthetic generator).  The reference itself never travels; only these small
+data files (inputs + expected outputs) are committed.
+
+  blocks.npz   per-function vectors from libp64ref.so (chendct.c, transform.c)
+  me.npz       per-MB FastBME (SL 31 and 15) and StepBME records, me.c
+  seq_*.npz    whole-encoder runs of p64hook (ref_hooks.c): per-MB MTYPE, CBP,
+               MVs, inputbuf levels, ME records and reconstructed pictures
+  decode.json  short.p64 decode MD5s (SETUP:15-32)
+
+Usage: python tests/golden/make_golden.py
+"""
+from __future__ import annotations
+
+import ctypes
+import hashlib
+import json
+import os
+import subprocess
+import sys
+import tempfile
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, REPO)
+REFDIR = "/root/reference"
+REF_OUT = os.path.join(REPO, "oracle", "_ref")
+
+import p64_amd  # noqa: E402  (synthetic generator only)
+
+
+class MEM(ctypes.Structure):  # mem.h:37-42
+    _fields_ = [("len", ctypes.c_int), ("width", ctypes.c_int), ("height", ctypes.c_int),
+                ("data", ctypes.c_void_p)]
+
+
+def reflib():
+    L = ctypes.CDLL(os.path.join(REF_OUT, "libp64ref.so"))
+    vp, i = ctypes.c_void_p, ctypes.c_int
+    for n in ("ChenDct", "ChenIDct", "ZigzagMatrix", "IZigzagMatrix"):
+        getattr(L, n).argtypes = [vp, vp]
+    for n in ("CCITTQuantize", "CCITTFlatQuantize", "ICCITTQuantize", "ICCITTFlatQuantize"):
+        getattr(L, n).argtypes = [vp, i, i]
+    for n in ("BoundDctMatrix", "BoundIDctMatrix", "FlatBoundQuantizeMatrix", "BoundQuantizeMatrix"):
+        getattr(L, n).argtypes = [vp]
+    for n in ("FastBME", "StepBME"):
+        getattr(L, n).argtypes = [i, i, ctypes.POINTER(MEM), i, i, ctypes.POINTER(MEM)]
+    return L
+
+
+def apply(L, name, blocks, *q):
+    src = np.ascontiguousarray(blocks, np.int32).reshape(-1, 64)
+    out = np.zeros_like(src)
+    f = getattr(L, name)
+    for k in range(src.shape[0]):
+        if name in ("ChenDct", "ChenIDct", "ZigzagMatrix", "IZigzagMatrix"):
+            a = src[k].copy()
+            f(a.ctypes.data, out[k].ctypes.data)
+        else:
+            out[k] = src[k]
+            f(out[k].ctypes.data, *q)
+    return out
+
+
+def dct_basis_signs():
+    """+-255 sign patterns of the 64 DCT basis functions (worst-case AC)."""
+    n = np.arange(8)
+    pats = []
+    for u in range(8):
+        for v in range(8):
+            b = np.outer(np.cos((2 * n + 1) * u * np.pi / 16), np.cos((2 * n + 1) * v * np.pi / 16))
+            s = np.where(b >= 0, 255, -255)
+            pats.append(s.reshape(64))
+            pats.append(np.where(b >= 0, 255, 0).reshape(64))
+    return np.array(pats, np.int32)
+
+
+def make_blocks(L, rng):
+    pix = rng.integers(0, 256, (600, 64))
+    res = rng.integers(-255, 256, (600, 64))
+    smooth = np.clip(rng.normal(128, 40, (200, 1)) + rng.normal(0, 6, (200, 64)), 0, 255).astype(np.int32)
+    dct_in = np.concatenate([pix, res, smooth, dct_basis_signs(),
+                             np.full((1, 64), 255), np.zeros((1, 64)), np.full((1, 64), -255)]).astype(np.int32)
+    dct_out = apply(L, "ChenDct", dct_in)
+
+    # IDCT inputs: dequantised levels of random sparse/dense blocks
+    idct_in = []
+    for k in range(1200):
+        q = int(rng.integers(1, 32))
+        lev = np.where(rng.random(64) < rng.random(), rng.integers(-127, 128, 64), 0).astype(np.int32)
+        deq = apply(L, "ICCITTQuantize", lev, q, q)[0]
+        idct_in.append(deq)
+    idct_in.append(np.full(64, 7905))
+    idct_in.append(np.where(np.arange(64) % 2, 7905, -7905))
+    idct_in = np.array(idct_in, np.int32)
+    idct_out = apply(L, "ChenIDct", idct_in)
+
+    # quantiser vectors for every q
+    qin = np.concatenate([rng.integers(-2048, 2049, (31, 64)),
+                          rng.integers(-6, 7, (31, 64))], axis=1).reshape(62, 64).astype(np.int32)
+    qin[:, :3] = [0, 1, -1]
+    quant = {}
+    for q in range(1, 32):
+        b = qin.copy()
+        quant[f"inter_q{q}"] = apply(L, "CCITTQuantize", b, q, q)
+        quant[f"intra_q{q}"] = apply(L, "CCITTFlatQuantize", b, 8, q)
+        lv = rng.integers(-127, 128, (8, 64)).astype(np.int32)
+        lv[:, :3] = [0, 1, -1]
+        quant[f"ilev_q{q}"] = lv
+        quant[f"iinter_q{q}"] = apply(L, "ICCITTQuantize", lv, q, q)
+        quant[f"iintra_q{q}"] = apply(L, "ICCITTFlatQuantize", lv, 8, q)
+    bnd_in = rng.integers(-3000, 3001, (200, 64)).astype(np.int32)
+    zz_in = rng.integers(-1000, 1000, (50, 64)).astype(np.int32)
+    np.savez_compressed(
+        os.path.join(HERE, "blocks.npz"),
+        dct_in=dct_in, dct_out=dct_out, idct_in=idct_in, idct_out=idct_out, quant_in=qin,
+        bound_in=bnd_in,
+        bound_dct=apply(L, "BoundDctMatrix", bnd_in), bound_idct=apply(L, "BoundIDctMatrix", bnd_in),
+        bound_qflat=apply(L, "FlatBoundQuantizeMatrix", bnd_in),
+        bound_quant=apply(L, "BoundQuantizeMatrix", bnd_in),
+        zz_in=zz_in, zz_out=apply(L, "ZigzagMatrix", zz_in), izz_out=apply(L, "IZigzagMatrix", zz_in),
+        **quant)
+
+
+def ref_me(L, ref_y, cur_y, w, h, mode, sl):
+    """Per-MB reference search: FastBME (mode 1) or StepBME (mode 0)."""
+    r = np.ascontiguousarray(ref_y, np.uint8)
+    c = np.ascontiguousarray(cur_y, np.uint8)
+    rm = MEM(w * h, w, h, r.ctypes.data)
+    cm = MEM(w * h, w, h, c.ctypes.data)
+    ctypes.c_int.in_dll(L, "SearchLimit").value = sl
+    out = []
+    for y in range(0, h, 16):
+        for x in range(0, w, 16):
+            (L.FastBME if mode == 1 else L.StepBME)(x, y, ctypes.byref(rm), x, y, ctypes.byref(cm))
+            g = lambda n: ctypes.c_int.in_dll(L, n).value  # noqa: E731
+            out.append((g("MX"), g("MY"), g("MV"), g("OMV"), g("refme_VAR"), g("refme_VAROR"),
+                        g("refme_MWOR")))
+    ctypes.c_int.in_dll(L, "SearchLimit").value = 15
+    return np.array(out, np.int32)
+
+
+def make_me(L, rng):
+    w, h = 176, 144
+    cases = []
+    # textured pairs from the synthetic generator (true motion + noise)
+    for seed in (1, 2, 3, 11, 24):
+        a = p64_amd.synth_frame(seed, 0, w, h)[: w * h]
+        b = p64_amd.synth_frame(seed, 1, w, h)[: w * h]
+        cases.append(("synth%d" % seed, a, b))
+    # pure noise: local minima everywhere
+    cases.append(("noise", rng.integers(0, 256, w * h, dtype=np.uint8),
+                  rng.integers(0, 256, w * h, dtype=np.uint8)))
+    # flat: every candidate ties
+    cases.append(("flat", np.full(w * h, 77, np.uint8), np.full(w * h, 77, np.uint8)))
+    # low-contrast: many exact ties between distinct vectors
+    lc = rng.integers(100, 103, w * h, dtype=np.uint8)
+    cases.append(("lowcontrast", lc, rng.integers(100, 103, w * h, dtype=np.uint8)))
+    # large pans (+-15 px) exercising the px < W-16 / py < H-16 exclusions
+    big = rng.integers(0, 256, (h + 40, w + 40), dtype=np.uint8)
+    for dx, dy in ((15, -15), (-15, 14), (14, 15), (-7, 3)):
+        ref = big[20:20 + h, 20:20 + w]
+        cur = big[20 - dy:20 - dy + h, 20 - dx:20 - dx + w]
+        cases.append((f"pan{dx}_{dy}", np.ascontiguousarray(ref).reshape(-1),
+                      np.ascontiguousarray(cur).reshape(-1)))
+    # two exact matches (+5,-3) and (-4,+6): FastBME must pick the dx-major first
+    ref = rng.integers(0, 256, (h, w), dtype=np.uint8)
+    cur = rng.integers(0, 256, (h, w), dtype=np.uint8)
+    for (x, y) in ((48, 48), (96, 64), (16, 96)):
+        blk = rng.integers(0, 256, (16, 16), dtype=np.uint8)
+        cur[y:y + 16, x:x + 16] = blk
+        ref[y - 3:y + 13, x + 5:x + 21] = blk
+        ref[y + 6:y + 22, x - 4:x + 12] = blk
+    cases.append(("twomatch", ref.reshape(-1), cur.reshape(-1)))
+    names, refs, curs, full31, full15, full7, tss = [], [], [], [], [], [], []
+    for n, r, c in cases:
+        names.append(n)
+        refs.append(r)
+        curs.append(c)
+        full31.append(ref_me(L, r, c, w, h, 1, 31))
+        full15.append(ref_me(L, r, c, w, h, 1, 15))
+        full7.append(ref_me(L, r, c, w, h, 1, 7))
+        tss.append(ref_me(L, r, c, w, h, 0, 15))
+    np.savez_compressed(os.path.join(HERE, "me.npz"), names=np.array(names), width=w, height=h,
+                        ref=np.array(refs), cur=np.array(curs), full31=np.array(full31),
+                        full15=np.array(full15), full7=np.array(full7), tss=np.array(tss))
+
+
+# ---------------------------------------------------------------------------
+# whole-encoder fixtures through the hooked reference binary
+
+FMT = {"QCIF": (176, 144), "CIF": (352, 288), "NTSC": (352, 240)}
+
+
+def write_y4m(path, frames, w, h):
+    with open(path, "wb") as f:
+        f.write(b"YUV4MPEG2 W%d H%d F30000:1001 Ip A0:0 C420jpeg\n" % (w, h))
+        for fr in frames:
+            f.write(b"FRAME\n")
+            f.write(fr.tobytes())
+
+
+def parse_dump(path, w, h):
+    raw = np.fromfile(path, np.uint8)
+    words = raw.view(np.int32) if raw.size % 4 == 0 else None
+    pos = 0
+    mbs, mes, recons = [], {}, {}
+    nbytes = raw.size
+    while pos < nbytes:
+        tag = int(np.frombuffer(raw[pos:pos + 4].tobytes(), np.int32)[0])
+        if tag == ord("E"):
+            fr, n = np.frombuffer(raw[pos + 4:pos + 12].tobytes(), np.int32)
+            arr = np.frombuffer(raw[pos + 12:pos + 12 + 28 * n].tobytes(), np.int32).reshape(7, n).T
+            mes[int(fr)] = arr.copy()
+            pos += 12 + 28 * n
+        elif tag == ord("M"):
+            hdr = np.frombuffer(raw[pos + 4:pos + 36].tobytes(), np.int32)
+            buf = np.frombuffer(raw[pos + 36:pos + 36 + 384 * 4].tobytes(), np.int32).reshape(6, 64)
+            mbs.append((hdr.copy(), buf.copy()))
+            pos += 36 + 384 * 4
+        elif tag == ord("R"):
+            fr, rw, rh = np.frombuffer(raw[pos + 4:pos + 16].tobytes(), np.int32)
+            n = rw * rh * 3 // 2
+            recons.setdefault(int(fr), raw[pos + 16:pos + 16 + n].copy())
+            pos += 16 + ((n + 3) // 4) * 4
+        else:
+            raise RuntimeError(f"bad dump tag {tag} at {pos}")
+    del words
+    return mbs, mes, recons
+
+
+def raster_index(fmt, g, m):
+    if fmt == "QCIF":  # io.c:733-736
+        return (3 * g + m // 11) * 11 + m % 11
+    mbx = (g & 1) * 11 + m % 11  # io.c:739-741
+    mby = (g >> 1) * 3 + m // 11
+    return mby * 22 + mbx
+
+
+def run_sequence(name, fmt, nframes, seed, *, me="tss", sl=15, q=8, oracle_prog=None):
+    w, h = FMT[fmt]
+    frames = [p64_amd.synth_frame(seed, t, w, h) for t in range(nframes)]
+    nmb = (w // 16) * (h // 16)
+    with tempfile.TemporaryDirectory() as td:
+        write_y4m(os.path.join(td, "in.y4m"), frames, w, h)
+        env = dict(os.environ, P64REF_DUMP=os.path.join(td, "dump.bin"))
+        if me == "full":
+            env["P64REF_ME"] = "full"
+        cmd = [os.path.join(REF_OUT, "p64hook"), "-" + fmt, "-y4m", "-a", "0", "-b",
+               str(nframes - 1), "-q", str(q), "-i", str(sl)]
+        if oracle_prog:
+            cmd.append("-o")
+        cmd += [os.path.join(td, "in"), "-z", ".y4m", "-s", os.path.join(td, "out.p64")]
+        stdin = open(os.path.join(REFDIR, oracle_prog)) if oracle_prog else subprocess.DEVNULL
+        subprocess.run(cmd, env=env, stdin=stdin, stdout=subprocess.DEVNULL, check=True)
+        mbs, mes, recons = parse_dump(os.path.join(td, "dump.bin"), w, h)
+        stream = open(os.path.join(td, "out.p64"), "rb").read()
+    mbrec = np.zeros((nframes, nmb, 4), np.int16)      # mtype cbp mvdh mvdv (as in ReadCompressMDU)
+    usequant = np.zeros((nframes, nmb), np.int16)
+    coef = np.zeros((nframes, nmb, 6, 64), np.int16)
+    seen = np.zeros((nframes, nmb), bool)
+    for hdr, buf in mbs:
+        fr, g, m, mt, cbp, mvh, mvv, uq = [int(x) for x in hdr]
+        k = raster_index(fmt, g, m)
+        mbrec[fr, k] = (mt, cbp, mvh, mvv)
+        usequant[fr, k] = uq
+        coef[fr, k] = buf
+        seen[fr, k] = True
+    assert seen.all(), "every MB of every picture is coded by the encoder"
+    merecs = np.zeros((nframes, nmb, 7), np.int32)
+    for fr, arr in mes.items():
+        merecs[fr] = arr
+    # recon of picture t is dumped when picture t+1 (or the trailer) starts
+    rec = np.zeros((nframes, w * h * 3 // 2), np.uint8)
+    for fr, pic in recons.items():
+        if fr >= 1:
+            rec[fr - 1] = pic
+    final = max(recons)
+    assert final == nframes, (final, nframes)
+    # Pictures are regenerated from the seeded generator (their SHA-256 pins the
+    # generator); QCIF runs also keep the raw bytes.
+    sha = lambda a: hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()  # noqa: E731
+    extra = {}
+    if fmt == "QCIF":
+        extra = dict(frames=np.array(frames), recon=rec)
+    np.savez_compressed(os.path.join(HERE, f"seq_{name}.npz"), fmt=fmt, width=w, height=h,
+                        seed=seed, nframes=nframes, me=me, sl=sl, q=q,
+                        oracle=oracle_prog or "", mb=mbrec, usequant=usequant, coef=coef,
+                        merec=merecs, frames_sha256=np.array([sha(f) for f in frames]),
+                        recon_sha256=np.array([sha(r) for r in rec]),
+                        stream_sha256=hashlib.sha256(stream).hexdigest(), stream_len=len(stream),
+                        **extra)
+    return mbrec
+
+
+def decode_md5():
+    with tempfile.TemporaryDirectory() as td:
+        subprocess.run([os.path.join(REF_OUT, "p64"), "-d", "-s", os.path.join(REFDIR, "short.p64"),
+                        os.path.join(td, "short")], stdout=subprocess.DEVNULL, check=True)
+        out = {}
+        for i in range(7):
+            for c in "YUV":
+                p = os.path.join(td, f"short{i}.{c}")
+                out[f"short{i}.{c}"] = hashlib.md5(open(p, "rb").read()).hexdigest()
+    with open(os.path.join(HERE, "decode.json"), "w") as f:
+        json.dump(out, f, indent=1, sort_keys=True)
+
+
+def main():
+    if not os.path.exists(os.path.join(REF_OUT, "p64hook")):
+        subprocess.run(["make", "-C", os.path.join(REPO, "oracle"), "ref"], check=True)
+    rng = np.random.default_rng(20261015)
+    L = reflib()
+    make_blocks(L, rng)
+    make_me(L, rng)
+    run_sequence("qcif_tss", "QCIF", 8, 3)
+    run_sequence("qcif_full31", "QCIF", 6, 4, me="full", sl=31)
+    run_sequence("qcif_full15", "QCIF", 4, 13, me="full", sl=15)
+    run_sequence("qcif_q31", "QCIF", 6, 5, q=31)
+    run_sequence("qcif_q1", "QCIF", 3, 6, q=1, me="full", sl=31)
+    run_sequence("qcif_q2", "QCIF", 3, 8, q=2)
+    run_sequence("qcif_clean_tss", "QCIF", 4, 6)
+    run_sequence("qcif_clean_full31", "QCIF", 4, 14, me="full", sl=31, q=16)
+    run_sequence("qcif_flat_tss", "QCIF", 4, 7, q=8)
+    run_sequence("qcif_flat_full31", "QCIF", 4, 15, me="full", sl=31, q=4)
+    run_sequence("qcif_intra", "QCIF", 4, 7, oracle_prog="test.intra")
+    run_sequence("cif_full31", "CIF", 3, 1, me="full", sl=31)
+    run_sequence("cif_tss", "CIF", 3, 2)
+    run_sequence("ntsc_tss", "NTSC", 3, 9)
+    run_sequence("cif_scene_full31", "CIF", 14, 5, me="full", sl=31, q=12)
+    decode_md5()
+
+
+if __name__ == "__main__":
+    main()

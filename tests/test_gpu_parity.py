@@ -1,0 +1,253 @@
+"""GPU parity: the HIP path (through the C ABI) against the golden fixtures and
+the pinned CPU oracle, bit-exact.  Run on an MI355X with `pytest -m gpu`."""
+import hashlib
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+from test_oracle_golden import SEQS, check_sequence_outputs, load, sequence_frames, sequence_params
+
+pytestmark = pytest.mark.gpu
+
+
+def dev(torch, a):
+    return torch.from_numpy(np.ascontiguousarray(a)).cuda()
+
+
+def host(t):
+    return t.cpu().numpy()
+
+
+# ---------------------------------------------------------------------------
+# block routines (chendct.c / transform.c)
+
+def test_block_ops_golden(p64, torch_dev):
+    torch = torch_dev
+    z = load("blocks.npz")
+    np.testing.assert_array_equal(host(p64.ChenDct(dev(torch, z["dct_in"]))), z["dct_out"])
+    np.testing.assert_array_equal(host(p64.ChenIDct(dev(torch, z["idct_in"]))), z["idct_out"])
+    b = dev(torch, z["bound_in"])
+    np.testing.assert_array_equal(host(p64.BoundDctMatrix(b)), z["bound_dct"])
+    np.testing.assert_array_equal(host(p64.BoundIDctMatrix(b)), z["bound_idct"])
+    np.testing.assert_array_equal(host(p64.FlatBoundQuantizeMatrix(b)), z["bound_qflat"])
+    np.testing.assert_array_equal(host(p64.BoundQuantizeMatrix(b)), z["bound_quant"])
+    zz = dev(torch, z["zz_in"])
+    np.testing.assert_array_equal(host(p64.ZigzagMatrix(zz)), z["zz_out"])
+    np.testing.assert_array_equal(host(p64.IZigzagMatrix(zz)), z["izz_out"])
+    qin = dev(torch, z["quant_in"])
+    for q in range(1, 32):
+        np.testing.assert_array_equal(host(p64.CCITTQuantize(qin, q, q)), z[f"inter_q{q}"])
+        np.testing.assert_array_equal(host(p64.CCITTFlatQuantize(qin, 8, q)), z[f"intra_q{q}"])
+        lv = dev(torch, z[f"ilev_q{q}"])
+        np.testing.assert_array_equal(host(p64.ICCITTQuantize(lv, q, q)), z[f"iinter_q{q}"])
+        np.testing.assert_array_equal(host(p64.ICCITTFlatQuantize(lv, 8, q)), z[f"iintra_q{q}"])
+
+
+def test_block_ops_random_vs_oracle(p64, oracle_mod, torch_dev):
+    torch = torch_dev
+    rng = np.random.default_rng(7)
+    x = rng.integers(-255, 256, (4096, 64)).astype(np.int32)
+    np.testing.assert_array_equal(host(p64.ChenDct(dev(torch, x))), oracle_mod.block_apply("orc_chen_dct", x))
+    y = rng.integers(-7905, 7906, (4096, 64)).astype(np.int32)
+    np.testing.assert_array_equal(host(p64.ChenIDct(dev(torch, y))), oracle_mod.block_apply("orc_chen_idct", y))
+
+
+def test_empty_batch(p64, torch_dev):
+    torch = torch_dev
+    e = torch.empty((0, 64), dtype=torch.int32, device="cuda")
+    assert p64.ChenDct(e).shape == (0, 64)
+
+
+# ---------------------------------------------------------------------------
+# motion estimation (me.c)
+
+@pytest.mark.parametrize("key,mode,sl", [("full31", 1, 31), ("full15", 1, 15), ("full7", 1, 7),
+                                         ("tss", 0, 15)])
+def test_motion_estimation_golden(p64, torch_dev, key, mode, sl):
+    torch = torch_dev
+    z = load("me.npz")
+    w, h = int(z["width"]), int(z["height"])
+    n = z["ref"].shape[0]
+    # batch every case into one launch: each luma plane is its own "picture"
+    ref = dev(torch, z["ref"].reshape(n, w * h))
+    cur = dev(torch, z["cur"].reshape(n, w * h))
+    got = host(p64.MotionEstimation(ref, cur, w, h, mode=mode, search_limit=sl, frame_stride=w * h))
+    for i, name in enumerate(z["names"]):
+        np.testing.assert_array_equal(got[i], z[key][i], err_msg=f"{key} case {name}")
+
+
+def test_motion_estimation_random_cif_vs_oracle(p64, oracle_mod, torch_dev):
+    torch = torch_dev
+    w, h = 352, 288
+    rng = np.random.default_rng(11)
+    frames = [p64.synth_frame(s, 3, w, h) for s in (1, 2)] + \
+        [rng.integers(0, 256, w * h * 3 // 2, dtype=np.uint8)]
+    prevs = [p64.synth_frame(s, 2, w, h) for s in (1, 2)] + \
+        [rng.integers(0, 256, w * h * 3 // 2, dtype=np.uint8)]
+    cur = dev(torch, np.stack(frames))
+    ref = dev(torch, np.stack(prevs))
+    for mode, sl in ((1, 31), (0, 15)):
+        got = host(p64.MotionEstimation(ref, cur, w, h, mode=mode, search_limit=sl))
+        for i in range(len(frames)):
+            exp = oracle_mod.motion_estimation(prevs[i][: w * h], frames[i][: w * h], w, h, mode, sl)
+            exp = np.stack([exp[f] for f in exp.dtype.names], axis=1)
+            np.testing.assert_array_equal(got[i], exp, err_msg=f"mode {mode} frame {i}")
+
+
+# ---------------------------------------------------------------------------
+# whole-encoder fixtures, through the batched device API and the host context
+
+def run_device_sequence(p64, torch, frames, w, h, *, quant, me_mode, search_limit, mtype_override):
+    """Closed loop through p64gpu_encode_frames, one stream."""
+    nmb = (w // 16) * (h // 16)
+    pic = w * h * 3 // 2
+    li = torch.zeros(nmb, dtype=torch.uint8, device="cuda")
+    bufs = [torch.zeros(pic, dtype=torch.uint8, device="cuda") for _ in range(2)]
+    ov = dev(torch, mtype_override) if mtype_override is not None else None
+    outs = []
+    for t, f in enumerate(frames):
+        cur = dev(torch, f)
+        ref, rec = bufs[(t + 1) % 2], bufs[t % 2]
+        o = p64.encode_frames(cur, ref, rec, li, width=w, height=h, intra=(t == 0), quant=quant,
+                              me_mode=me_mode, search_limit=search_limit,
+                              mtype_override=(ov if t > 0 else None))
+        coef = host(o.coef)[0]
+        mb = host(o.mb)[0].view(p64.MB_DTYPE).reshape(nmb)
+        me = host(o.me)[0].view(p64.ME_DTYPE).reshape(nmb)
+        outs.append((coef, mb, me, host(rec).copy()))
+    return outs
+
+
+@pytest.mark.parametrize("name", SEQS)
+def test_sequence_golden_device(p64, torch_dev, name):
+    z = load(f"seq_{name}.npz")
+    w, h = int(z["width"]), int(z["height"])
+    frames = sequence_frames(p64, z)
+    outs = run_device_sequence(p64, torch_dev, frames, w, h, **sequence_params(z))
+    check_sequence_outputs(z, outs, name)
+
+
+@pytest.mark.parametrize("name", ["qcif_tss", "cif_full31", "qcif_intra", "qcif_flat_tss"])
+def test_sequence_golden_host_context(p64, torch_dev, name):
+    z = load(f"seq_{name}.npz")
+    w, h = int(z["width"]), int(z["height"])
+    prm = sequence_params(z)
+    frames = sequence_frames(p64, z)
+    enc = p64.Encoder(w, h, me_mode=prm["me_mode"], search_limit=prm["search_limit"])
+    outs = []
+    for t, f in enumerate(frames):
+        ov = prm["mtype_override"] if t > 0 else None
+        coef, mb, me, recon = enc.frame(f, intra=(t == 0), quant=prm["quant"], mtype_override=ov,
+                                        want_recon=True)
+        outs.append((coef, mb, me, recon))
+    enc.close()
+    check_sequence_outputs(z, outs, name)
+
+
+# ---------------------------------------------------------------------------
+# batched multi-stream closed loop vs the oracle (the bench's shape, smaller)
+
+@pytest.mark.parametrize("w,h,me_mode,sl,q", [(352, 288, 1, 31, 8), (352, 288, 0, 15, 5),
+                                             (704, 576, 1, 31, 12), (176, 144, 1, 15, 3),
+                                             (352, 240, 1, 31, 31)])
+def test_batched_streams_vs_oracle(p64, oracle_mod, torch_dev, w, h, me_mode, sl, q):
+    torch = torch_dev
+    nstreams, nframes = 4, 3
+    seeds = [3 + 5 * s for s in range(nstreams)]
+    nmb = (w // 16) * (h // 16)
+    pic = w * h * 3 // 2
+    frames = np.stack([[p64.synth_frame(s, t, w, h) for s in seeds] for t in range(nframes)])
+    li = torch.zeros(nstreams * nmb, dtype=torch.uint8, device="cuda")
+    bufs = [torch.zeros(nstreams * pic, dtype=torch.uint8, device="cuda") for _ in range(2)]
+    qmb = np.full((nstreams, nmb), q, np.uint8)
+    qmb[1] = np.arange(nmb) % 31 + 1  # per-MB UseQuant on one stream
+    qmb_d = dev(torch, qmb)
+    got = []
+    for t in range(nframes):
+        cur = dev(torch, frames[t])
+        ref, rec = bufs[(t + 1) % 2], bufs[t % 2]
+        o = p64.encode_frames(cur, ref, rec, li, width=w, height=h, intra=(t == 0), quant=q,
+                              me_mode=me_mode, search_limit=sl, quant_mb=qmb_d)
+        got.append((host(o.coef), host(o.mb), host(o.me), host(rec).reshape(nstreams, pic)))
+    for s in range(nstreams):
+        li_o = np.zeros(nmb, np.uint8)
+        ref = None
+        for t in range(nframes):
+            coef, mb, me, recon = oracle_mod.encode_frame(
+                w, h, frames[t][s], ref, li_o, intra=(t == 0), quant=q, me_mode=me_mode,
+                search_limit=sl, quant_mb=qmb[s])
+            ref = recon
+            g = got[t]
+            np.testing.assert_array_equal(g[0][s], coef, err_msg=f"coef s{s} t{t}")
+            np.testing.assert_array_equal(g[1][s].view(p64.MB_DTYPE).reshape(nmb), mb,
+                                          err_msg=f"mb s{s} t{t}")
+            if t > 0:
+                np.testing.assert_array_equal(g[2][s].view(p64.ME_DTYPE).reshape(nmb), me,
+                                              err_msg=f"me s{s} t{t}")
+            np.testing.assert_array_equal(g[3][s], recon, err_msg=f"recon s{s} t{t}")
+
+
+def test_intra_refresh_and_override(p64, oracle_mod, torch_dev):
+    """LastIntra > 131 forces MTYPE 0 (p64.c:772); -o overrides (p64.c:761-768),
+    including MC types without coefficients (4, 7) and MQUANT types."""
+    torch = torch_dev
+    w, h = 176, 144
+    nmb = 99
+    rng = np.random.default_rng(5)
+    f0, f1 = p64.synth_frame(21, 0, w, h), p64.synth_frame(21, 1, w, h)
+    li0 = rng.integers(120, 140, nmb).astype(np.uint8)
+    ov = rng.integers(-1, 10, nmb).astype(np.int8)
+    # reference picture = oracle intra recon of f0
+    li_tmp = np.zeros(nmb, np.uint8)
+    _, _, _, rec0 = oracle_mod.encode_frame(w, h, f0, None, li_tmp, intra=True, quant=8)
+    li_o = li0.copy()
+    coef, mb, me, recon = oracle_mod.encode_frame(w, h, f1, rec0, li_o, intra=False, quant=8,
+                                                  me_mode=1, search_limit=31, mtype_override=ov)
+    li_d = dev(torch, li0)
+    rec_d = torch.zeros(w * h * 3 // 2, dtype=torch.uint8, device="cuda")
+    o = p64.encode_frames(dev(torch, f1), dev(torch, rec0), rec_d, li_d, width=w, height=h,
+                          intra=False, quant=8, me_mode=1, search_limit=31,
+                          mtype_override=dev(torch, ov))
+    np.testing.assert_array_equal(host(o.coef)[0], coef)
+    np.testing.assert_array_equal(host(o.mb)[0].view(p64.MB_DTYPE).reshape(nmb), mb)
+    np.testing.assert_array_equal(host(rec_d), recon)
+    np.testing.assert_array_equal(host(li_d), li_o)
+    assert (mb["mtype"][li0 > 131] == 0).all()
+
+
+def test_decoder_recon_matches_encoder(p64, torch_dev):
+    """Decode-side reconstruction of the encoder's own output reproduces the
+    encoder's closed-loop reconstruction (encoder recon ==
+    decoder output)."""
+    torch = torch_dev
+    w, h = 352, 288
+    nmb = 396
+    seeds = [1, 6, 7, 13]
+    pic = w * h * 3 // 2
+    f0 = dev(torch, np.stack([p64.synth_frame(s, 0, w, h) for s in seeds]))
+    f1 = dev(torch, np.stack([p64.synth_frame(s, 1, w, h) for s in seeds]))
+    li = torch.zeros(len(seeds) * nmb, dtype=torch.uint8, device="cuda")
+    r0 = torch.zeros(len(seeds) * pic, dtype=torch.uint8, device="cuda")
+    r1 = torch.zeros_like(r0)
+    o0 = p64.encode_frames(f0, None, r0, li, width=w, height=h, intra=True, quant=6)
+    o1 = p64.encode_frames(f1, r0, r1, li, width=w, height=h, intra=False, quant=6, me_mode=1,
+                           search_limit=31)
+    qmb = torch.full((len(seeds) * nmb,), 6, dtype=torch.uint8, device="cuda")
+    mask = torch.ones_like(qmb)
+    d0 = torch.zeros_like(r0)
+    p64.decode_recon(d0, d0, o0.coef, o0.mb, qmb, mask, width=w, height=h)
+    assert torch.equal(d0, r0)
+    d1 = d0.clone()
+    p64.decode_recon(d0, d1, o1.coef, o1.mb, qmb, mask, width=w, height=h)
+    assert torch.equal(d1, r1)
+
+
+def test_invalid_arguments_raise(p64, torch_dev):
+    torch = torch_dev
+    x = torch.zeros(10, dtype=torch.uint8, device="cuda")
+    with pytest.raises(p64.P64GpuError):
+        p64.encode_frames(x, x, x, x, width=100, height=64, intra=True)
+    with pytest.raises(p64.P64GpuError):
+        p64.MotionEstimation(x, x, 176, 144, mode=5)
