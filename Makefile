@@ -8,6 +8,7 @@
 
 HIPCC   ?= /opt/rocm/bin/hipcc
 CC      ?= gcc
+CXX     ?= g++
 ARCH    ?= gfx950
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Wall -Wno-unused-function
 LIB     := p64_amd/libp64gpu.so

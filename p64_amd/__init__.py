@@ -88,7 +88,15 @@ def lib() -> ctypes.CDLL:
         return _lib
     if not os.path.exists(LIB_PATH):
         raise P64GpuError(f"{LIB_PATH} not built: run `make` (or __graft_entry__.build())")
+    # One HIP runtime per process: PyTorch bundles its own libamdhip64 (SONAME
+    # libamdhip64.so.7).  Loading torch first lets our DT_NEEDED resolve to that
+    # already-mapped copy, so device pointers and streams are shared with torch.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = ctypes.CDLL(LIB_PATH)
+    _check_single_runtime()
     vp, i32, i64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64
     L.p64gpu_abi_version.restype = i32
     L.p64gpu_strerror.restype = ctypes.c_char_p
@@ -114,6 +122,17 @@ def lib() -> ctypes.CDLL:
         raise P64GpuError("libp64gpu.so ABI version mismatch")
     _lib = L
     return L
+
+
+def _check_single_runtime() -> None:
+    paths = set()
+    with open("/proc/self/maps") as f:
+        for line in f:
+            if "libamdhip64" in line:
+                paths.add(os.path.realpath(line.split()[-1]))
+    if len(paths) > 1:
+        raise P64GpuError(f"two HIP runtimes mapped in this process: {sorted(paths)}; "
+                          "import torch before loading libp64gpu.so")
 
 
 def _check(status: int) -> None:
