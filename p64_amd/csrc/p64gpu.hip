@@ -10,11 +10,13 @@
 //     SAD accumulators; the argmin is one wave-wide min over packed
 //     (SAD, scan-order) keys, reproducing FastBME's first-minimum rule;
 //   * TSS: lane = (candidate, row pair); four dependent steps of 8 candidates;
-//   * encode: lane = (block, row) for 6 blocks; the Chen DCT/IDCT row and
-//     column passes exchange through LDS; quantisation, zigzag, CBP and the
-//     reconstruction are fused into the same wave.
+//   * encode: "row" layout lane = (block, row) for the prediction, the loop
+//     filter (vertical taps exchanged with DPP) and the Chen row/column passes;
+//     "element" layout lane = coefficient for quantisation, zigzag, CBP (wave
+//     ballots) and dequantisation; the layouts exchange through LDS.
 // All arithmetic is integer except the MTYPE decision, which is evaluated in
-// IEEE binary64 exactly as p64.c:745-756 writes it.
+// IEEE binary64 exactly as p64.c:745-756 writes it.  Products whose operands
+// are provably below 2^23 use the full-rate 24-bit multiplier.
 
 #include <hip/hip_runtime.h>
 
@@ -81,29 +83,37 @@ constexpr ZigZag make_zigzag() {
 __constant__ ZigZag c_zz = make_zigzag();
 
 // ---------------------------------------------------------------------------
-// Chen integer DCT kernels of one 8-point line (chendct.c:97-375)
+// Chen integer DCT of one 8-point line (chendct.c:97-375).
+// NARROW = operands proven < 2^23 (fused kernels): full-rate v_mul_i32_i24;
+// otherwise (block-op API, arbitrary int32) the 32-bit multiply.
 
 constexpr int C1D4 = 362, C1D8 = 473, C3D8 = 196, C1D16 = 502, C3D16 = 426,
               C5D16 = 284, C7D16 = 100;
 
+template <bool NARROW>
+__device__ __forceinline__ int kmul(int c, int v) {
+  return NARROW ? __mul24(c, v) : c * v;
+}
 __device__ __forceinline__ int ms9(int v) { return v >> 9; }  // MSCALE, arithmetic
 
 // forward butterfly on scaled sums s[k] and differences d[k] (chendct.c:135-159)
+template <bool N>
 __device__ __forceinline__ void fwd8(const int s[4], const int d[4], int o[8]) {
   const int e0 = s[0] + s[3], e1 = s[1] + s[2], e2 = s[1] - s[2], e3 = s[0] - s[3];
-  o[0] = ms9(C1D4 * (e0 + e1));
-  o[4] = ms9(C1D4 * (e0 - e1));
-  o[2] = ms9(C3D8 * e2 + C1D8 * e3);
-  o[6] = ms9(C3D8 * e3 - C1D8 * e2);
-  const int r0 = ms9(C1D4 * (d[1] - d[2])), r1 = ms9(C1D4 * (d[1] + d[2]));
+  o[0] = ms9(kmul<N>(C1D4, e0 + e1));
+  o[4] = ms9(kmul<N>(C1D4, e0 - e1));
+  o[2] = ms9(kmul<N>(C3D8, e2) + kmul<N>(C1D8, e3));
+  o[6] = ms9(kmul<N>(C3D8, e3) - kmul<N>(C1D8, e2));
+  const int r0 = ms9(kmul<N>(C1D4, d[1] - d[2])), r1 = ms9(kmul<N>(C1D4, d[1] + d[2]));
   const int u0 = d[3] + r0, u1 = d[3] - r0, u2 = d[0] - r1, u3 = d[0] + r1;
-  o[1] = ms9(C7D16 * u0 + C1D16 * u3);
-  o[3] = ms9(C3D16 * u2 - C5D16 * u1);
-  o[5] = ms9(C3D16 * u1 + C5D16 * u2);
-  o[7] = ms9(C7D16 * u3 - C1D16 * u0);
+  o[1] = ms9(kmul<N>(C7D16, u0) + kmul<N>(C1D16, u3));
+  o[3] = ms9(kmul<N>(C3D16, u2) - kmul<N>(C5D16, u1));
+  o[5] = ms9(kmul<N>(C3D16, u1) + kmul<N>(C5D16, u2));
+  o[7] = ms9(kmul<N>(C7D16, u3) - kmul<N>(C1D16, u0));
 }
 
 // column pass: sums/differences scaled <<2 (chendct.c:120-133)
+template <bool N>
 __device__ __forceinline__ void fwd_col(const int x[8], int o[8]) {
   int s[4], d[4];
 #pragma unroll
@@ -111,9 +121,10 @@ __device__ __forceinline__ void fwd_col(const int x[8], int o[8]) {
     s[k] = (x[k] + x[7 - k]) << 2;
     d[k] = (x[k] - x[7 - k]) << 2;
   }
-  fwd8(s, d, o);
+  fwd8<N>(s, d, o);
 }
 // row pass: sums/differences >>1 (chendct.c:167-174)
+template <bool N>
 __device__ __forceinline__ void fwd_row(const int x[8], int o[8]) {
   int s[4], d[4];
 #pragma unroll
@@ -121,20 +132,22 @@ __device__ __forceinline__ void fwd_row(const int x[8], int o[8]) {
     s[k] = (x[k] + x[7 - k]) >> 1;
     d[k] = (x[k] - x[7 - k]) >> 1;
   }
-  fwd8(s, d, o);
+  fwd8<N>(s, d, o);
 }
 
 // inverse butterfly (chendct.c:254-303 == 320-365)
+template <bool N>
 __device__ __forceinline__ void inv8(const int x[8], int o[8]) {
-  const int p0 = ms9(C7D16 * x[1] - C1D16 * x[7]);
-  const int p1 = ms9(C3D16 * x[5] - C5D16 * x[3]);
-  const int p2 = ms9(C3D16 * x[3] + C5D16 * x[5]);
-  const int p3 = ms9(C1D16 * x[1] + C7D16 * x[7]);
-  const int q0 = ms9(C1D4 * (x[0] + x[4])), q1 = ms9(C1D4 * (x[0] - x[4]));
-  const int q2 = ms9(C3D8 * x[2] - C1D8 * x[6]), q3 = ms9(C1D8 * x[2] + C3D8 * x[6]);
+  const int p0 = ms9(kmul<N>(C7D16, x[1]) - kmul<N>(C1D16, x[7]));
+  const int p1 = ms9(kmul<N>(C3D16, x[5]) - kmul<N>(C5D16, x[3]));
+  const int p2 = ms9(kmul<N>(C3D16, x[3]) + kmul<N>(C5D16, x[5]));
+  const int p3 = ms9(kmul<N>(C1D16, x[1]) + kmul<N>(C7D16, x[7]));
+  const int q0 = ms9(kmul<N>(C1D4, x[0] + x[4])), q1 = ms9(kmul<N>(C1D4, x[0] - x[4]));
+  const int q2 = ms9(kmul<N>(C3D8, x[2]) - kmul<N>(C1D8, x[6]));
+  const int q3 = ms9(kmul<N>(C1D8, x[2]) + kmul<N>(C3D8, x[6]));
   const int e0 = q0 + q3, e1 = q1 + q2, e2 = q1 - q2, e3 = q0 - q3;
   const int f0 = p0 + p1, f1 = p0 - p1, f2 = p3 - p2, f3 = p3 + p2;
-  const int g1 = ms9(C1D4 * (f2 - f1)), g2 = ms9(C1D4 * (f2 + f1));
+  const int g1 = ms9(kmul<N>(C1D4, f2 - f1)), g2 = ms9(kmul<N>(C1D4, f2 + f1));
   o[0] = e0 + f3;
   o[1] = e1 + g2;
   o[2] = e2 + g1;
@@ -152,7 +165,7 @@ __device__ __forceinline__ int clampi(int v, int lo, int hi) { return min(max(v,
 // ---------------------------------------------------------------------------
 // quantisers (transform.c:271-451, non-VERSION_1_0)
 
-// Truncating c / d for d = 2q.  In the fused kernel |c| <= 2048 (BoundDctMatrix
+// Truncating c / d for d = 2q.  In the fused kernels |c| <= 2048 (BoundDctMatrix
 // plus the +-1 of even q), where the 20-bit reciprocal is exact for every
 // d <= 62 (tests/test_quant_magic.py checks it exhaustively); the block-op path
 // handles arbitrary int32 with a true division.
@@ -160,7 +173,7 @@ template <bool BOUNDED>
 __device__ __forceinline__ int div_trunc(int c, int d, unsigned magic) {
   if (BOUNDED) {
     const unsigned a = (unsigned)abs(c);
-    const int qq = (int)((a * magic) >> 20);
+    const int qq = (int)(__umul24(a, magic) >> 20);
     return c < 0 ? -qq : qq;
   }
   return c / d;
@@ -178,10 +191,11 @@ __device__ __forceinline__ int qdc_intra(int c, int dcq) {
   return c > 0 ? (c + dcq / 2) / dcq : (c - dcq / 2) / dcq;
 }
 // reconstruction level (transform.c:376-389, 436-448)
+template <bool NARROW>
 __device__ __forceinline__ int rlevel(int l, int q) {
   if (l == 0) return 0;
   const int sg = l > 0 ? 1 : -1;
-  int v = (2 * l + sg) * q;
+  int v = kmul<NARROW>(2 * l + sg, q);
   if (!(q & 1)) v -= sg;
   return v;
 }
@@ -207,6 +221,22 @@ __device__ __forceinline__ uint32_t sad4(uint32_t a, uint32_t b, uint32_t acc) {
 __device__ __forceinline__ uint32_t align4(uint32_t hi, uint32_t lo, int shift) {
   return __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)shift);
 }
+// value of lane-1 / lane+1 inside the 16-lane DPP row (row_shr:1 / row_shl:1)
+__device__ __forceinline__ int from_prev_lane(int v) {
+  return __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, false);
+}
+__device__ __forceinline__ int from_next_lane(int v) {
+  return __builtin_amdgcn_update_dpp(0, v, 0x101, 0xf, 0xf, false);
+}
+
+// workgroup id -> macroblock id, bijective, so that ids sharing an XCD
+// (blockIdx % 8 under round-robin dispatch) get contiguous macroblocks and
+// neighbouring search windows meet in the same L2 (speed only, never
+// correctness: cdna_hip_programming.md T1)
+__device__ __forceinline__ unsigned xcd_remap(unsigned bid, unsigned n) {
+  const unsigned q = n >> 3, r = n & 7, x = bid & 7, k = bid >> 3;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + k;
+}
 
 // ---------------------------------------------------------------------------
 // per-macroblock LDS image
@@ -220,6 +250,7 @@ constexpr int BLK_STRIDE = 72, ROW_STRIDE = 9;  // padded DCT scratch
 struct __align__(16) MbLds {
   uint32_t win[WIN_ROWS * WIN_WORDS];  // previous reconstruction, luma
   uint32_t cur[64];                    // current 16x16 luma
+  uint32_t cpred[2 * 16];              // chroma prediction sources, 2 x 8x8 bytes
   int blk[6 * BLK_STRIDE];             // row/column exchange for DCT/IDCT
   int16_t zz[6 * 64];                  // zigzagged levels for the store
 };
@@ -244,10 +275,10 @@ __device__ __forceinline__ void stage_luma(MbLds &L, const uint8_t *ref_y, const
     const int gy = y0 - WIN_OY + row, gx = x0 - WIN_OX + seg * 16;
     uint4 v = make_uint4(0, 0, 0, 0);
     if (gy >= 0 && gy < h && gx >= 0 && gx < w)
-      v = *reinterpret_cast<const uint4 *>(ref_y + (size_t)gy * w + gx);
+      v = *reinterpret_cast<const uint4 *>(ref_y + gy * w + gx);
     reinterpret_cast<uint4 *>(L.win)[t] = v;
   }
-  L.cur[lane] = *reinterpret_cast<const uint32_t *>(cur_y + (size_t)(y0 + (lane >> 2)) * w + x0 +
+  L.cur[lane] = *reinterpret_cast<const uint32_t *>(cur_y + (y0 + (lane >> 2)) * w + x0 +
                                                     4 * (lane & 3));
 }
 
@@ -261,7 +292,7 @@ __device__ __forceinline__ int sad_zero(const MbLds &L, int lane) {
   return wave_sum((int)sad4(r, L.cur[lane], 0));
 }
 
-// FastBME (me.c:187-227) over [-sl/2, sl/2)^2.  Returns the packed winner key.
+// FastBME (me.c:187-227) over [-sl/2, sl/2)^2.
 __device__ __forceinline__ void me_full(const MbLds &L, int w, int h, int x0, int y0, int sl,
                                         int lane, int sad0, int &mx, int &my, int &best) {
   const int half = lane >> 5, dxi = lane & 31;
@@ -299,18 +330,31 @@ __device__ __forceinline__ void me_full(const MbLds &L, int w, int h, int x0, in
   }
 
   // key = SAD<<11 | (1 + scan order); scan order (dx+15)*30+(dy+15) is
-  // FastBME's dx-major order; key 0-order (0) is reserved for the (0,0) vector,
-  // which wins every tie because it is evaluated first (me.c:203, 220).
+  // FastBME's dx-major order; order 0 is reserved for the (0,0) vector, which
+  // wins every tie because it is evaluated first (me.c:203, 220).
   const int hl = sl >> 1;
-  const int dx = dxi - 15, px = x0 + dx;
-  const bool col_ok = lane_ok && dx >= -hl && dx < hl && px >= 0 && px < w - 16;
+  const unsigned base = (unsigned)(dxi * 30 + 15 * half + 1);
   unsigned bk = 0xFFFFFFFFu;
+  const bool interior = hl == 15 && x0 >= 16 && x0 + 32 <= w && y0 >= 16 && y0 + 32 <= h;
+  if (interior) {  // every candidate of every working lane is inside the picture
 #pragma unroll
-  for (int d = 0; d < 15; d++) {
-    const int dy = -15 + 15 * half + d, py = y0 + dy;
-    const bool ok = col_ok && dy >= -hl && dy < hl && py >= 0 && py < h - 16;
-    const unsigned key = (acc[d] << 11) | (unsigned)(dxi * 30 + 15 * half + d + 1);
-    if (ok && key < bk) bk = key;
+    for (int d = 0; d < 15; d += 3) {
+      const unsigned k0 = (acc[d] << 11) + base + d;
+      const unsigned k1 = (acc[d + 1] << 11) + base + d + 1;
+      const unsigned k2 = (acc[d + 2] << 11) + base + d + 2;
+      bk = min(bk, min(k0, min(k1, k2)));
+    }
+    if (!lane_ok) bk = 0xFFFFFFFFu;
+  } else {
+    const int dx = dxi - 15, px = x0 + dx;
+    const bool col_ok = lane_ok && dx >= -hl && dx < hl && px >= 0 && px < w - 16;
+#pragma unroll
+    for (int d = 0; d < 15; d++) {
+      const int dy = -15 + 15 * half + d, py = y0 + dy;
+      const bool ok = col_ok && dy >= -hl && dy < hl && py >= 0 && py < h - 16;
+      const unsigned key = (acc[d] << 11) + base + d;
+      if (ok && key < bk) bk = key;
+    }
   }
   bk = min(wave_min(bk), (unsigned)sad0 << 11);
   const int ord = (int)(bk & 2047u);
@@ -378,22 +422,18 @@ __device__ __forceinline__ void me_tss(const MbLds &L, int w, int h, int x0, int
   best = (int)bsad;
 }
 
-// decision statistics on the chosen block (me.c:229-245 == 313-329)
+// decision statistics on the chosen block (me.c:229-245 == 313-329), with the
+// byte dot product: sum (r-c)^2 = r.r - 2 r.c + c.c, all exact in u32
 __device__ __forceinline__ void me_stats(const MbLds &L, int lane, MeOut &o) {
   const int colb = WIN_OX + o.mx + 4 * (lane & 3);
   const uint32_t *p = L.win + (WIN_OY + o.my + (lane >> 2)) * WIN_WORDS + (colb >> 2);
   const uint32_t rw = align4(p[1], p[0], colb & 3), cw = L.cur[lane];
-  int var = 0, sq = 0, sum = 0;
-#pragma unroll
-  for (int j = 0; j < 4; j++) {
-    const int rb = (rw >> (8 * j)) & 255, cb = (cw >> (8 * j)) & 255, d = rb - cb;
-    var += d * d;
-    sq += rb * rb;
-    sum += rb;
-  }
-  var = wave_sum(var);
-  sq = wave_sum(sq);
-  sum = wave_sum(sum);
+  const unsigned rr = __builtin_amdgcn_udot4(rw, rw, 0u, false);
+  const unsigned rc = __builtin_amdgcn_udot4(rw, cw, 0u, false);
+  const unsigned cc = __builtin_amdgcn_udot4(cw, cw, 0u, false);
+  const int var = wave_sum((int)(rr + cc - 2 * rc));
+  const int sq = wave_sum((int)rr);
+  const int sum = wave_sum((int)sad4(rw, 0u, 0u));
   o.var = var / 256;
   o.varor = sq / 256 - (sum / 256) * (sum / 256);
   o.mwor = sum;
@@ -426,39 +466,62 @@ __device__ __forceinline__ int decide_mtype(const MeOut &m) {
 }
 
 // ---------------------------------------------------------------------------
-// prediction of row r of block b (io.c:142-496).  SRC(rr, k) returns the
-// reference byte at row rr, column k relative to the block's compensated origin.
+// prediction (io.c:142-496), row layout: lane (b, r) computes row r of block b.
+// The 8 source bytes of the row arrive packed in (lo, hi).
 
-template <typename Src>
-__device__ __forceinline__ void pred_row(Src src, bool filter, int r, int p[8]) {
+__device__ __forceinline__ void unpack8(uint32_t lo, uint32_t hi, int v[8]) {
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    v[k] = (lo >> (8 * k)) & 255;
+    v[4 + k] = (hi >> (8 * k)) & 255;
+  }
+}
+// Values are taken through an empty asm first: on ROCm 7.2 hipcc fuses
+// "(x >> 4) clamped to 0..255, packed" into gfx950's v_ashr_pk_u8_i32 and then
+// ORs the packed pair into a dword whose upper half it assumes is zero, which
+// corrupted byte 3 on the hardware (tools/repro_ashr_pk.hip); the barrier keeps
+// the clamp and the pack as separate instructions.
+__device__ __forceinline__ int opaque(int v) {
+  asm volatile("" : "+v"(v));
+  return v;
+}
+__device__ __forceinline__ uint2 pack8(const int in[8]) {
+  int v[8];
+#pragma unroll
+  for (int k = 0; k < 8; k++) v[k] = opaque(in[k]);
+  uint2 q;
+  q.x = (uint32_t)v[0] | ((uint32_t)v[1] << 8) | ((uint32_t)v[2] << 16) | ((uint32_t)v[3] << 24);
+  q.y = (uint32_t)v[4] | ((uint32_t)v[5] << 8) | ((uint32_t)v[6] << 16) | ((uint32_t)v[7] << 24);
+  return q;
+}
+
+// MUST run on all 64 lanes (DPP): the vertical taps of the H.261 loop filter
+// (LoadFilterMatrix io.c:323-372) come from lanes r-1 / r+1 of the same block.
+__device__ __forceinline__ void pred_from_row(uint32_t lo, uint32_t hi, bool filter, int r,
+                                              int p[8]) {
+  int s[8];
+  unpack8(lo, hi, s);
   if (!filter) {
 #pragma unroll
-    for (int k = 0; k < 8; k++) p[k] = src(r, k);
+    for (int k = 0; k < 8; k++) p[k] = s[k];
     return;
   }
-  // LoadFilterMatrix (io.c:323-372)
-  int hz[3][8];
+  int hz[8];
+  hz[0] = s[0] << 2;
 #pragma unroll
-  for (int t = 0; t < 3; t++) {
-    const int rr = min(max(r - 1 + t, 0), 7);
-    int s[8];
-#pragma unroll
-    for (int k = 0; k < 8; k++) s[k] = src(rr, k);
-    hz[t][0] = s[0] << 2;
-#pragma unroll
-    for (int k = 1; k < 7; k++) hz[t][k] = s[k - 1] + 2 * s[k] + s[k + 1];
-    hz[t][7] = s[7] << 2;
-  }
-  const bool edge = r == 0 || r == 7;
+  for (int k = 1; k < 7; k++) hz[k] = s[k - 1] + 2 * s[k] + s[k + 1];
+  hz[7] = s[7] << 2;
+  const bool edge = r == 0 || r == 7;  // rows 0 and 7 are not filtered vertically
 #pragma unroll
   for (int k = 0; k < 8; k++) {
-    const int v = edge ? hz[1][k] : (hz[0][k] + 2 * hz[1][k] + hz[2][k]) >> 2;
-    p[k] = (v & 2) ? (v >> 2) + 1 : (v >> 2);
+    const int up = from_prev_lane(hz[k]), dn = from_next_lane(hz[k]);
+    const int v = edge ? hz[k] : (up + 2 * hz[k] + dn) >> 2;
+    p[k] = (v + 2) >> 2;  // == (v & 2) ? (v >> 2) + 1 : v >> 2 for v >= 0
   }
 }
 
-// compensated origin of block b for MTYPE mt (MoveTo io.c:719-747; luma MV,
-// chroma MV/2 with C truncation io.c:268-270; zero vector for non-MC types)
+// compensated block geometry (MoveTo io.c:719-747): luma MV, chroma MV/2 with
+// C truncation (io.c:268-270), zero vector for non-MC types
 struct BlockGeom {
   int plane;  // 0 Y, 1 U, 2 V
   int x, y;   // block origin in its plane
@@ -477,57 +540,64 @@ __device__ __forceinline__ BlockGeom block_geom(int b, int mbx, int mby) {
   return g;
 }
 
-__device__ __forceinline__ void read_row8(const uint8_t *p, int v[8]) {
-  const uint2 q = *reinterpret_cast<const uint2 *>(p);
-#pragma unroll
-  for (int k = 0; k < 4; k++) {
-    v[k] = (q.x >> (8 * k)) & 255;
-    v[4 + k] = (q.y >> (8 * k)) & 255;
-  }
-}
-__device__ __forceinline__ void write_row8(uint8_t *p, const int v[8]) {
-  uint2 q;
-  q.x = (uint32_t)v[0] | ((uint32_t)v[1] << 8) | ((uint32_t)v[2] << 16) | ((uint32_t)v[3] << 24);
-  q.y = (uint32_t)v[4] | ((uint32_t)v[5] << 8) | ((uint32_t)v[6] << 16) | ((uint32_t)v[7] << 24);
-  *reinterpret_cast<uint2 *>(p) = q;
+// stage the two 8x8 chroma prediction sources of this MB at the compensated
+// origin (one byte pair per lane)
+__device__ __forceinline__ void stage_chroma(MbLds &L, const Picture &ref, int w, int mbx, int mby,
+                                             int mt, int mvx, int mvy, int lane) {
+  const int cw = w >> 1;
+  const bool mf = mt_mf(mt);
+  const int ox = 8 * mbx + (mf ? mvx / 2 : 0), oy = 8 * mby + (mf ? mvy / 2 : 0);
+  const int pl = lane >> 5, row = (lane >> 2) & 7, c2 = (lane & 3) * 2;
+  const uint8_t *src = (pl ? ref.v : ref.u) + (oy + row) * cw + ox + c2;
+  const uint32_t v = (uint32_t)src[0] | ((uint32_t)src[1] << 8);
+  reinterpret_cast<uint16_t *>(L.cpred)[pl * 32 + row * 4 + (c2 >> 1)] = (uint16_t)v;
 }
 
-// Prediction from LDS (luma) / global (chroma) for the encoder.
-__device__ __forceinline__ void predict_enc(const MbLds &L, const Picture &ref, int w, int b,
-                                            int mbx, int mby, int r, int mt, int mvx, int mvy,
+// prediction row for the encoder: luma from the LDS search window, chroma from
+// the staged sources.  All 64 lanes execute (lanes b >= 6 compute garbage).
+__device__ __forceinline__ void predict_row(const MbLds &L, int b, int r, int mt, int mvx, int mvy,
                                             int p[8]) {
-  const bool mf = mt_mf(mt), filt = mt_filter(mt);
+  const bool mf = mt_mf(mt);
+  uint32_t lo, hi;
   if (b < 4) {
-    const uint8_t *wb = reinterpret_cast<const uint8_t *>(L.win);
-    const int ox = WIN_OX + 8 * (b & 1) + (mf ? mvx : 0);
-    const int oy = WIN_OY + 8 * (b >> 1) + (mf ? mvy : 0);
-    pred_row([&](int rr, int k) { return (int)wb[(oy + rr) * WIN_BYTES + ox + k]; }, filt, r, p);
+    const int col = WIN_OX + 8 * (b & 1) + (mf ? mvx : 0);
+    const int row = WIN_OY + 8 * (b >> 1) + (mf ? mvy : 0) + r;
+    const uint32_t *q = L.win + row * WIN_WORDS + (col >> 2);
+    const uint32_t a0 = q[0], a1 = q[1], a2 = q[2];
+    lo = align4(a1, a0, col & 3);
+    hi = align4(a2, a1, col & 3);
   } else {
-    const int cw = w / 2;
-    const uint8_t *pl = b == 4 ? ref.u : ref.v;
-    const int ox = 8 * mbx + (mf ? mvx / 2 : 0), oy = 8 * mby + (mf ? mvy / 2 : 0);
-    const uint8_t *base = pl + (size_t)oy * cw + ox;
-    pred_row([&](int rr, int k) { return (int)base[(size_t)rr * cw + k]; }, filt, r, p);
+    const uint32_t *q = L.cpred + (b - 4) * 16 + r * 2;
+    lo = q[0];
+    hi = q[1];
   }
+  pred_from_row(lo, hi, mt_filter(mt), r, p);
 }
 
-// Prediction straight from global memory (decoder recon).
-__device__ __forceinline__ void predict_glb(const Picture &ref, int w, int b, int mbx, int mby,
-                                            int r, int mt, int mvx, int mvy, int p[8]) {
-  const bool mf = mt_mf(mt), filt = mt_filter(mt);
+// prediction row straight from global memory (decoder)
+__device__ __forceinline__ void predict_row_glb(const Picture &ref, int w, int b, int mbx, int mby,
+                                                int r, int mt, int mvx, int mvy, int p[8]) {
+  const bool mf = mt_mf(mt);
   const BlockGeom g = block_geom(b, mbx, mby);
   const int pw = g.plane ? w / 2 : w;
   const uint8_t *pl = g.plane == 0 ? ref.y : (g.plane == 1 ? ref.u : ref.v);
   const int dx = mf ? (g.plane ? mvx / 2 : mvx) : 0, dy = mf ? (g.plane ? mvy / 2 : mvy) : 0;
-  const uint8_t *base = pl + (size_t)(g.y + dy) * pw + g.x + dx;
-  pred_row([&](int rr, int k) { return (int)base[(size_t)rr * pw + k]; }, filt, r, p);
+  const uint8_t *src = pl + (g.y + dy + r) * pw + g.x + dx;
+  uint32_t lo = 0, hi = 0;
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    lo |= (uint32_t)src[k] << (8 * k);
+    hi |= (uint32_t)src[4 + k] << (8 * k);
+  }
+  pred_from_row(lo, hi, mt_filter(mt), r, p);
 }
 
 // ---------------------------------------------------------------------------
-// forward transform + quantisation of row r of block b (lanes 0..47 active)
+// transforms through the LDS scratch (lanes b < 6 active in row/column passes)
 
-__device__ __forceinline__ void dct_quant_rows(MbLds &L, bool act, int b, int r, const int res[8],
-                                               bool intra, int q, unsigned magic, int lev[8]) {
+// rows res[8] of block b -> forward 2-D transform -> raw (pre-/8) coefficients
+// left in L.blk in natural order
+__device__ __forceinline__ void forward_2d(MbLds &L, bool act, int b, int r, const int res[8]) {
   int *B = L.blk + b * BLK_STRIDE;
   if (act) {
 #pragma unroll
@@ -538,47 +608,31 @@ __device__ __forceinline__ void dct_quant_rows(MbLds &L, bool act, int b, int r,
     int x[8], o[8];
 #pragma unroll
     for (int k = 0; k < 8; k++) x[k] = B[k * ROW_STRIDE + r];
-    fwd_col(x, o);
+    fwd_col<true>(x, o);
 #pragma unroll
     for (int k = 0; k < 8; k++) B[k * ROW_STRIDE + r] = o[k];
   }
   __syncthreads();
-  int x[8], o[8];
-#pragma unroll
-  for (int k = 0; k < 8; k++) x[k] = act ? B[r * ROW_STRIDE + k] : 0;
-  fwd_row(x, o);
-#pragma unroll
-  for (int k = 0; k < 8; k++) {
-    int v = dct_final(o[k]);
-    const bool dc = (r == 0 && k == 0);
-    v = dc ? min(v, 2047) : clampi(v, -1023, 1023);  // BoundDctMatrix
-    if (intra) {
-      v = dc ? clampi(qdc_intra(v, 8), 1, 254) : clampi(qlevel<true>(v, q, magic), -127, 127);
-    } else {
-      v = clampi(qlevel<true>(v, q, magic), -127, 127);
-    }
-    lev[k] = act ? v : 0;
-  }
-}
-
-// dequantisation + inverse transform of row r of block b -> residual res[8]
-__device__ __forceinline__ void iq_idct_rows(MbLds &L, bool act, bool coded, int b, int r,
-                                             const int lev[8], bool intra, int q, int res[8]) {
-  int *B = L.blk + b * BLK_STRIDE;
-  __syncthreads();  // previous users of blk are done
   if (act) {
+    int x[8], o[8];
 #pragma unroll
-    for (int k = 0; k < 8; k++) {
-      const bool dc = (r == 0 && k == 0);
-      B[r * ROW_STRIDE + k] = (intra && dc) ? lev[k] * 8 : rlevel(lev[k], q);
-    }
+    for (int k = 0; k < 8; k++) x[k] = B[r * ROW_STRIDE + k];
+    fwd_row<true>(x, o);
+#pragma unroll
+    for (int k = 0; k < 8; k++) B[r * ROW_STRIDE + k] = o[k];
   }
   __syncthreads();
+}
+
+// dequantised blocks in L.blk (natural order) -> inverse 2-D transform -> row r
+// of block b's residual
+__device__ __forceinline__ void inverse_2d(MbLds &L, bool act, int b, int r, int res[8]) {
+  int *B = L.blk + b * BLK_STRIDE;
   if (act) {  // column pass: inputs <<2
     int x[8], o[8];
 #pragma unroll
     for (int k = 0; k < 8; k++) x[k] = B[k * ROW_STRIDE + r] << 2;
-    inv8(x, o);
+    inv8<true>(x, o);
 #pragma unroll
     for (int k = 0; k < 8; k++) B[k * ROW_STRIDE + r] = o[k];
   }
@@ -586,9 +640,50 @@ __device__ __forceinline__ void iq_idct_rows(MbLds &L, bool act, bool coded, int
   int x[8], o[8];
 #pragma unroll
   for (int k = 0; k < 8; k++) x[k] = act ? B[r * ROW_STRIDE + k] : 0;
-  inv8(x, o);
+  inv8<true>(x, o);
 #pragma unroll
-  for (int k = 0; k < 8; k++) res[k] = (act && coded) ? idct_final(o[k]) : 0;
+  for (int k = 0; k < 8; k++) res[k] = idct_final(o[k]);
+}
+
+// element layout: lane e holds natural coefficient e of each block k
+__device__ __forceinline__ int blk_at(const MbLds &L, int k, int e) {
+  return L.blk[k * BLK_STRIDE + (e >> 3) * ROW_STRIDE + (e & 7)];
+}
+__device__ __forceinline__ void blk_put(MbLds &L, int k, int e, int v) {
+  L.blk[k * BLK_STRIDE + (e >> 3) * ROW_STRIDE + (e & 7)] = v;
+}
+
+// BoundDctMatrix + CCITT(Flat)Quantize + (Flat)BoundQuantizeMatrix of one raw
+// coefficient (transform.c:271-350, 460-537)
+__device__ __forceinline__ int quantise(int raw, bool dc, bool intra, int q, unsigned magic) {
+  int v = dct_final(raw);
+  v = dc ? min(v, 2047) : clampi(v, -1023, 1023);
+  if (intra && dc) return clampi(qdc_intra(v, 8), 1, 254);
+  return clampi(qlevel<true>(v, q, magic), -127, 127);
+}
+__device__ __forceinline__ int dequantise(int lev, bool dc, bool intra, int q) {
+  return (intra && dc) ? lev * 8 : rlevel<true>(lev, q);  // ICCITT(Flat)Quantize
+}
+
+// CBP decision from the six blocks' levels (p64.c:887-908), with wave ballots:
+// sum|level| > 1 <=> two or more nonzero levels, or one of magnitude > 1.
+struct CbpOut {
+  int cbp;       // CBP bits, block c -> bit 5-c
+  bool nothing;  // no block has any nonzero level
+};
+__device__ __forceinline__ CbpOut cbp_decide(const int lev[6]) {
+  int cbp = 0, pmask = 0;
+#pragma unroll
+  for (int k = 0; k < 6; k++) {
+    const uint64_t nz = __ballot(lev[k] != 0);
+    const uint64_t big = __ballot(lev[k] > 1 || lev[k] < -1);
+    if (nz && !pmask) pmask = 1 << (5 - k);
+    if (big || __popcll(nz) >= 2) cbp |= 1 << (5 - k);
+  }
+  CbpOut o;
+  o.nothing = pmask == 0;
+  o.cbp = cbp ? cbp : pmask;
+  return o;
 }
 
 // ---------------------------------------------------------------------------
@@ -601,12 +696,21 @@ __global__ __launch_bounds__(64) void k_encode(p64gpu_encode_args a) {
   __shared__ MbLds L;
   const int lane = threadIdx.x;
   const int w = a.width, h = a.height, mbw = w >> 4, nmb = mbw * (h >> 4);
-  const int fi = blockIdx.x / nmb, mb = blockIdx.x - fi * nmb;
+  const unsigned gid = xcd_remap(blockIdx.x, gridDim.x);
+  const int fi = (int)(gid / (unsigned)nmb), mb = (int)(gid - (unsigned)fi * nmb);
   const int mbx = mb % mbw, mby = mb / mbw, x0 = 16 * mbx, y0 = 16 * mby;
   const size_t gmb = (size_t)fi * nmb + mb;
   const Picture cur = picture_at(a.cur + (size_t)fi * a.frame_stride, w, h);
   const Picture ref = picture_at(a.ref + (size_t)fi * a.frame_stride, w, h);
   uint8_t *rec = a.recon + (size_t)fi * a.frame_stride;
+
+  // row layout coordinates (lanes 48..63 shadow block 5 and are masked)
+  const int b = min(lane >> 3, 5), r = lane & 7;
+  const bool act = lane < 48;
+  const BlockGeom g = block_geom(b, mbx, mby);
+  const int pw = g.plane ? w >> 1 : w;
+  const uint8_t *cplane = g.plane == 0 ? cur.y : (g.plane == 1 ? cur.u : cur.v);
+  const uint2 crow = *reinterpret_cast<const uint2 *>(cplane + (g.y + r) * pw + g.x);
 
   int mt = 0, mvx = 0, mvy = 0;
   if (MODE != 0) {
@@ -614,15 +718,15 @@ __global__ __launch_bounds__(64) void k_encode(p64gpu_encode_args a) {
     __syncthreads();
     const MeOut me = motion_estimate<MODE>(L, w, h, x0, y0, a.search_limit, lane);
     if (a.me && lane == 0) {
-      p64_me_rec r;
-      r.mx = me.mx;
-      r.my = me.my;
-      r.sad = me.sad;
-      r.sad0 = me.sad0;
-      r.var = me.var;
-      r.varor = me.varor;
-      r.mwor = me.mwor;
-      a.me[gmb] = r;
+      p64_me_rec o;
+      o.mx = me.mx;
+      o.my = me.my;
+      o.sad = me.sad;
+      o.sad0 = me.sad0;
+      o.var = me.var;
+      o.varor = me.varor;
+      o.mwor = me.mwor;
+      a.me[gmb] = o;
     }
     mt = decide_mtype(me);
     if (a.mtype_override) {
@@ -637,78 +741,65 @@ __global__ __launch_bounds__(64) void k_encode(p64gpu_encode_args a) {
   const int q = a.quant_mb ? a.quant_mb[gmb] : a.quant;
   const unsigned magic = quant_magic(q);
 
-  const int b = lane >> 3, r = lane & 7;
-  const bool act = b < 6;
-  const BlockGeom g = block_geom(act ? b : 0, mbx, mby);
-  const int pw = g.plane ? w / 2 : w;
-
   int pred[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  if (!mt_intra(mt) && act) predict_enc(L, ref, w, b, mbx, mby, r, mt, mvx, mvy, pred);
+  if (!mt_intra(mt)) {
+    stage_chroma(L, ref, w, mbx, mby, mt, mvx, mvy, lane);
+    __syncthreads();
+    predict_row(L, b, r, mt, mvx, mvy, pred);
+  }
 
-  // ReadCompressMDU (p64.c:830-912)
-  int lev[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  const bool intra = mt_intra(mt);
+  // ReadCompressMDU (p64.c:830-912): levels in element layout
+  const int e = lane;
+  int lev[6] = {0, 0, 0, 0, 0, 0};
+  bool intra = mt_intra(mt);
   if (mt_tcoeff(mt)) {
-    int res[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    if (act) {
-      const uint8_t *pl = g.plane == 0 ? cur.y : (g.plane == 1 ? cur.u : cur.v);
-      read_row8(pl + (size_t)(g.y + r) * pw + g.x, res);
-      if (!intra) {
+    int res[8];
+    unpack8(crow.x, crow.y, res);
 #pragma unroll
-        for (int k = 0; k < 8; k++) res[k] -= pred[k];
-      }
-    }
-    dct_quant_rows(L, act, b, r, res, intra, q, magic, lev);
+    for (int k = 0; k < 8; k++) res[k] -= pred[k];
+    forward_2d(L, act, b, r, res);
+#pragma unroll
+    for (int k = 0; k < 6; k++) lev[k] = quantise(blk_at(L, k, e), e == 0, intra, q, magic);
   }
   int cbp = 0x3f;
   if (mt_cbp(mt)) {
-    int acc = 0;
-#pragma unroll
-    for (int k = 0; k < 8; k++) acc += abs(lev[k]);
-    acc += __shfl_xor(acc, 1);
-    acc += __shfl_xor(acc, 2);
-    acc += __shfl_xor(acc, 4);
-    int pmask = 0;
-    cbp = 0;
-#pragma unroll
-    for (int c = 0; c < 6; c++) {
-      const int s = __shfl(acc, 8 * c);
-      if (s && !pmask) pmask = 1 << (5 - c);
-      if (s > 1) cbp |= 1 << (5 - c);  // CBPThreshold = 1 (p64.c:151)
-    }
-    if (!cbp) {
-      if (pmask) {
-        cbp = pmask;
-      } else {  // no coefficients: MC without coefficients, ME vector kept
-        const int old = mt;
-        mt = mt_filter(mt) ? 7 : 4;
-        cbp = 0x3f;
-#pragma unroll
-        for (int k = 0; k < 8; k++) lev[k] = 0;
-        if (!mt_mf(old) && act) predict_enc(L, ref, w, b, mbx, mby, r, mt, mvx, mvy, pred);
+    const CbpOut c = cbp_decide(lev);
+    cbp = c.cbp;
+    if (c.nothing) {  // no coefficients: MC without coefficients, ME vector kept
+      const int old = mt;
+      mt = mt_filter(mt) ? 7 : 4;
+      cbp = 0x3f;
+      if (!mt_mf(old)) {  // 2/3 -> 4 switches from the zero vector to the ME vector
+        __syncthreads();
+        stage_chroma(L, ref, w, mbx, mby, mt, mvx, mvy, lane);
+        __syncthreads();
+        predict_row(L, b, r, mt, mvx, mvy, pred);
       }
     }
   }
-
-  // levels -> LDS in zigzag order -> global (768 B per MB)
-  if (act) {
+  const int zpos = c_zz.pos[e];
+  __syncthreads();  // element reads of blk are complete before it is rewritten
+  int coded = 0;
 #pragma unroll
-    for (int k = 0; k < 8; k++) L.zz[b * 64 + c_zz.pos[r * 8 + k]] = (int16_t)lev[k];
+  for (int k = 0; k < 6; k++) {
+    L.zz[k * 64 + zpos] = (int16_t)lev[k];
+    const bool ck = ((cbp >> (5 - k)) & 1) && mt_tcoeff(mt);
+    coded |= ck ? 1 << k : 0;
+    blk_put(L, k, e, ck ? dequantise(lev[k], e == 0, mt_intra(mt), q) : 0);
   }
   __syncthreads();
   if (lane < 48)
     reinterpret_cast<uint4 *>(a.coef + gmb * 384)[lane] = reinterpret_cast<const uint4 *>(L.zz)[lane];
 
   // reconstruction (p64.c:945-959, 971-1013)
-  const bool coded = act && ((cbp >> (5 - b)) & 1) && mt_tcoeff(mt);
-  int res[8];
-  iq_idct_rows(L, act, coded, b, r, lev, mt_intra(mt), q, res);
+  int res[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (coded) inverse_2d(L, act, b, r, res);
   if (act) {
     const bool add = !mt_intra(mt);
 #pragma unroll
     for (int k = 0; k < 8; k++) res[k] = clampi(res[k] + (add ? pred[k] : 0), 0, 255);
-    uint8_t *pl = rec + (g.plane == 0 ? 0 : (size_t)w * h + (size_t)(g.plane - 1) * (w / 2) * (h / 2));
-    write_row8(pl + (size_t)(g.y + r) * pw + g.x, res);
+    uint8_t *pl = rec + (g.plane == 0 ? 0 : w * h + (g.plane - 1) * (w >> 1) * (h >> 1));
+    *reinterpret_cast<uint2 *>(pl + (g.y + r) * pw + g.x) = pack8(res);
   }
   if (lane == 0) {
     p64_mb_rec o;
@@ -728,25 +819,27 @@ __global__ __launch_bounds__(64) void k_motion(int w, int h, int64_t stride, con
   __shared__ MbLds L;
   const int lane = threadIdx.x;
   const int mbw = w >> 4, nmb = mbw * (h >> 4);
-  const int fi = blockIdx.x / nmb, mb = blockIdx.x - fi * nmb;
+  const unsigned gid = xcd_remap(blockIdx.x, gridDim.x);
+  const int fi = (int)(gid / (unsigned)nmb), mb = (int)(gid - (unsigned)fi * nmb);
   const int x0 = 16 * (mb % mbw), y0 = 16 * (mb / mbw);
   stage_luma(L, ref_y + (size_t)fi * stride, cur_y + (size_t)fi * stride, w, h, x0, y0, lane);
   __syncthreads();
   const MeOut me = motion_estimate<MODE>(L, w, h, x0, y0, sl, lane);
   if (lane == 0) {
-    p64_me_rec r;
-    r.mx = me.mx;
-    r.my = me.my;
-    r.sad = me.sad;
-    r.sad0 = me.sad0;
-    r.var = me.var;
-    r.varor = me.varor;
-    r.mwor = me.mwor;
-    out[(size_t)fi * nmb + mb] = r;
+    p64_me_rec o;
+    o.mx = me.mx;
+    o.my = me.my;
+    o.sad = me.sad;
+    o.sad0 = me.sad0;
+    o.var = me.var;
+    o.varor = me.varor;
+    o.mwor = me.mwor;
+    out[(size_t)fi * nmb + mb] = o;
   }
 }
 
-// decoder-side reconstruction of coded macroblocks
+// decoder-side reconstruction of coded macroblocks (DecompressMDU p64.c:1179 +
+// DecodeSaveMDU p64.c:971)
 __global__ __launch_bounds__(64) void k_decode_recon(int w, int h, int64_t stride,
                                                      const uint8_t *refp, uint8_t *recp,
                                                      const int16_t *coef, const p64_mb_rec *mbr,
@@ -755,7 +848,8 @@ __global__ __launch_bounds__(64) void k_decode_recon(int w, int h, int64_t strid
   __shared__ MbLds L;
   const int lane = threadIdx.x;
   const int mbw = w >> 4, nmb = mbw * (h >> 4);
-  const int fi = blockIdx.x / nmb, mb = blockIdx.x - fi * nmb;
+  const unsigned gid = xcd_remap(blockIdx.x, gridDim.x);
+  const int fi = (int)(gid / (unsigned)nmb), mb = (int)(gid - (unsigned)fi * nmb);
   const size_t gmb = (size_t)fi * nmb + mb;
   if (!coded_mask[gmb]) return;  // whole workgroup exits together
   const int mbx = mb % mbw, mby = mb / mbw;
@@ -764,28 +858,34 @@ __global__ __launch_bounds__(64) void k_decode_recon(int w, int h, int64_t strid
   const p64_mb_rec m = mbr[gmb];
   const int mt = m.mtype, q = quant_mb[gmb];
   const int cbp = mt_cbp(mt) ? m.cbp : 0x3f;  // p64.c:1200
-  const int b = lane >> 3, r = lane & 7;
-  const bool act = b < 6;
-  const BlockGeom g = block_geom(act ? b : 0, mbx, mby);
+  const int b = min(lane >> 3, 5), r = lane & 7;
+  const bool act = lane < 48;
+  const BlockGeom g = block_geom(b, mbx, mby);
   const int pw = g.plane ? w / 2 : w;
-  int lev[8];
+  const int e = lane, zpos = c_zz.pos[e];
+  int coded = 0;
 #pragma unroll
-  for (int k = 0; k < 8; k++) lev[k] = act ? coef[gmb * 384 + b * 64 + c_zz.pos[r * 8 + k]] : 0;
-  const bool coded = act && ((cbp >> (5 - b)) & 1) && mt_tcoeff(mt);
-  int res[8];
-  iq_idct_rows(L, act, coded, b, r, lev, mt_intra(mt), q, res);
+  for (int k = 0; k < 6; k++) {
+    const bool ck = ((cbp >> (5 - k)) & 1) && mt_tcoeff(mt);
+    coded |= ck ? 1 << k : 0;
+    const int lev = ck ? coef[gmb * 384 + k * 64 + zpos] : 0;  // IZigzagMatrix
+    blk_put(L, k, e, ck ? dequantise(lev, e == 0, mt_intra(mt), q) : 0);
+  }
+  int pred[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (!mt_intra(mt)) predict_row_glb(ref, w, b, mbx, mby, r, mt, m.mvx, m.mvy, pred);
+  __syncthreads();
+  int res[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (coded) inverse_2d(L, act, b, r, res);
   if (act) {
-    int pred[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    if (!mt_intra(mt)) predict_glb(ref, w, b, mbx, mby, r, mt, m.mvx, m.mvy, pred);
 #pragma unroll
     for (int k = 0; k < 8; k++) res[k] = clampi(res[k] + pred[k], 0, 255);
-    uint8_t *pl = rec + (g.plane == 0 ? 0 : (size_t)w * h + (size_t)(g.plane - 1) * (w / 2) * (h / 2));
-    write_row8(pl + (size_t)(g.y + r) * pw + g.x, res);
+    uint8_t *pl = rec + (g.plane == 0 ? 0 : w * h + (g.plane - 1) * (w / 2) * (h / 2));
+    *reinterpret_cast<uint2 *>(pl + (g.y + r) * pw + g.x) = pack8(res);
   }
 }
 
 // batched 8x8 block operations (one thread per block; shares the device
-// functions of the fused kernel)
+// functions of the fused kernels, full 32-bit arithmetic for arbitrary input)
 __global__ void k_block_op(int op, const int32_t *in, int32_t *out, int64_t nblocks, int dcq,
                            int acq) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -799,12 +899,12 @@ __global__ void k_block_op(int op, const int32_t *in, int32_t *out, int64_t nblo
       int x[8], o[8];
       for (int c = 0; c < 8; c++) {
         for (int k = 0; k < 8; k++) x[k] = m[8 * k + c];
-        fwd_col(x, o);
+        fwd_col<false>(x, o);
         for (int k = 0; k < 8; k++) t[8 * k + c] = o[k];
       }
       for (int rr = 0; rr < 8; rr++) {
         for (int k = 0; k < 8; k++) x[k] = t[8 * rr + k];
-        fwd_row(x, o);
+        fwd_row<false>(x, o);
         for (int k = 0; k < 8; k++) m[8 * rr + k] = dct_final(o[k]);
       }
       break;
@@ -813,12 +913,12 @@ __global__ void k_block_op(int op, const int32_t *in, int32_t *out, int64_t nblo
       int x[8], o[8];
       for (int c = 0; c < 8; c++) {
         for (int k = 0; k < 8; k++) x[k] = m[8 * k + c] << 2;
-        inv8(x, o);
+        inv8<false>(x, o);
         for (int k = 0; k < 8; k++) t[8 * k + c] = o[k];
       }
       for (int rr = 0; rr < 8; rr++) {
         for (int k = 0; k < 8; k++) x[k] = t[8 * rr + k];
-        inv8(x, o);
+        inv8<false>(x, o);
         for (int k = 0; k < 8; k++) m[8 * rr + k] = idct_final(o[k]);
       }
       break;
@@ -833,11 +933,11 @@ __global__ void k_block_op(int op, const int32_t *in, int32_t *out, int64_t nblo
       break;
     case P64GPU_OP_IQUANT_INTRA:
       m[0] = m[0] * dcq;
-      for (int n = 1; n < 64; n++) m[n] = rlevel(m[n], acq);
+      for (int n = 1; n < 64; n++) m[n] = rlevel<false>(m[n], acq);
       break;
     case P64GPU_OP_IQUANT_INTER:
-      m[0] = rlevel(m[0], dcq);
-      for (int n = 1; n < 64; n++) m[n] = rlevel(m[n], acq);
+      m[0] = rlevel<false>(m[0], dcq);
+      for (int n = 1; n < 64; n++) m[n] = rlevel<false>(m[n], acq);
       break;
     case P64GPU_OP_BOUND_DCT:
       m[0] = min(m[0], 2047);

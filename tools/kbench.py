@@ -1,0 +1,63 @@
+"""Per-kernel timing on the bench workload (development aid, GPU box).
+
+Times, on S CIF sequences resident in HBM: the fused encode (FULL and TSS),
+motion estimation alone (FULL and TSS), and the intra-picture encode, each as
+the median of R launches bracketed by HIP events on torch's stream.
+"""
+import argparse
+import os
+import statistics
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+import p64_amd  # noqa: E402
+
+
+def timed(fn, reps):
+    ts = []
+    for _ in range(reps):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        fn()
+        b.record()
+        torch.cuda.synchronize()
+        ts.append(a.elapsed_time(b) * 1e3)
+    return statistics.median(ts), min(ts)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--streams", type=int, default=256)
+    ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--width", type=int, default=352)
+    ap.add_argument("--height", type=int, default=288)
+    a = ap.parse_args()
+    w, h, S = a.width, a.height, a.streams
+    nmb = (w // 16) * (h // 16)
+    pic = w * h * 3 // 2
+    fr = p64_amd.synth_frames_device(w, h, 1, S, 0, 3)
+    li = torch.zeros(S * nmb, dtype=torch.uint8, device="cuda")
+    r0 = torch.zeros(S * pic, dtype=torch.uint8, device="cuda")
+    r1 = torch.zeros_like(r0)
+    out = p64_amd.FrameBatchOut(coef=torch.empty((S, nmb, 6, 64), dtype=torch.int16, device="cuda"),
+                                mb=torch.empty((S, nmb, 4), dtype=torch.int8, device="cuda"),
+                                me=torch.empty((S, nmb, 7), dtype=torch.int32, device="cuda"))
+    p64_amd.encode_frames(fr[0].reshape(-1), None, r0, li, width=w, height=h, intra=True, out=out)
+    torch.cuda.synchronize()
+    res = {}
+    res["intra_encode"] = timed(lambda: p64_amd.encode_frames(
+        fr[0].reshape(-1), None, r1, li, width=w, height=h, intra=True, out=out), a.reps)
+    for mode, name in ((p64_amd.ME_FULL, "full"), (p64_amd.ME_TSS, "tss")):
+        res[f"fused_{name}"] = timed(lambda: p64_amd.encode_frames(
+            fr[1].reshape(-1), r0, r1, li, width=w, height=h, intra=False, me_mode=mode,
+            search_limit=31, out=out), a.reps)
+        res[f"me_only_{name}"] = timed(lambda: p64_amd.MotionEstimation(
+            r0, fr[1].reshape(-1), w, h, mode=mode, search_limit=31), a.reps)
+    for k, (med, mn) in res.items():
+        print(f"{k:16s} median {med:9.1f} us  min {mn:9.1f} us  {S * nmb / med * 1e6 / 1e6:8.1f} M MB/s")
+
+
+if __name__ == "__main__":
+    main()
