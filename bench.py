@@ -27,7 +27,6 @@ from __future__ import annotations
 import argparse
 import json
 import os
-import shutil
 import subprocess
 import sys
 import tempfile
@@ -38,9 +37,11 @@ sys.path.insert(0, REPO)
 
 METRIC = "macroblocks/s (full-search ME+DCT+quant), CIF inter; % HBM roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
-# v_sad_u8: 4 byte-absolute-differences per lane; 256 CUs x 4 SIMD32 x 32 lanes
-# per clock at 2.4 GHz (MI355X_MICROARCH.md: 4 SIMD-32 per CU, 2400 MHz)
-SAD_PEAK = 256 * 4 * 32 * 4 * 2.4e9
+# v_sad_u8 = 4 byte-absolute-differences per lane.  It issues at HALF rate on
+# gfx950 (tools/ubench_sad.hip: 0.57e12 wave-instr/s chip-wide = 4 cycles per
+# wave64 instruction per SIMD), so the ceiling is 256 CUs x 4 SIMDs x 16 lanes
+# per clock x 4 B x 2.4 GHz (MI355X_MICROARCH.md chip table).
+SAD_PEAK = 256 * 4 * 16 * 4 * 2.4e9
 # algorithmic HBM bytes per macroblock of the fused kernel:
 #   read  cur 384 + previous recon 384 + last_intra 1
 #   write coef 768 + recon 384 + p64_mb_rec 4 + p64_me_rec 28 + last_intra 1
@@ -69,6 +70,23 @@ def parse():
 def shard_seeds(rank: int, streams: int) -> tuple[int, int]:
     """Weak scaling: rank r owns sequences seed0 .. seed0+streams-1."""
     return 1 + rank * streams, streams
+
+
+def max_over_ranks(value: float, world: int, device=None) -> float:
+    """MAX of a per-rank float over the process group (identity at world 1)."""
+    if world == 1:
+        return value
+    import torch
+    import torch.distributed as dist
+
+    t = torch.tensor([value], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def aggregate_rate(world: int, units_per_rank_step: int, steps: int, tmax: float) -> float:
+    """Whole-job throughput: every rank's units over the slowest rank's time."""
+    return world * units_per_rank_step * steps / tmax
 
 
 # ---------------------------------------------------------------------------
@@ -205,10 +223,7 @@ def main():
     elapsed = time.perf_counter() - t0
     kern = [ev[k].elapsed_time(ev[k + 1]) * 1e-3 for k in range(args.steps)]
     kavg = sum(kern) / len(kern)
-    tmax = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-    if world > 1:
-        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
-    tmax = float(tmax.item())
+    tmax = max_over_ranks(elapsed, world, device="cuda")
 
     verified = None
     if rank == 0 and not args.no_verify:
@@ -237,7 +252,7 @@ def main():
         return
 
     mbs_launch = S * nmb
-    value = world * mbs_launch * args.steps / tmax
+    value = aggregate_rate(world, mbs_launch, args.steps, tmax)
     bytes_launch = mbs_launch * BYTES_PER_MB
     hbm_gbs = bytes_launch / kavg / 1e9
     cand = 900 if args.mode == "full" else 33

@@ -90,10 +90,16 @@ int p64gpu_abi_version(void);
 const char *p64gpu_strerror(int status);
 const char *p64gpu_last_error(void);
 
-/* ---- device selection / stream helpers (for C hosts without a runtime) ---- */
+/* ---- device selection, memory and stream helpers (C hosts need no HIP
+ * headers: these wrap hipGetDeviceCount/hipSetDevice/hipMalloc/hipFree/
+ * hipMemcpyAsync/hipStreamSynchronize) ---- */
 int p64gpu_device_count(int *count);
 int p64gpu_set_device(int device);
 int p64gpu_synchronize(void *stream);
+int p64gpu_alloc(void **ptr, size_t bytes);
+int p64gpu_free(void *ptr);
+int p64gpu_copy_to_device(void *dst, const void *src, size_t bytes, void *stream);
+int p64gpu_copy_to_host(void *dst, const void *src, size_t bytes, void *stream);
 
 /* ---- 8x8 block operations, batched (device pointers) -------------------- */
 enum p64gpu_block_op {

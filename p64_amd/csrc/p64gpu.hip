@@ -1050,6 +1050,31 @@ int p64gpu_synchronize(void *stream) {
   return P64GPU_OK;
 }
 
+int p64gpu_alloc(void **ptr, size_t bytes) {
+  if (!ptr) return fail(P64GPU_E_INVALID, "ptr is NULL");
+  *ptr = nullptr;
+  if (hipMalloc(ptr, bytes ? bytes : 1) != hipSuccess)
+    return fail(P64GPU_E_NOMEM, "hipMalloc(%zu) failed", bytes);
+  return P64GPU_OK;
+}
+
+int p64gpu_free(void *ptr) {
+  if (ptr) HIP_TRY(hipFree(ptr));
+  return P64GPU_OK;
+}
+
+int p64gpu_copy_to_device(void *dst, const void *src, size_t bytes, void *stream) {
+  if ((!dst || !src) && bytes) return fail(P64GPU_E_INVALID, "NULL copy operand");
+  HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, (hipStream_t)stream));
+  return P64GPU_OK;
+}
+
+int p64gpu_copy_to_host(void *dst, const void *src, size_t bytes, void *stream) {
+  if ((!dst || !src) && bytes) return fail(P64GPU_E_INVALID, "NULL copy operand");
+  HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, (hipStream_t)stream));
+  return P64GPU_OK;
+}
+
 int p64gpu_block_op(int op, const int32_t *in, int32_t *out, int64_t nblocks, int dcq, int acq,
                     void *stream) {
   if (op < 0 || op >= P64GPU_OP_COUNT) return fail(P64GPU_E_INVALID, "block op %d", op);

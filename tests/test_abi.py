@@ -1,0 +1,124 @@
+"""CPU-side checks of the C ABI (no GPU needed): the library loads, exports
+every entry point include/p64gpu.h declares, lays out its structs the way the
+ctypes mirror does, and rejects bad arguments before touching a device."""
+import ctypes
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import REPO
+
+HEADER = os.path.join(REPO, "include", "p64gpu.h")
+
+
+def declared_functions():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(p64(?:gpu)?_\w+)\s*\(", text)))
+
+
+def test_header_declares_expected_entry_points():
+    names = declared_functions()
+    for n in ("p64gpu_block_op", "p64gpu_motion_estimation", "p64gpu_encode_frames",
+              "p64gpu_decode_recon", "p64gpu_encoder_open", "p64gpu_encoder_frame",
+              "p64gpu_encoder_close", "p64gpu_synth_frames", "p64_synth_frame"):
+        assert n in names
+
+
+def test_library_exports_every_declared_symbol(p64):
+    out = subprocess.run(["nm", "-D", "--defined-only", p64.LIB_PATH], capture_output=True,
+                         text=True, check=True).stdout
+    exported = set(l.split()[-1] for l in out.splitlines() if " T " in l)
+    missing = [n for n in declared_functions() if n not in exported]
+    assert not missing, missing
+
+
+def test_abi_version_and_strings(p64):
+    L = p64.lib()
+    assert L.p64gpu_abi_version() == 1
+    assert L.p64gpu_strerror(0) == b"ok"
+    assert L.p64gpu_strerror(-1) == b"invalid argument"
+
+
+def test_struct_layout_matches_ctypes(p64, tmp_path):
+    src = tmp_path / "layout.c"
+    src.write_text(r'''
+#include <stdio.h>
+#include <stddef.h>
+#include "p64gpu.h"
+#define O(f) printf("%s %zu\n", #f, offsetof(p64gpu_encode_args, f))
+int main(void) {
+  printf("sizeof_args %zu\nsizeof_me %zu\nsizeof_mb %zu\n", sizeof(p64gpu_encode_args),
+         sizeof(p64_me_rec), sizeof(p64_mb_rec));
+  O(width); O(height); O(nframes); O(intra); O(quant); O(me_mode); O(search_limit);
+  O(reserved); O(frame_stride); O(cur); O(ref); O(recon); O(last_intra); O(quant_mb);
+  O(mtype_override); O(coef); O(mb); O(me);
+  return 0;
+}''')
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-I", os.path.join(REPO, "include"), str(src), "-o", str(exe)], check=True)
+    got = dict(l.split() for l in subprocess.run([str(exe)], capture_output=True, text=True,
+                                                 check=True).stdout.splitlines())
+    assert int(got["sizeof_args"]) == ctypes.sizeof(p64.EncodeArgs)
+    assert int(got["sizeof_me"]) == ctypes.sizeof(p64.MeRec) == p64.ME_DTYPE.itemsize
+    assert int(got["sizeof_mb"]) == ctypes.sizeof(p64.MbRec) == p64.MB_DTYPE.itemsize
+    for name, _ in p64.EncodeArgs._fields_:
+        assert int(got[name]) == getattr(p64.EncodeArgs, name).offset, name
+
+
+def test_invalid_arguments_rejected_without_device(p64):
+    L = p64.lib()
+    a = p64.EncodeArgs(width=100, height=64, nframes=1, quant=8, frame_stride=9600)
+    assert L.p64gpu_encode_frames(ctypes.byref(a), None) == -1
+    assert b"multiples of 16" in L.p64gpu_last_error()
+    assert L.p64gpu_encode_frames(None, None) == -1
+    a = p64.EncodeArgs(width=176, height=144, nframes=1, quant=0, frame_stride=38016,
+                       cur=16, recon=16, last_intra=16, coef=16, mb=16, intra=1)
+    assert L.p64gpu_encode_frames(ctypes.byref(a), None) == -1
+    assert b"quant" in L.p64gpu_last_error()
+    assert L.p64gpu_block_op(99, 16, 16, 1, 8, 8, None) == -1
+    assert L.p64gpu_block_op(2, 16, 16, 1, 8, 0, None) == -1  # acq 0
+    assert L.p64gpu_block_op(0, None, None, 0, 8, 8, None) == 0  # empty batch is a no-op
+    assert L.p64gpu_motion_estimation(176, 144, 1, 176 * 144, 16, 16, 7, 15, 16, None) == -1
+    assert L.p64gpu_motion_estimation(176, 144, 1, 176 * 144, 16, 16, 1, 32, 16, None) == -1
+    assert L.p64gpu_synth_frames(176, 144, 1, 0, 0, 1, 38016, 16, None) == -1
+
+
+def test_device_count_without_gpu_is_not_an_error(p64):
+    n = ctypes.c_int(-1)
+    assert p64.lib().p64gpu_device_count(ctypes.byref(n)) == 0
+    assert n.value >= 0
+
+
+def test_synth_is_deterministic_and_moves(p64):
+    a = p64.synth_frame(9, 3, 176, 144)
+    b = p64.synth_frame(9, 3, 176, 144)
+    assert np.array_equal(a, b)
+    mvx, mvy = p64.synth_motion(9)
+    f0 = p64.synth_frame(6, 0, 176, 144)[: 176 * 144].reshape(144, 176)  # seed 6: no noise
+    f1 = p64.synth_frame(6, 1, 176, 144)[: 176 * 144].reshape(144, 176)
+    mx, my = p64.synth_motion(6)
+    # frame 1 at (x, y) == frame 0 at (x + mx, y + my) for the noise-free class
+    assert np.array_equal(f1[20:100, 20:100], f0[20 + my:100 + my, 20 + mx:100 + mx])
+    assert (mvx, mvy) == (9 % 7 - 3, (9 // 7) % 5 - 2)
+
+
+def test_host_driver_built():
+    exe = os.path.join(REPO, "p64_amd", "p64gpu_enc")
+    assert os.access(exe, os.X_OK)
+    r = subprocess.run([exe], capture_output=True, text=True)
+    assert r.returncode == 1 and "usage" in r.stderr
+
+
+def test_product_does_not_reference_oracle():
+    """The product path never routes through the checker."""
+    for root in ("p64_amd",):
+        for dirpath, _, files in os.walk(os.path.join(REPO, root)):
+            for f in files:
+                if f.endswith((".py", ".hip", ".c", ".h")):
+                    text = open(os.path.join(dirpath, f), errors="ignore").read()
+                    assert "import oracle" not in text and "liboracle" not in text, f
+                    assert "orc_" not in text, f

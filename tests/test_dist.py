@@ -1,0 +1,80 @@
+"""Multi-process (world_size 2, gloo, CPU) coverage of bench.py's N>1 path:
+sequence sharding is a partition with no data-path exchange, per-rank results
+do not depend on the number of ranks, and the timing reduction is a MAX."""
+import hashlib
+import os
+import socket
+
+import numpy as np
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from conftest import REPO
+
+
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def encode_digest(seed, w=176, h=144, nframes=2):
+    """Per-sequence work stand-in: the CPU oracle encoding one short sequence."""
+    import sys
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle
+    import p64_amd
+
+    frames = [p64_amd.synth_frame(seed, t, w, h) for t in range(nframes)]
+    outs = oracle.encode_sequence(frames, w, h, quant=8, me_mode=1, search_limit=31)
+    hsh = hashlib.sha256()
+    for coef, mb, _, recon in outs:
+        hsh.update(coef.tobytes())
+        hsh.update(mb.tobytes())
+        hsh.update(recon.tobytes())
+    return int.from_bytes(hsh.digest()[:7], "little")
+
+
+def _worker(rank, world, port, streams, q):
+    import sys
+    sys.path.insert(0, REPO)
+    import torch
+    import bench
+
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
+                            world_size=world)
+    seed0, n = bench.shard_seeds(rank, streams)
+    digests = torch.tensor([encode_digest(seed0 + k) for k in range(n)], dtype=torch.int64)
+    gathered = [torch.zeros_like(digests) for _ in range(world)]
+    dist.barrier()
+    dist.all_gather(gathered, digests)  # verification only, outside any timed region
+    fake_time = 1.0 + rank  # rank 1 is "slower"
+    tmax = bench.max_over_ranks(fake_time, world)
+    seeds = [bench.shard_seeds(r, streams)[0] + k for r in range(world) for k in range(streams)]
+    if rank == 0:
+        q.put((torch.cat(gathered).tolist(), tmax, seeds,
+               bench.aggregate_rate(world, streams * 99, 10, tmax)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_sharding_matches_single_process():
+    world, streams = 2, 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, streams, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    digests, tmax, seeds, rate = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert len(set(seeds)) == world * streams          # disjoint shards
+    assert seeds == list(range(1, 1 + world * streams))  # cover 1..N*S exactly
+    single = [encode_digest(s) for s in seeds]
+    assert digests == single
+    assert tmax == 2.0
+    assert np.isclose(rate, world * streams * 99 * 10 / 2.0)

@@ -251,3 +251,36 @@ def test_invalid_arguments_raise(p64, torch_dev):
         p64.encode_frames(x, x, x, x, width=100, height=64, intra=True)
     with pytest.raises(p64.P64GpuError):
         p64.MotionEstimation(x, x, 176, 144, mode=5)
+
+
+# ---------------------------------------------------------------------------
+# link-level drop-in: the reference CLI with MotionEstimation/ChenDct/ChenIDct
+# served by the GPU (p64_amd/host/p64gpu_refshim.c)
+
+REFSHIM = os.path.join(os.path.dirname(GOLDEN), "..", "oracle", "_ref", "p64gpu_ref")
+
+
+@pytest.mark.parametrize("name", ["qcif_tss", "qcif_full31", "qcif_q31", "cif_full31",
+                                  "qcif_flat_tss"])
+def test_reference_cli_with_gpu_shim(p64, torch_dev, tmp_path, name):
+    import subprocess
+    if not os.access(REFSHIM, os.X_OK):
+        pytest.skip("oracle/_ref/p64gpu_ref not built (needs /root/reference at build time)")
+    z = load(f"seq_{name}.npz")
+    w, h, n = int(z["width"]), int(z["height"]), int(z["nframes"])
+    frames = sequence_frames(p64, z)
+    y4m = tmp_path / "in.y4m"
+    with open(y4m, "wb") as f:
+        f.write(b"YUV4MPEG2 W%d H%d F30000:1001 Ip A0:0 C420jpeg\n" % (w, h))
+        for fr in frames:
+            f.write(b"FRAME\n" + fr.tobytes())
+    env = dict(os.environ)
+    if str(z["me"]) == "full":
+        env["P64GPU_ME"] = "full"
+    out = tmp_path / "out.p64"
+    subprocess.run([REFSHIM, "-" + str(z["fmt"]), "-y4m", "-a", "0", "-b", str(n - 1), "-q",
+                    str(int(z["q"])), "-i", str(int(z["sl"])), str(tmp_path / "in"), "-z", ".y4m",
+                    "-s", str(out)], env=env, stdout=subprocess.DEVNULL, check=True, timeout=300)
+    data = out.read_bytes()
+    assert len(data) == int(z["stream_len"])
+    assert hashlib.sha256(data).hexdigest() == str(z["stream_sha256"])
