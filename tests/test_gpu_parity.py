@@ -284,3 +284,12 @@ def test_reference_cli_with_gpu_shim(p64, torch_dev, tmp_path, name):
     data = out.read_bytes()
     assert len(data) == int(z["stream_len"])
     assert hashlib.sha256(data).hexdigest() == str(z["stream_sha256"])
+
+
+def test_device_synth_matches_host(p64, torch_dev):
+    """The bench's on-device inputs are the same bytes the CPU legs use."""
+    for (w, h) in ((352, 288), (176, 144)):
+        d = host(p64.synth_frames_device(w, h, 5, 3, 10, 2))
+        for t in range(2):
+            for s in range(3):
+                np.testing.assert_array_equal(d[t, s], p64.synth_frame(5 + s, 10 + t, w, h))
