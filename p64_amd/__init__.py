@@ -30,7 +30,8 @@ from dataclasses import dataclass
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libp64gpu.so")
+# P64GPU_LIB lets development A/B runs point at an alternative build.
+LIB_PATH = os.environ.get("P64GPU_LIB", os.path.join(_HERE, "libp64gpu.so"))
 
 ME_TSS = 0
 ME_FULL = 1

@@ -169,11 +169,20 @@ __device__ __forceinline__ int clampi(int v, int lo, int hi) { return min(max(v,
 // plus the +-1 of even q), where the 20-bit reciprocal is exact for every
 // d <= 62 (tests/test_quant_magic.py checks it exhaustively); the block-op path
 // handles arbitrary int32 with a true division.
+// a * m for a, m < 2^24 on the full-rate 24-bit multiplier.  The backend only
+// selects v_mul_u32_u24 when it can prove the operand widths itself and
+// otherwise falls back to the quarter-rate v_mul_lo_u32.
+__device__ __forceinline__ unsigned mul_u24_s(unsigned a, unsigned m_uniform) {
+  unsigned r;
+  asm("v_mul_u32_u24 %0, %1, %2" : "=v"(r) : "s"(m_uniform), "v"(a));
+  return r;
+}
+
 template <bool BOUNDED>
 __device__ __forceinline__ int div_trunc(int c, int d, unsigned magic) {
   if (BOUNDED) {
     const unsigned a = (unsigned)abs(c);
-    const int qq = (int)(__umul24(a, magic) >> 20);
+    const int qq = (int)(mul_u24_s(a, magic) >> 20);
     return c < 0 ? -qq : qq;
   }
   return c / d;
@@ -439,16 +448,26 @@ __device__ __forceinline__ void me_stats(const MbLds &L, int lane, MeOut &o) {
   o.mwor = sum;
 }
 
+// wave-uniform by construction (results of wave reductions); saying so lets
+// hipcc use scalar registers and scalar branches for everything that follows
+__device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
+
 template <int MODE>  // 1 = TSS, 2 = FULL
 __device__ __forceinline__ MeOut motion_estimate(MbLds &L, int w, int h, int x0, int y0, int sl,
                                                  int lane) {
   MeOut o;
-  o.sad0 = sad_zero(L, lane);
+  o.sad0 = uni(sad_zero(L, lane));
   if (MODE == 2)
     me_full(L, w, h, x0, y0, sl, lane, o.sad0, o.mx, o.my, o.sad);
   else
     me_tss(L, w, h, x0, y0, lane, o.sad0, o.mx, o.my, o.sad);
+  o.mx = uni(o.mx);
+  o.my = uni(o.my);
+  o.sad = uni(o.sad);
   me_stats(L, lane, o);
+  o.var = uni(o.var);
+  o.varor = uni(o.varor);
+  o.mwor = uni(o.mwor);
   return o;
 }
 
@@ -593,7 +612,9 @@ __device__ __forceinline__ void predict_row_glb(const Picture &ref, int w, int b
 }
 
 // ---------------------------------------------------------------------------
-// transforms through the LDS scratch (lanes b < 6 active in row/column passes)
+// transforms through the LDS scratch.  All 64 lanes compute the row/column
+// passes (lanes 48..63 shadow block 5, b is clamped); only lanes < 48 (act)
+// store, so no two lanes write one LDS word.
 
 // rows res[8] of block b -> forward 2-D transform -> raw (pre-/8) coefficients
 // left in L.blk in natural order
@@ -604,22 +625,26 @@ __device__ __forceinline__ void forward_2d(MbLds &L, bool act, int b, int r, con
     for (int k = 0; k < 8; k++) B[r * ROW_STRIDE + k] = res[k];
   }
   __syncthreads();
-  if (act) {  // column pass, lane owns column c = r
+  {  // column pass, lane owns column c = r
     int x[8], o[8];
 #pragma unroll
     for (int k = 0; k < 8; k++) x[k] = B[k * ROW_STRIDE + r];
     fwd_col<true>(x, o);
+    if (act) {
 #pragma unroll
-    for (int k = 0; k < 8; k++) B[k * ROW_STRIDE + r] = o[k];
+      for (int k = 0; k < 8; k++) B[k * ROW_STRIDE + r] = o[k];
+    }
   }
   __syncthreads();
-  if (act) {
+  {
     int x[8], o[8];
 #pragma unroll
     for (int k = 0; k < 8; k++) x[k] = B[r * ROW_STRIDE + k];
     fwd_row<true>(x, o);
+    if (act) {
 #pragma unroll
-    for (int k = 0; k < 8; k++) B[r * ROW_STRIDE + k] = o[k];
+      for (int k = 0; k < 8; k++) B[r * ROW_STRIDE + k] = o[k];
+    }
   }
   __syncthreads();
 }
@@ -628,18 +653,20 @@ __device__ __forceinline__ void forward_2d(MbLds &L, bool act, int b, int r, con
 // of block b's residual
 __device__ __forceinline__ void inverse_2d(MbLds &L, bool act, int b, int r, int res[8]) {
   int *B = L.blk + b * BLK_STRIDE;
-  if (act) {  // column pass: inputs <<2
+  {  // column pass: inputs <<2
     int x[8], o[8];
 #pragma unroll
     for (int k = 0; k < 8; k++) x[k] = B[k * ROW_STRIDE + r] << 2;
     inv8<true>(x, o);
+    if (act) {
 #pragma unroll
-    for (int k = 0; k < 8; k++) B[k * ROW_STRIDE + r] = o[k];
+      for (int k = 0; k < 8; k++) B[k * ROW_STRIDE + r] = o[k];
+    }
   }
   __syncthreads();
   int x[8], o[8];
 #pragma unroll
-  for (int k = 0; k < 8; k++) x[k] = act ? B[r * ROW_STRIDE + k] : 0;
+  for (int k = 0; k < 8; k++) x[k] = B[r * ROW_STRIDE + k];
   inv8<true>(x, o);
 #pragma unroll
   for (int k = 0; k < 8; k++) res[k] = idct_final(o[k]);
@@ -654,15 +681,30 @@ __device__ __forceinline__ void blk_put(MbLds &L, int k, int e, int v) {
 }
 
 // BoundDctMatrix + CCITT(Flat)Quantize + (Flat)BoundQuantizeMatrix of one raw
-// coefficient (transform.c:271-350, 460-537)
-__device__ __forceinline__ int quantise(int raw, bool dc, bool intra, int q, unsigned magic) {
+// coefficient (transform.c:271-350, 460-537), branch-free.  dc: lane holds the
+// DC coefficient; INTRA selects the flat DC quantiser.
+template <bool INTRA>
+__device__ __forceinline__ int quantise(int raw, bool dc, bool qeven, unsigned magic) {
   int v = dct_final(raw);
-  v = dc ? min(v, 2047) : clampi(v, -1023, 1023);
-  if (intra && dc) return clampi(qdc_intra(v, 8), 1, 254);
-  return clampi(qlevel<true>(v, q, magic), -127, 127);
+  v = clampi(v, dc ? -0x7fffffff : -1023, dc ? 2047 : 1023);
+  const int c = qeven ? v + (v > 0 ? 1 : -1) : v;  // sign(0) = -1 (transform.c:285)
+  const int sm = c >> 31;
+  const unsigned a = (unsigned)((c ^ sm) - sm);
+  int l = (int)((mul_u24_s(a, magic) >> 20) ^ (unsigned)sm) - sm;  // trunc(c / 2q)
+  l = clampi(l, -127, 127);
+  if (INTRA) l = dc ? clampi(qdc_intra(v, 8), 1, 254) : l;
+  return l;
 }
-__device__ __forceinline__ int dequantise(int lev, bool dc, bool intra, int q) {
-  return (intra && dc) ? lev * 8 : rlevel<true>(lev, q);  // ICCITT(Flat)Quantize
+// ICCITT(Flat)Quantize of one level (transform.c:359-451), branch-free: with
+// sg = sign(l) (0 for l = 0) the reconstruction is (2l + sg) q, minus sg for
+// even q, and 0 stays 0.
+template <bool INTRA>
+__device__ __forceinline__ int dequantise(int l, bool dc, int q, bool qeven) {
+  const int sg = clampi(l, -1, 1);
+  int v = __mul24(2 * l + sg, q);
+  if (qeven) v -= sg;
+  if (INTRA) v = dc ? l * 8 : v;
+  return v;
 }
 
 // CBP decision from the six blocks' levels (p64.c:887-908), with wave ballots:
@@ -704,7 +746,7 @@ __global__ __launch_bounds__(64) void k_encode(p64gpu_encode_args a) {
   const Picture ref = picture_at(a.ref + (size_t)fi * a.frame_stride, w, h);
   uint8_t *rec = a.recon + (size_t)fi * a.frame_stride;
 
-  // row layout coordinates (lanes 48..63 shadow block 5 and are masked)
+  // row layout coordinates (lanes 48..63 shadow block 5, masked on stores)
   const int b = min(lane >> 3, 5), r = lane & 7;
   const bool act = lane < 48;
   const BlockGeom g = block_geom(b, mbx, mby);
@@ -738,8 +780,10 @@ __global__ __launch_bounds__(64) void k_encode(p64gpu_encode_args a) {
   }
   const uint8_t li = a.last_intra[gmb];
   if (li > 131) mt = 0;  // SEQUENCE_INTRA_THRESHOLD (p64.c:159, 772)
-  const int q = a.quant_mb ? a.quant_mb[gmb] : a.quant;
+  mt = uni(mt);
+  const int q = uni(a.quant_mb ? a.quant_mb[gmb] : a.quant);
   const unsigned magic = quant_magic(q);
+  const bool qeven = !(q & 1);
 
   int pred[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   if (!mt_intra(mt)) {
@@ -750,24 +794,29 @@ __global__ __launch_bounds__(64) void k_encode(p64gpu_encode_args a) {
 
   // ReadCompressMDU (p64.c:830-912): levels in element layout
   const int e = lane;
+  const bool dc = e == 0;
   int lev[6] = {0, 0, 0, 0, 0, 0};
-  bool intra = mt_intra(mt);
   if (mt_tcoeff(mt)) {
     int res[8];
     unpack8(crow.x, crow.y, res);
 #pragma unroll
     for (int k = 0; k < 8; k++) res[k] -= pred[k];
     forward_2d(L, act, b, r, res);
+    if (mt_intra(mt)) {
 #pragma unroll
-    for (int k = 0; k < 6; k++) lev[k] = quantise(blk_at(L, k, e), e == 0, intra, q, magic);
+      for (int k = 0; k < 6; k++) lev[k] = quantise<true>(blk_at(L, k, e), dc, qeven, magic);
+    } else {
+#pragma unroll
+      for (int k = 0; k < 6; k++) lev[k] = quantise<false>(blk_at(L, k, e), dc, qeven, magic);
+    }
   }
   int cbp = 0x3f;
   if (mt_cbp(mt)) {
     const CbpOut c = cbp_decide(lev);
-    cbp = c.cbp;
+    cbp = uni(c.cbp);
     if (c.nothing) {  // no coefficients: MC without coefficients, ME vector kept
       const int old = mt;
-      mt = mt_filter(mt) ? 7 : 4;
+      mt = uni(mt_filter(mt) ? 7 : 4);
       cbp = 0x3f;
       if (!mt_mf(old)) {  // 2/3 -> 4 switches from the zero vector to the ME vector
         __syncthreads();
@@ -779,13 +828,14 @@ __global__ __launch_bounds__(64) void k_encode(p64gpu_encode_args a) {
   }
   const int zpos = c_zz.pos[e];
   __syncthreads();  // element reads of blk are complete before it is rewritten
-  int coded = 0;
+  const int coded = mt_tcoeff(mt) ? cbp : 0;  // block c coded <=> bit 5-c
+  const bool intra = mt_intra(mt);
 #pragma unroll
   for (int k = 0; k < 6; k++) {
     L.zz[k * 64 + zpos] = (int16_t)lev[k];
-    const bool ck = ((cbp >> (5 - k)) & 1) && mt_tcoeff(mt);
-    coded |= ck ? 1 << k : 0;
-    blk_put(L, k, e, ck ? dequantise(lev[k], e == 0, mt_intra(mt), q) : 0);
+    const int dq = intra ? dequantise<true>(lev[k], dc, q, qeven)
+                         : dequantise<false>(lev[k], dc, q, qeven);
+    blk_put(L, k, e, ((coded >> (5 - k)) & 1) ? dq : 0);
   }
   __syncthreads();
   if (lane < 48)
@@ -795,9 +845,8 @@ __global__ __launch_bounds__(64) void k_encode(p64gpu_encode_args a) {
   int res[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   if (coded) inverse_2d(L, act, b, r, res);
   if (act) {
-    const bool add = !mt_intra(mt);
 #pragma unroll
-    for (int k = 0; k < 8; k++) res[k] = clampi(res[k] + (add ? pred[k] : 0), 0, 255);
+    for (int k = 0; k < 8; k++) res[k] = clampi(res[k] + pred[k], 0, 255);  // pred = 0 if intra
     uint8_t *pl = rec + (g.plane == 0 ? 0 : w * h + (g.plane - 1) * (w >> 1) * (h >> 1));
     *reinterpret_cast<uint2 *>(pl + (g.y + r) * pw + g.x) = pack8(res);
   }
@@ -856,20 +905,21 @@ __global__ __launch_bounds__(64) void k_decode_recon(int w, int h, int64_t strid
   const Picture ref = picture_at(refp + (size_t)fi * stride, w, h);
   uint8_t *rec = recp + (size_t)fi * stride;
   const p64_mb_rec m = mbr[gmb];
-  const int mt = m.mtype, q = quant_mb[gmb];
-  const int cbp = mt_cbp(mt) ? m.cbp : 0x3f;  // p64.c:1200
+  const int mt = uni(m.mtype), q = uni(quant_mb[gmb]);
+  const int cbp = uni(mt_cbp(mt) ? m.cbp : 0x3f);  // p64.c:1200
   const int b = min(lane >> 3, 5), r = lane & 7;
   const bool act = lane < 48;
   const BlockGeom g = block_geom(b, mbx, mby);
   const int pw = g.plane ? w / 2 : w;
   const int e = lane, zpos = c_zz.pos[e];
-  int coded = 0;
+  const bool dc = e == 0, qeven = !(q & 1), intra = mt_intra(mt);
+  const int coded = mt_tcoeff(mt) ? cbp : 0;
 #pragma unroll
   for (int k = 0; k < 6; k++) {
-    const bool ck = ((cbp >> (5 - k)) & 1) && mt_tcoeff(mt);
-    coded |= ck ? 1 << k : 0;
+    const bool ck = (coded >> (5 - k)) & 1;
     const int lev = ck ? coef[gmb * 384 + k * 64 + zpos] : 0;  // IZigzagMatrix
-    blk_put(L, k, e, ck ? dequantise(lev, e == 0, mt_intra(mt), q) : 0);
+    const int dq = intra ? dequantise<true>(lev, dc, q, qeven) : dequantise<false>(lev, dc, q, qeven);
+    blk_put(L, k, e, ck ? dq : 0);
   }
   int pred[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   if (!mt_intra(mt)) predict_row_glb(ref, w, b, mbx, mby, r, mt, m.mvx, m.mvy, pred);

@@ -1,0 +1,80 @@
+// Issue-rate probe for the VALU ops the SAD kernels use (gfx950):
+// 8 independent chains per wave, 256-thread blocks, 16 blocks/CU-worth of grid.
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdint>
+
+__device__ unsigned long long g_clk[4];
+template <int OP, bool SOP>
+__global__ __launch_bounds__(256) void k(uint32_t seed, int iters, uint32_t* out) {
+  unsigned long long t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
+  uint32_t s0 = SOP ? __builtin_amdgcn_readfirstlane(seed * 7 + blockIdx.x) : seed * 7 + threadIdx.x;
+  uint32_t s1 = SOP ? __builtin_amdgcn_readfirstlane(seed * 13 + 1) : seed * 13 + threadIdx.x * 3;
+  uint32_t r[8], a[8];
+#pragma unroll
+  for (int j = 0; j < 8; j++) { r[j] = (threadIdx.x + 37 * j) * 0x01010101u ^ (j * 0x1f2e3d4c); a[j] = j; }
+  for (int it = 0; it < iters; it++) {
+#pragma unroll
+    for (int u = 0; u < 8; u++)
+#pragma unroll
+      for (int j = 0; j < 8; j++) {
+        uint32_t x = r[(u + j) & 7], y = (j & 1) ? s1 : s0;
+        if (OP == 0) a[j] = __builtin_amdgcn_sad_u8(x, y, a[j]);
+        if (OP == 1) a[j] = x + a[j] + y;                       // v_add3_u32
+        if (OP == 2) a[j] = __builtin_amdgcn_udot4(x, y, a[j], false);
+        if (OP == 3) a[j] = __builtin_amdgcn_msad_u8(x, y, a[j]);
+        if (OP == 4) a[j] = __builtin_amdgcn_alignbyte(x, a[j], y);
+        if (OP == 5) a[j] = __builtin_amdgcn_sad_hi_u8(x, y, a[j]);
+        if (OP == 6) a[j] = __builtin_amdgcn_sad_u16(x, y, a[j]);
+        if (OP == 7) a[j] = __mul24((int)x, (int)a[j]) ;
+        if (OP == 8) a[j] = x ^ a[j];
+        if (OP == 9) a[j] = __builtin_amdgcn_qsad_pk_u16_u8(((uint64_t)x << 32) | y, y, a[j]);
+      }
+    asm volatile("" : "+v"(r[0]), "+v"(r[3]));
+  }
+  uint32_t t = 0;
+  for (int j = 0; j < 8; j++) t += a[j];
+  out[blockIdx.x * 256 + threadIdx.x] = t;
+  if (blockIdx.x == 17 && threadIdx.x == 0) {
+    unsigned long long t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+    g_clk[0] = t1 - t0;
+    g_clk[1] = r1 - r0;
+  }
+}
+
+template <int OP, bool SOP>
+void run(const char* name, uint32_t* d) {
+  int blocks = 256 * 16, iters = 1000;
+  hipEvent_t e0, e1; (void)hipEventCreate(&e0); (void)hipEventCreate(&e1);
+  float best = 1e9;
+  for (int rep = 0; rep < 4; rep++) {
+    (void)hipEventRecord(e0);
+    k<OP, SOP><<<blocks, 256>>>(1, iters, d);
+    (void)hipEventRecord(e1); (void)hipEventSynchronize(e1);
+    float ms; (void)hipEventElapsedTime(&ms, e0, e1);
+    if (rep && ms < best) best = ms;
+  }
+  double winstr = (double)blocks * 4 * iters * 64;
+  double per_simd = winstr / 1024 / (best * 1e-3);
+  unsigned long long c[2];
+  (void)hipMemcpyFromSymbol(c, HIP_SYMBOL(g_clk), sizeof c);
+  double ghz = (double)c[0] / (double)c[1] * 0.1;
+  printf("%-20s %s  %.3f ms  %.3f Twave-instr/s  block clock %.2f GHz  %.2f cycles/instr/SIMD at that clock\n",
+         name, SOP ? "sgpr" : "vgpr", best, winstr / best / 1e9, ghz, ghz * 1e9 / per_simd);
+}
+
+int main() {
+  uint32_t* d; (void)hipMalloc(&d, 256 * 4096 * 4 * 4);
+  run<1, false>("v_add3_u32", d);
+  run<0, true>("v_sad_u8", d);
+  run<0, false>("v_sad_u8", d);
+  run<3, true>("v_msad_u8", d);
+  run<5, true>("v_sad_hi_u8", d);
+  run<6, true>("v_sad_u16", d);
+  run<2, true>("v_dot4_u32_u8", d);
+  run<4, false>("v_alignbyte_b32", d);
+  run<7, false>("v_mul_i32_i24", d);
+  run<8, false>("v_xor_b32", d);
+  run<9, true>("v_qsad_pk_u16_u8", d);
+  return 0;
+}
