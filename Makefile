@@ -13,7 +13,7 @@ ARCH    ?= gfx950
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Wall -Wno-unused-function
 LIB     := p64_amd/libp64gpu.so
 
-all: $(LIB) p64_amd/p64gpu_enc oracle
+all: $(LIB) p64_amd/p64gpu oracle
 
 p64_amd/csrc/synth.o: p64_amd/csrc/synth.c include/p64gpu.h
 	$(CC) -O2 -fPIC -Wall -c $< -o $@
@@ -21,11 +21,14 @@ p64_amd/csrc/synth.o: p64_amd/csrc/synth.c include/p64gpu.h
 p64_amd/csrc/p64gpu.o: p64_amd/csrc/p64gpu.hip include/p64gpu.h
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-$(LIB): p64_amd/csrc/p64gpu.o p64_amd/csrc/synth.o
+p64_amd/csrc/p64stream.o: p64_amd/csrc/p64stream.c include/p64stream.h include/p64gpu.h
+	$(CC) -O2 -fPIC -Wall -Wextra -c $< -o $@
+
+$(LIB): p64_amd/csrc/p64gpu.o p64_amd/csrc/synth.o p64_amd/csrc/p64stream.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $^
 
-p64_amd/p64gpu_enc: p64_amd/host/p64gpu_enc.c $(LIB) include/p64gpu.h
-	$(CC) -O2 -Wall -o $@ $< -Lp64_amd -lp64gpu -Wl,-rpath,'$$ORIGIN'
+p64_amd/p64gpu: p64_amd/host/p64gpu_cli.c $(LIB) include/p64gpu.h include/p64stream.h
+	$(CC) -O2 -Wall -Wextra -o $@ $< -Lp64_amd -lp64gpu -Wl,-rpath,'$$ORIGIN'
 
 oracle:
 	$(MAKE) -C oracle

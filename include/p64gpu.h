@@ -61,7 +61,8 @@ enum p64gpu_status {
   P64GPU_E_INVALID = -1,  /* bad argument: shape, range, alignment or NULL */
   P64GPU_E_NODEVICE = -2, /* no usable HIP device */
   P64GPU_E_HIP = -3,      /* a HIP runtime call failed */
-  P64GPU_E_NOMEM = -4     /* device or host allocation failed */
+  P64GPU_E_NOMEM = -4,    /* device or host allocation failed */
+  P64GPU_E_STREAM = -5    /* malformed or unsupported bitstream (p64stream.h) */
 };
 
 /* Motion search (me.c).  TSS is what the reference ships (me.c:352); FULL is
@@ -100,6 +101,7 @@ int p64gpu_alloc(void **ptr, size_t bytes);
 int p64gpu_free(void *ptr);
 int p64gpu_copy_to_device(void *dst, const void *src, size_t bytes, void *stream);
 int p64gpu_copy_to_host(void *dst, const void *src, size_t bytes, void *stream);
+int p64gpu_copy_on_device(void *dst, const void *src, size_t bytes, void *stream);
 
 /* ---- 8x8 block operations, batched (device pointers) -------------------- */
 enum p64gpu_block_op {

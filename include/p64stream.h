@@ -1,0 +1,107 @@
+/*
+ * p64stream.h -- H.261 bitstream layer of the drop-in (host C, part of
+ * libp64gpu.so; no GPU involved).
+ *
+ * The GPU path (p64gpu.h) stops at the coefficient boundary: per macroblock
+ * MTYPE/CBP/MV records and zigzagged levels.  These entry points turn those
+ * records into the reference's .p64 bytes and back:
+ *
+ *   p64s_write_picture   WritePictureHeader marker.c:103 + WriteGOBHeader
+ *                        marker.c:171 + the MDU loop of p64EncodeGOB
+ *                        p64.c:692-786 as far as it writes: WriteMDU p64.c:920
+ *                        -> WriteMBHeader marker.c:288 (MBA/MTYPE/MQUANT/MVD/CBP,
+ *                        with the reference's MVD predictor reset rule), EncodeDC
+ *                        codec.c:343, EncodeAC codec.c:96, CBPEncodeAC codec.c:141;
+ *                        VLC tables huffman.c:102-290 + ctables.h (the H.261
+ *                        tables), bit order stream.c:112-190 (MSB first)
+ *   p64s_write_end       the trailing picture header p64.c:608-610 and mwclose
+ *                        stream.c:121 (last byte padded with ones)
+ *   p64s_read_picture    p64DecodeSequence p64.c:1022 / p64DecodeGOB p64.c:1131 /
+ *                        ReadMBHeader marker.c:372 / DecompressMDU p64.c:1179 up to
+ *                        the levels (DecodeDC codec.c:326, DecodeAC codec.c:215,
+ *                        CBPDecodeAC codec.c:258); the IQ/IDCT/prediction half runs
+ *                        on the GPU (p64gpu_decode_recon)
+ *
+ * Every function returns 0 (or a documented positive value) on success and a
+ * negative P64GPU_E_* status on failure, with the text in p64gpu_last_error().
+ * Macroblock arrays are in RASTER order (mb = mby*(w/16)+mbx), the layout of
+ * the GPU records; the GOB/MDU order of the bitstream (Bpos io.c:757) is
+ * applied here.
+ */
+#ifndef P64STREAM_H
+#define P64STREAM_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "p64gpu.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Picture formats the reference codes (SetCCITT p64.c:1373, PType p64.c:414-431). */
+enum p64s_format { P64S_QCIF = 0, P64S_CIF = 1, P64S_NTSC = 2 };
+
+/* Geometry of a format: 176x144 / 352x288 / 352x240 and 3 / 12 / 10 GOBs of
+ * 33 MBs.  Returns P64GPU_E_INVALID for an unknown format. */
+int p64s_geometry(int format, int *width, int *height, int *ngob);
+/* Format of a picture size, or P64GPU_E_INVALID. */
+int p64s_format_of(int width, int height);
+
+/* ---- writer ------------------------------------------------------------- */
+typedef struct p64s_writer p64s_writer;
+int p64s_writer_open(p64s_writer **out);
+void p64s_writer_close(p64s_writer *w);
+/* One coded picture: picture header with temporal reference tr (mod 32),
+ * then every GOB (header with gquant[g]) and every macroblock in GOB order.
+ * mb/coef are the GPU records ([nmb], [nmb][6][64] zigzag levels before CBP
+ * zeroing); quant_mb ([nmb], may be NULL if no MB has an MQUANT type 1/3/6/9)
+ * gives MQUANT.  Blocks are written when their CBP bit is set and the MTYPE
+ * carries coefficients, exactly as WriteMDU. */
+int p64s_write_picture(p64s_writer *w, int format, int tr, const uint8_t *gquant,
+                       const uint8_t *quant_mb, const p64_mb_rec *mb, const int16_t *coef);
+/* Trailing picture header (tr = frame after the last, mod 32) and final
+ * ones-padding.  The writer accepts no more pictures afterwards. */
+int p64s_write_end(p64s_writer *w, int format, int tr);
+/* The bytes completed so far; *bits (may be NULL) receives the total number
+ * of bits written (mwtell, stream.c:201). */
+const uint8_t *p64s_writer_data(const p64s_writer *w, size_t *len, int64_t *bits);
+/* Drops the first n completed bytes (after the caller has stored them). */
+int p64s_writer_consume(p64s_writer *w, size_t n);
+
+/* ---- reader ------------------------------------------------------------- */
+typedef struct {
+  int format, width, height, ngob;
+  int tr;          /* temporal reference of the picture (5 bits)            */
+  int ptype;       /* PTYPE (6 bits)                                        */
+  int pspare;      /* PSPARE byte, -1 if none                               */
+  int coded_mbs;   /* macroblocks present in the stream for this picture    */
+} p64s_picture_info;
+
+typedef struct p64s_reader p64s_reader;
+/* The reader keeps a pointer to data, which must outlive it.  Fails with
+ * P64GPU_E_STREAM when the stream does not start with a picture start code. */
+int p64s_reader_open(const uint8_t *data, size_t len, p64s_reader **out);
+void p64s_reader_close(p64s_reader *r);
+/* Geometry of the stream (from its first picture header). */
+int p64s_reader_info(const p64s_reader *r, p64s_picture_info *info);
+/* Decodes the next picture's headers and levels.  Returns 1 with a picture,
+ * 0 at the end of the stream (info->tr then holds the temporal reference of
+ * the trailing picture header, or the last picture's tr + 1 if the stream
+ * ends without one -- the two cases of p64DecodeSequence p64.c:1040-1046).
+ * Outputs, raster order, all [nmb]:
+ *   mb        mtype, cbp (0x3f for types without CBP), MV (0 for non-MC types)
+ *   quant_mb  UseQuant of the macroblock (GQUANT or MQUANT)
+ *   coded     1 if the macroblock is present in the stream, else 0 (the
+ *             decoder keeps the previous picture there, p64DecodeGOB)
+ *   coef      [nmb][6][64] zigzag levels; zero where a block is not coded
+ * The arrays are fully written (absent MBs get zeros). */
+int p64s_read_picture(p64s_reader *r, p64s_picture_info *info, p64_mb_rec *mb,
+                      uint8_t *quant_mb, uint8_t *coded, int16_t *coef);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* P64STREAM_H */

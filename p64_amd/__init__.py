@@ -14,6 +14,8 @@ reference (/root/reference):
     encode_frames                            p64.c:622-1013 per-MB compute, batched
     Encoder                                  p64EncodeSequence/p64EncodeFrame loop
                                              (closed loop, reconstruction on device)
+    stream.Writer / stream.Reader            the H.261 bitstream either side of the
+                                             GPU records (marker.c, codec.c, huffman.c)
 
 Block functions take/return int32 tensors of shape [..., 64] (row-major 8x8
 blocks) on a CUDA(HIP) device; the reference works on one `int[64]` at a time,
@@ -119,6 +121,22 @@ def lib() -> ctypes.CDLL:
     L.p64_synth_frame.restype = None
     L.p64_synth_motion.argtypes = [ctypes.c_uint32, ctypes.POINTER(i32), ctypes.POINTER(i32)]
     L.p64_synth_motion.restype = None
+    # H.261 bitstream layer (include/p64stream.h), host C
+    L.p64s_geometry.argtypes = [i32, ctypes.POINTER(i32), ctypes.POINTER(i32), ctypes.POINTER(i32)]
+    L.p64s_format_of.argtypes = [i32, i32]
+    L.p64s_writer_open.argtypes = [ctypes.POINTER(vp)]
+    L.p64s_writer_close.argtypes = [vp]
+    L.p64s_writer_close.restype = None
+    L.p64s_write_picture.argtypes = [vp, i32, i32, vp, vp, vp, vp]
+    L.p64s_write_end.argtypes = [vp, i32, i32]
+    L.p64s_writer_data.argtypes = [vp, ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(i64)]
+    L.p64s_writer_data.restype = vp
+    L.p64s_writer_consume.argtypes = [vp, ctypes.c_size_t]
+    L.p64s_reader_open.argtypes = [vp, ctypes.c_size_t, ctypes.POINTER(vp)]
+    L.p64s_reader_close.argtypes = [vp]
+    L.p64s_reader_close.restype = None
+    L.p64s_reader_info.argtypes = [vp, vp]
+    L.p64s_read_picture.argtypes = [vp, vp, vp, vp, vp, vp]
     if L.p64gpu_abi_version() != 1:
         raise P64GpuError("libp64gpu.so ABI version mismatch")
     _lib = L

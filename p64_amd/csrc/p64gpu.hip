@@ -1072,11 +1072,15 @@ const char *p64gpu_strerror(int s) {
     case P64GPU_E_NODEVICE: return "no HIP device";
     case P64GPU_E_HIP: return "HIP runtime error";
     case P64GPU_E_NOMEM: return "out of memory";
+    case P64GPU_E_STREAM: return "bitstream error";
     default: return "unknown status";
   }
 }
 
 const char *p64gpu_last_error(void) { return g_err; }
+
+// error reporting for the host C parts of the library (p64stream.c)
+int p64gpu_fail_(int status, const char *msg) { return fail(status, "%s", msg); }
 
 int p64gpu_device_count(int *count) {
   if (!count) return fail(P64GPU_E_INVALID, "count is NULL");
@@ -1122,6 +1126,12 @@ int p64gpu_copy_to_device(void *dst, const void *src, size_t bytes, void *stream
 int p64gpu_copy_to_host(void *dst, const void *src, size_t bytes, void *stream) {
   if ((!dst || !src) && bytes) return fail(P64GPU_E_INVALID, "NULL copy operand");
   HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, (hipStream_t)stream));
+  return P64GPU_OK;
+}
+
+int p64gpu_copy_on_device(void *dst, const void *src, size_t bytes, void *stream) {
+  if ((!dst || !src) && bytes) return fail(P64GPU_E_INVALID, "NULL copy operand");
+  HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, (hipStream_t)stream));
   return P64GPU_OK;
 }
 

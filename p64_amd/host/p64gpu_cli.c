@@ -1,0 +1,317 @@
+/*
+ * p64gpu_cli.c -- the reference CLI's encode and decode modes over the C ABI.
+ *
+ * Encode (p64EncodeSequence p64.c:524 / p64EncodeFrame p64.c:622):
+ *   y4m in -> p64gpu_encoder_frame (GPU: ME, decision, DCT/quant, closed-loop
+ *   reconstruction kept on the device) -> p64s_write_picture (host VLC) -> .p64,
+ *   byte-identical to the reference's for the same flags.
+ * Decode (p64DecodeSequence p64.c:1022):
+ *   .p64 -> p64s_read_picture (host VLC parse) -> p64gpu_decode_recon (GPU:
+ *   IQ/IDCT/prediction/filter) -> component files "<prefix><n>.Y/.U/.V"
+ *   (MakeFileNames p64.c:1581, SaveMem) or one y4m (WriteIob io.c:686).
+ *
+ * Flags follow the reference (p64.c:262-404, p64.1):
+ *   -NTSC | -CIF | -QCIF   picture format (checked against the y4m header)
+ *   -y4m                    y4m input (encode) / output (decode)
+ *   -a n  -b n  -k n        first / last frame, frame skip (TR = frame mod 32)
+ *   -q n  -i n              quantiser 1..31, search limit 1..31 (BoundValue)
+ *   -s file                 stream file (default <prefix>.p64)
+ *   -z suffix               component file suffix (default .y4m with -y4m)
+ *   -d                      decode
+ *   -                       y4m from stdin
+ * Additions: -full / -tss (FastBME vs the shipped StepBME), -D device.
+ * Not supported here (CPU policy rows of SURVEY.md 8(f)4): -r/-x rate control,
+ * -o interpreter, -p parity, -y reference DCT, raw component-file input.
+ *
+ * Differences from the reference: a y4m that ends before -b finishes the
+ * stream (trailer written) instead of exit(ERROR_BOUNDS) with an unterminated
+ * file; every failure exits non-zero with a message, never a segfault.
+ */
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../../include/p64gpu.h"
+#include "../../include/p64stream.h"
+
+static const char *const FMT_NAME[3] = {"QCIF", "CIF", "NTSC"};
+
+static int die(const char *what, int s) {
+  fprintf(stderr, "p64gpu: %s: %s (%s)\n", what, p64gpu_strerror(s), p64gpu_last_error());
+  return 2;
+}
+
+static int read_y4m_header(FILE *f, int *w, int *h) {
+  char line[512];
+  if (!fgets(line, sizeof line, f) || strncmp(line, "YUV4MPEG2", 9)) return -1;
+  *w = *h = 0;
+  for (char *t = strtok(line, " \n"); t; t = strtok(NULL, " \n")) {
+    if (t[0] == 'W') *w = atoi(t + 1);
+    if (t[0] == 'H') *h = atoi(t + 1);
+    if (t[0] == 'C' && strncmp(t, "C420", 4)) return -2; /* 4:2:0 only */
+  }
+  return (*w > 0 && *h > 0) ? 0 : -1;
+}
+
+static int read_frame(FILE *f, unsigned char *buf, size_t n) {
+  char line[256];
+  if (!fgets(line, sizeof line, f)) return 0;
+  if (strncmp(line, "FRAME", 5)) return -1;
+  return fread(buf, 1, n, f) == n ? 1 : -1;
+}
+
+static int drain(p64s_writer *wr, FILE *o) {
+  size_t n;
+  const uint8_t *d = p64s_writer_data(wr, &n, NULL);
+  if (n && fwrite(d, 1, n, o) != n) return -1;
+  return n ? p64s_writer_consume(wr, n) : 0;
+}
+
+typedef struct {
+  int format, y4m, first, last, skip, quant, sl, mode, device, decode, from_stdin;
+  const char *prefix, *suffix, *stream;
+} opts;
+
+static int encode(const opts *o) {
+  char path[4096];
+  FILE *f;
+  if (o->from_stdin) {
+    f = stdin;
+  } else {
+    snprintf(path, sizeof path, "%s%s", o->prefix, o->suffix ? o->suffix : (o->y4m ? ".y4m" : ""));
+    f = fopen(path, "rb");
+  }
+  if (!o->y4m) {
+    fprintf(stderr, "p64gpu: only -y4m input is supported\n");
+    return 1;
+  }
+  int w, h, s;
+  if (!f || read_y4m_header(f, &w, &h)) {
+    fprintf(stderr, "p64gpu: cannot read y4m input\n");
+    return 1;
+  }
+  const int fmt = p64s_format_of(w, h);
+  if (fmt < 0 || (o->format >= 0 && fmt != o->format)) {
+    fprintf(stderr, "p64gpu: y4m is %dx%d, not %s\n", w, h, o->format >= 0 ? FMT_NAME[o->format] : "QCIF/CIF/NTSC");
+    return 1;
+  }
+  int ngob;
+  p64s_geometry(fmt, NULL, NULL, &ngob);
+  const size_t pic = (size_t)w * h * 3 / 2;
+  const int nmb = ngob * 33;
+  unsigned char *buf = malloc(pic);
+  int16_t *coef = malloc((size_t)nmb * 384 * sizeof(int16_t));
+  p64_mb_rec *mb = malloc((size_t)nmb * sizeof(p64_mb_rec));
+  uint8_t gq[12];
+  for (int g = 0; g < ngob; g++) gq[g] = (uint8_t)o->quant;
+  /* seek to StartFrame (p64.c:562-565) */
+  for (int i = 0; i < o->first; i++)
+    if (read_frame(f, buf, pic) != 1) {
+      fprintf(stderr, "p64gpu: input ends before frame %d\n", o->first);
+      return 1;
+    }
+  char spath[4096];
+  if (o->stream) snprintf(spath, sizeof spath, "%s", o->stream);
+  else snprintf(spath, sizeof spath, "%s.p64", o->prefix);
+  FILE *out = fopen(spath, "wb");
+  if (!out) {
+    fprintf(stderr, "p64gpu: cannot open %s\n", spath);
+    return 1;
+  }
+  p64gpu_encoder *enc = NULL;
+  p64s_writer *wr = NULL;
+  if ((s = p64gpu_encoder_open(o->device, w, h, o->mode, o->sl, &enc))) return die("encoder_open", s);
+  if ((s = p64s_writer_open(&wr))) return die("writer_open", s);
+  int hist[10] = {0}, coded = 0, cur = o->first;
+  int64_t bits0 = 0;
+  printf("START>SEQUENCE\n");
+  for (; cur <= o->last; cur += o->skip) {
+    const int r = read_frame(f, buf, pic);
+    if (r <= 0) {
+      if (r < 0) fprintf(stderr, "p64gpu: bad y4m frame at %d\n", cur);
+      break;
+    }
+    if ((s = p64gpu_encoder_frame(enc, buf, cur == o->first, o->quant, NULL, coef, mb, NULL, NULL)))
+      return die("encode", s);
+    if ((s = p64s_write_picture(wr, fmt, cur % 32, gq, NULL, mb, coef))) return die("write", s);
+    int64_t bits;
+    p64s_writer_data(wr, NULL, &bits);
+    for (int k = 0; k < nmb; k++) hist[mb[k].mtype]++;
+    printf("END>Frame: %d  bits %lld\n", cur, (long long)(bits - bits0));
+    bits0 = bits;
+    if (drain(wr, out)) {
+      fprintf(stderr, "p64gpu: write error on %s\n", spath);
+      return 1;
+    }
+    coded++;
+  }
+  /* trailer: p64.c:606-610 */
+  if (cur > o->last + 1) cur = o->last + 1;
+  if ((s = p64s_write_end(wr, fmt, cur % 32))) return die("write_end", s);
+  if (drain(wr, out) || fclose(out)) {
+    fprintf(stderr, "p64gpu: write error on %s\n", spath);
+    return 1;
+  }
+  printf("END>SEQUENCE\nframes %d  MTYPE histogram:", coded);
+  for (int k = 0; k < 10; k++) printf(" %d", hist[k]);
+  printf("\n");
+  p64s_writer_close(wr);
+  p64gpu_encoder_close(enc);
+  if (f != stdin) fclose(f);
+  free(buf);
+  free(coef);
+  free(mb);
+  return 0;
+}
+
+static int save(const char *path, const uint8_t *d, size_t n) {
+  FILE *f = fopen(path, "wb");
+  if (!f || fwrite(d, 1, n, f) != n || fclose(f)) {
+    fprintf(stderr, "p64gpu: cannot write %s\n", path);
+    return 1;
+  }
+  return 0;
+}
+
+static int decode(const opts *o) {
+  if (!o->stream) {
+    fprintf(stderr, "p64gpu: -d needs -s stream\n");
+    return 1;
+  }
+  FILE *f = fopen(o->stream, "rb");
+  if (!f) {
+    fprintf(stderr, "p64gpu: cannot read %s\n", o->stream);
+    return 1;
+  }
+  fseek(f, 0, SEEK_END);
+  const long len = ftell(f);
+  fseek(f, 0, SEEK_SET);
+  uint8_t *data = malloc(len > 0 ? (size_t)len : 1);
+  if (len < 0 || fread(data, 1, (size_t)len, f) != (size_t)len) {
+    fprintf(stderr, "p64gpu: read error on %s\n", o->stream);
+    return 1;
+  }
+  fclose(f);
+  p64s_reader *rd;
+  p64s_picture_info info;
+  int s;
+  if ((s = p64s_reader_open(data, (size_t)len, &rd))) return die("reader_open", s);
+  p64s_reader_info(rd, &info);
+  const int w = info.width, h = info.height, nmb = info.ngob * 33;
+  const size_t pic = (size_t)w * h * 3 / 2;
+  if ((s = p64gpu_set_device(o->device))) return die("set_device", s);
+  p64_mb_rec *mb = malloc(nmb * sizeof *mb);
+  uint8_t *qm = malloc(nmb), *coded = malloc(nmb), *host = calloc(pic, 1);
+  int16_t *coef = malloc((size_t)nmb * 384 * sizeof *coef);
+  uint8_t *d_pic[2], *d_qm, *d_coded;
+  int16_t *d_coef;
+  p64_mb_rec *d_mb;
+  if ((s = p64gpu_alloc((void **)&d_pic[0], pic)) || (s = p64gpu_alloc((void **)&d_pic[1], pic)) ||
+      (s = p64gpu_alloc((void **)&d_qm, nmb)) || (s = p64gpu_alloc((void **)&d_coded, nmb)) ||
+      (s = p64gpu_alloc((void **)&d_coef, (size_t)nmb * 384 * sizeof *coef)) ||
+      (s = p64gpu_alloc((void **)&d_mb, nmb * sizeof *mb)) ||
+      (s = p64gpu_copy_to_device(d_pic[0], host, pic, NULL))) /* ClearFS */
+    return die("device buffers", s);
+  FILE *y4m = NULL;
+  char path[4096];
+  if (o->y4m) {
+    snprintf(path, sizeof path, "%s%s", o->prefix, o->suffix ? o->suffix : ".y4m");
+    y4m = fopen(path, "wb");
+    if (!y4m) {
+      fprintf(stderr, "p64gpu: cannot open %s\n", path);
+      return 1;
+    }
+    fprintf(y4m, "YUV4MPEG2 W%d H%d C420jpeg Ip F30000:1001\n", w, h); /* p64.c:249-251, 1102 */
+  }
+  /* frame output schedule, p64DecodeSequence p64.c:1047-1056 */
+  int frame = o->first, offset = 0, npics = 0, written = 0, prev = 0;
+  for (;;) {
+    const int r = p64s_read_picture(rd, &info, mb, qm, coded, coef);
+    if (r < 0) return die("bitstream", r);
+    if (npics) { /* the previous picture is complete: write it until TR matches */
+      int guard = 0;
+      while ((frame + offset) % 32 != info.tr && guard++ < 32) {
+        if (y4m) {
+          if (fwrite("FRAME\n", 1, 6, y4m) != 6 || fwrite(host, 1, pic, y4m) != pic) return 1;
+        } else {
+          const char *sfx[3] = {".Y", ".U", ".V"};
+          const size_t off[3] = {0, (size_t)w * h, (size_t)w * h * 5 / 4};
+          const size_t n[3] = {(size_t)w * h, (size_t)w * h / 4, (size_t)w * h / 4};
+          for (int c = 0; c < 3; c++) {
+            snprintf(path, sizeof path, "%s%d%s", o->prefix, frame, sfx[c]);
+            if (save(path, host + off[c], n[c])) return 1;
+          }
+        }
+        printf("END> Frame: %d\n", frame);
+        frame++;
+        written++;
+      }
+    }
+    if (r == 0) break;
+    if (!npics) offset = (info.tr - frame) % 32;
+    /* recon starts as the previous picture: untransmitted MBs keep it */
+    uint8_t *ref = d_pic[prev], *rec = d_pic[prev ^ 1];
+    if ((s = p64gpu_copy_on_device(rec, ref, pic, NULL)) ||
+        (s = p64gpu_copy_to_device(d_mb, mb, nmb * sizeof *mb, NULL)) ||
+        (s = p64gpu_copy_to_device(d_qm, qm, nmb, NULL)) ||
+        (s = p64gpu_copy_to_device(d_coded, coded, nmb, NULL)) ||
+        (s = p64gpu_copy_to_device(d_coef, coef, (size_t)nmb * 384 * sizeof *coef, NULL)) ||
+        (s = p64gpu_decode_recon(w, h, 1, (int64_t)pic, ref, rec, d_coef, d_mb, d_qm, d_coded, NULL)) ||
+        (s = p64gpu_copy_to_host(host, rec, pic, NULL)) || (s = p64gpu_synchronize(NULL)))
+      return die("decode", s);
+    prev ^= 1;
+    npics++;
+  }
+  printf("pictures %d  frames written %d\n", npics, written);
+  if (y4m && fclose(y4m)) return 1;
+  p64s_reader_close(rd);
+  free(data);
+  return 0;
+}
+
+int main(int argc, char **argv) {
+  opts o = {.format = -1, .first = 0, .last = 0, .skip = 1, .quant = 8, .sl = 15,
+            .mode = P64GPU_ME_TSS};
+  for (int i = 1; i < argc; i++) {
+    const char *a = argv[i];
+    const int more = i + 1 < argc;
+    if (!strcmp(a, "-NTSC")) o.format = P64S_NTSC;
+    else if (!strcmp(a, "-CIF")) o.format = P64S_CIF;
+    else if (!strcmp(a, "-QCIF")) o.format = P64S_QCIF;
+    else if (!strcmp(a, "-y4m")) o.y4m = 1;
+    else if (!strcmp(a, "-full")) o.mode = P64GPU_ME_FULL;
+    else if (!strcmp(a, "-tss")) o.mode = P64GPU_ME_TSS;
+    else if (!strcmp(a, "-D") && more) o.device = atoi(argv[++i]);
+    else if (!strcmp(a, "-a") && more) o.first = atoi(argv[++i]);
+    else if (!strcmp(a, "-b") && more) o.last = atoi(argv[++i]);
+    else if (!strcmp(a, "-k") && more) o.skip = atoi(argv[++i]);
+    else if (!strcmp(a, "-q") && more) o.quant = atoi(argv[++i]);
+    else if (!strcmp(a, "-i") && more) o.sl = atoi(argv[++i]);
+    else if (!strcmp(a, "-s") && more) o.stream = argv[++i];
+    else if (!strcmp(a, "-z") && more) o.suffix = argv[++i];
+    else if (!strcmp(a, "-d")) o.decode = 1;
+    else if (!strcmp(a, "-")) {
+      o.from_stdin = 1;
+      o.prefix = "stdin";
+    } else if (a[0] == '-') {
+      fprintf(stderr, "p64gpu: unsupported option %s\n", a);
+      return 1;
+    } else {
+      o.prefix = a;
+    }
+  }
+  if (!o.prefix) {
+    fprintf(stderr,
+            "usage: p64gpu [-NTSC|-CIF|-QCIF] -y4m [-a n] [-b n] [-k n] [-q q] [-i sl] [-full|-tss]\n"
+            "              [-D dev] [-s out.p64] [-z suffix] prefix|-\n"
+            "       p64gpu -d [-y4m] -s in.p64 [-z suffix] prefix\n");
+    return 1;
+  }
+  /* BoundValue (p64.c:341-352) */
+  if (o.quant < 1) o.quant = 1;
+  if (o.quant > 31) o.quant = 31;
+  if (o.sl < 1) o.sl = 1;
+  if (o.sl > 31) o.sl = 31;
+  if (o.skip < 1) o.skip = 1;
+  return o.decode ? decode(&o) : encode(&o);
+}

@@ -11,20 +11,24 @@ import pytest
 
 from conftest import REPO
 
-HEADER = os.path.join(REPO, "include", "p64gpu.h")
+HEADERS = [os.path.join(REPO, "include", h) for h in ("p64gpu.h", "p64stream.h")]
 
 
 def declared_functions():
-    text = open(HEADER).read()
-    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
-    return sorted(set(re.findall(r"\b(p64(?:gpu)?_\w+)\s*\(", text)))
+    names = set()
+    for hdr in HEADERS:
+        text = re.sub(r"/\*.*?\*/", "", open(hdr).read(), flags=re.S)
+        names |= set(re.findall(r"\b(p64(?:gpu|s)?_\w+)\s*\(", text))
+    return sorted(names)
 
 
 def test_header_declares_expected_entry_points():
     names = declared_functions()
     for n in ("p64gpu_block_op", "p64gpu_motion_estimation", "p64gpu_encode_frames",
               "p64gpu_decode_recon", "p64gpu_encoder_open", "p64gpu_encoder_frame",
-              "p64gpu_encoder_close", "p64gpu_synth_frames", "p64_synth_frame"):
+              "p64gpu_encoder_close", "p64gpu_synth_frames", "p64_synth_frame",
+              "p64gpu_copy_on_device", "p64s_write_picture", "p64s_write_end",
+              "p64s_read_picture", "p64s_reader_open"):
         assert n in names
 
 
@@ -107,7 +111,7 @@ def test_synth_is_deterministic_and_moves(p64):
 
 
 def test_host_driver_built():
-    exe = os.path.join(REPO, "p64_amd", "p64gpu_enc")
+    exe = os.path.join(REPO, "p64_amd", "p64gpu")
     assert os.access(exe, os.X_OK)
     r = subprocess.run([exe], capture_output=True, text=True)
     assert r.returncode == 1 and "usage" in r.stderr
