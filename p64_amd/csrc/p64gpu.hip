@@ -224,6 +224,9 @@ __device__ __forceinline__ int wave_sum(int v) {
   for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m);
   return v;
 }
+// wave-uniform by construction (results of wave reductions); saying so lets
+// hipcc use scalar registers and scalar branches for everything that follows
+__device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
 __device__ __forceinline__ uint32_t sad4(uint32_t a, uint32_t b, uint32_t acc) {
   return __builtin_amdgcn_sad_u8(a, b, acc);
 }
@@ -301,31 +304,39 @@ __device__ __forceinline__ int sad_zero(const MbLds &L, int lane) {
   return wave_sum((int)sad4(r, L.cur[lane], 0));
 }
 
-// FastBME (me.c:187-227) over [-sl/2, sl/2)^2.
-__device__ __forceinline__ void me_full(const MbLds &L, int w, int h, int x0, int y0, int sl,
-                                        int lane, int sad0, int &mx, int &my, int &best) {
-  const int half = lane >> 5, dxi = lane & 31;
-  const bool lane_ok = dxi < 30;
-  const int colb = (lane_ok ? dxi : 29) + 1;  // window byte column of dx = dxi-15
-  const int w0 = colb >> 2, sh = colb & 3;
+// FastBME (me.c:187-227) over [-sl/2, sl/2)^2, exact, with a partial-distortion
+// pre-pass (the GPU form of ComputeError's early exit, me.c:122-170).
+//
+// Lane layout: lane = (dy half, dx index); each lane owns the 15 candidates
+// dy = -15 + 15*half + d, d = 0..14, of its column dx = dxi - 15.  The window
+// row i of the lane's half meets current row r at candidate d = i - r, so a
+// row of window bytes, aligned once, feeds up to 15 candidates.
+//
+//  1. rows 0..7 of every candidate (half the SAD work)
+//  2. c* = the valid candidate with the least partial sum (first in scan order);
+//     its full SAD, and SAD(0,0), bound the answer: T = min(SAD(c*), SAD(0,0))
+//  3. a candidate whose partial sum already exceeds T can neither win nor tie
+//     (its SAD only grows), so rows 8..15 are summed only for the survivors:
+//     compacted into an LDS list and finished one per lane when there are few
+//     (textured content: a handful), densely otherwise (flat content, where
+//     nothing prunes)
+//  4. the winner is the least (SAD, scan order) key among c*, the survivors and
+//     (0,0), which wins ties because FastBME evaluates it first (me.c:203, 220).
+// The result is identical to the exhaustive search for every input.
+constexpr int ME_LIST_MAX = 128;  // above this many survivors, finish densely
 
-  uint32_t cs[64];  // current block, wave-uniform -> SGPR operands of v_sad_u8
+// rows [R0, R1) of the current block against window rows [I0, I1) of the lane
+template <int R0, int R1, int I0, int I1>
+__device__ __forceinline__ void full_rows(const uint32_t *wrow, int sh, const uint32_t *cs,
+                                          uint32_t *acc) {
 #pragma unroll
-  for (int k = 0; k < 64; k++) cs[k] = __builtin_amdgcn_readfirstlane(L.cur[k]);
-
-  uint32_t acc[15];
-#pragma unroll
-  for (int d = 0; d < 15; d++) acc[d] = 0;
-
-  const uint32_t *wrow = L.win + (15 * half) * WIN_WORDS + w0;
-#pragma unroll
-  for (int i = 0; i < 30; i++) {  // window row of this lane's dy-half
+  for (int i = I0; i < I1; i++) {
     const uint32_t *p = wrow + i * WIN_WORDS;
     const uint32_t a0 = p[0], a1 = p[1], a2 = p[2], a3 = p[3], a4 = p[4];
     const uint32_t r0 = align4(a1, a0, sh), r1 = align4(a2, a1, sh);
     const uint32_t r2 = align4(a3, a2, sh), r3 = align4(a4, a3, sh);
 #pragma unroll
-    for (int r = 0; r < 16; r++) {  // current row r meets candidate dy-index d = i - r
+    for (int r = R0; r < R1; r++) {
       const int d = i - r;
       if (d >= 0 && d < 15) {
         uint32_t a = acc[d];
@@ -336,36 +347,131 @@ __device__ __forceinline__ void me_full(const MbLds &L, int w, int h, int x0, in
         acc[d] = a;
       }
     }
+    // keep the scheduler from hoisting later rows' loads: occupancy, not
+    // single-wave latency, hides LDS latency here
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+// current-block rows r0..r0+n-1 as wave-uniform dwords, read straight from
+// global memory into SGPRs (scalar loads: no vector instructions spent)
+template <int R0, int N>
+__device__ __forceinline__ void load_cur_rows(const uint8_t *cur_blk, int w, uint32_t *cs) {
+#pragma unroll
+  for (int r = R0; r < R0 + N; r++) {
+    const uint4 v = *reinterpret_cast<const uint4 *>(cur_blk + (size_t)r * w);
+    cs[4 * r + 0] = v.x;
+    cs[4 * r + 1] = v.y;
+    cs[4 * r + 2] = v.z;
+    cs[4 * r + 3] = v.w;
+  }
+}
+
+__device__ __forceinline__ void me_full(MbLds &L, const uint8_t *cur_blk, int w, int h, int x0,
+                                        int y0, int sl, int lane, int sad0, int &mx, int &my,
+                                        int &best) {
+  const int half = lane >> 5, dxi = lane & 31;
+  const bool lane_ok = dxi < 30;
+  const int colb = (lane_ok ? dxi : 29) + 1;  // window byte column of dx = dxi-15
+  const int w0 = colb >> 2, sh = colb & 3;
+  const uint32_t *wrow = L.win + (15 * half) * WIN_WORDS + w0;
+
+  // Validity (me.c:206-212: range and `< W-16`) is folded into the sums: an
+  // invalid candidate starts at INVALID, above any real SAD (<= 65280), so it
+  // never survives and never wins, and needs no per-candidate test later.
+  constexpr uint32_t INVALID = 1u << 19;
+  const int hl = sl >> 1;
+  const int dx = dxi - 15, px = x0 + dx;
+  const bool col_ok = lane_ok && dx >= -hl && dx < hl && px >= 0 && px < w - 16;
+  // valid dy: [max(-hl, -y0), min(hl, h-16-y0)), i.e. d in [dlo, dhi) for this half
+  const int dlo = max(-hl, -y0) + 15 - 15 * half, dhi = min(hl, h - 16 - y0) + 15 - 15 * half;
+  const bool all_rows = dlo <= 0 && dhi >= 15;
+  uint32_t acc[15];
+  if (uni(__all(!lane_ok || (col_ok && all_rows)))) {  // interior: one select for all
+    const uint32_t init = lane_ok ? 0u : INVALID;
+#pragma unroll
+    for (int d = 0; d < 15; d++) acc[d] = init;
+  } else {
+#pragma unroll
+    for (int d = 0; d < 15; d++) acc[d] = (col_ok && d >= dlo && d < dhi) ? 0u : INVALID;
   }
 
-  // key = SAD<<11 | (1 + scan order); scan order (dx+15)*30+(dy+15) is
-  // FastBME's dx-major order; order 0 is reserved for the (0,0) vector, which
-  // wins every tie because it is evaluated first (me.c:203, 220).
-  const int hl = sl >> 1;
+  uint32_t cs[64];
+  load_cur_rows<0, 8>(cur_blk, w, cs);
+  // 1. rows 0..7
+  full_rows<0, 8, 0, 22>(wrow, sh, cs, acc);
+  load_cur_rows<8, 8>(cur_blk, w, cs);
+
+  // key = SUM<<11 | (1 + scan order); scan order (dx+15)*30+(dy+15)
   const unsigned base = (unsigned)(dxi * 30 + 15 * half + 1);
-  unsigned bk = 0xFFFFFFFFu;
-  const bool interior = hl == 15 && x0 >= 16 && x0 + 32 <= w && y0 >= 16 && y0 + 32 <= h;
-  if (interior) {  // every candidate of every working lane is inside the picture
+  // 2. c* and its full SAD
+  unsigned pk = 0xFFFFFFFFu;
 #pragma unroll
-    for (int d = 0; d < 15; d += 3) {
-      const unsigned k0 = (acc[d] << 11) + base + d;
-      const unsigned k1 = (acc[d + 1] << 11) + base + d + 1;
-      const unsigned k2 = (acc[d + 2] << 11) + base + d + 2;
-      bk = min(bk, min(k0, min(k1, k2)));
-    }
-    if (!lane_ok) bk = 0xFFFFFFFFu;
+  for (int d = 0; d < 15; d++) pk = min(pk, (acc[d] << 11) + base + d);
+  pk = uni((int)wave_min(pk));
+  unsigned ckey = 0xFFFFFFFFu;  // full key of c* (none if nothing is valid)
+  if ((pk >> 11) < INVALID) {
+    const int ord = (int)(pk & 2047u) - 1;
+    const int cdx = ord / 30 - 15, cdy = ord % 30 - 15;
+    const int cb = WIN_OX + cdx + 4 * (lane & 3);
+    const uint32_t *p = L.win + (WIN_OY + cdy + 8 + ((lane >> 2) & 7)) * WIN_WORDS + (cb >> 2);
+    const uint32_t s = lane < 32 ? sad4(align4(p[1], p[0], cb & 3), L.cur[32 + lane], 0u) : 0u;
+    ckey = pk + ((unsigned)uni(wave_sum((int)s)) << 11);
+  }
+  const unsigned T = min(ckey >> 11, (unsigned)sad0);
+
+  // 3. survivors: partial <= T (c* itself included: one more list entry is free)
+  int nsurv = 0;
+#pragma unroll
+  for (int d = 0; d < 15; d++) nsurv += __popcll(__ballot(acc[d] <= T));
+  nsurv = uni(nsurv);
+
+  unsigned bk = 0xFFFFFFFFu;
+  if (nsurv > ME_LIST_MAX) {  // little pruned: finish every candidate densely
+    full_rows<8, 16, 8, 30>(wrow, sh, cs, acc);
+#pragma unroll
+    for (int d = 0; d < 15; d++) bk = min(bk, (acc[d] << 11) + base + d);
   } else {
-    const int dx = dxi - 15, px = x0 + dx;
-    const bool col_ok = lane_ok && dx >= -hl && dx < hl && px >= 0 && px < w - 16;
+    // compact the survivors' partial keys into LDS (the DCT scratch is free
+    // during the search), then finish them 64 at a time, one per lane
+    uint32_t *list = reinterpret_cast<uint32_t *>(L.blk);
+    int pos = 0;
 #pragma unroll
     for (int d = 0; d < 15; d++) {
-      const int dy = -15 + 15 * half + d, py = y0 + dy;
-      const bool ok = col_ok && dy >= -hl && dy < hl && py >= 0 && py < h - 16;
-      const unsigned key = (acc[d] << 11) + base + d;
-      if (ok && key < bk) bk = key;
+      const bool sv = acc[d] <= T;
+      const uint64_t bl = __ballot(sv);
+      if (bl) {
+        const int idx = pos + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bl >> 32),
+                                                             __builtin_amdgcn_mbcnt_lo((uint32_t)bl, 0u));
+        if (sv) list[idx] = (acc[d] << 11) + base + d;
+        pos += __popcll(bl);
+      }
+    }
+    __syncthreads();
+    for (int c0 = 0; c0 < nsurv; c0 += 64) {
+      if (c0 + lane < nsurv) {
+        const unsigned pk_i = list[c0 + lane];
+        const int ord = (int)(pk_i & 2047u) - 1;
+        const int cdx = ord / 30 - 15, cdy = ord % 30 - 15;
+        const int cb = WIN_OX + cdx, csh = cb & 3;
+        const uint32_t *p0 = L.win + (WIN_OY + cdy + 8) * WIN_WORDS + (cb >> 2);
+        uint32_t a = 0;
+#pragma unroll
+        for (int r = 8; r < 16; r++) {
+          const uint32_t *p = p0 + (r - 8) * WIN_WORDS;
+          const uint32_t a0 = p[0], a1 = p[1], a2 = p[2], a3 = p[3], a4 = p[4];
+          a = sad4(align4(a1, a0, csh), cs[4 * r + 0], a);
+          a = sad4(align4(a2, a1, csh), cs[4 * r + 1], a);
+          a = sad4(align4(a3, a2, csh), cs[4 * r + 2], a);
+          a = sad4(align4(a4, a3, csh), cs[4 * r + 3], a);
+        }
+        bk = min(bk, pk_i + (a << 11));
+      }
     }
   }
-  bk = min(wave_min(bk), (unsigned)sad0 << 11);
+
+  // 4. winner
+  bk = min(min(wave_min(bk), ckey), (unsigned)sad0 << 11);
   const int ord = (int)(bk & 2047u);
   best = (int)(bk >> 11);
   if (ord == 0) {
@@ -448,17 +554,14 @@ __device__ __forceinline__ void me_stats(const MbLds &L, int lane, MeOut &o) {
   o.mwor = sum;
 }
 
-// wave-uniform by construction (results of wave reductions); saying so lets
-// hipcc use scalar registers and scalar branches for everything that follows
-__device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
 
 template <int MODE>  // 1 = TSS, 2 = FULL
-__device__ __forceinline__ MeOut motion_estimate(MbLds &L, int w, int h, int x0, int y0, int sl,
-                                                 int lane) {
+__device__ __forceinline__ MeOut motion_estimate(MbLds &L, const uint8_t *cur_y, int w, int h,
+                                                 int x0, int y0, int sl, int lane) {
   MeOut o;
   o.sad0 = uni(sad_zero(L, lane));
   if (MODE == 2)
-    me_full(L, w, h, x0, y0, sl, lane, o.sad0, o.mx, o.my, o.sad);
+    me_full(L, cur_y + (size_t)y0 * w + x0, w, h, x0, y0, sl, lane, o.sad0, o.mx, o.my, o.sad);
   else
     me_tss(L, w, h, x0, y0, lane, o.sad0, o.mx, o.my, o.sad);
   o.mx = uni(o.mx);
@@ -758,7 +861,7 @@ __global__ __launch_bounds__(64) void k_encode(p64gpu_encode_args a) {
   if (MODE != 0) {
     stage_luma(L, ref.y, cur.y, w, h, x0, y0, lane);
     __syncthreads();
-    const MeOut me = motion_estimate<MODE>(L, w, h, x0, y0, a.search_limit, lane);
+    const MeOut me = motion_estimate<MODE>(L, cur.y, w, h, x0, y0, a.search_limit, lane);
     if (a.me && lane == 0) {
       p64_me_rec o;
       o.mx = me.mx;
@@ -873,7 +976,7 @@ __global__ __launch_bounds__(64) void k_motion(int w, int h, int64_t stride, con
   const int x0 = 16 * (mb % mbw), y0 = 16 * (mb / mbw);
   stage_luma(L, ref_y + (size_t)fi * stride, cur_y + (size_t)fi * stride, w, h, x0, y0, lane);
   __syncthreads();
-  const MeOut me = motion_estimate<MODE>(L, w, h, x0, y0, sl, lane);
+  const MeOut me = motion_estimate<MODE>(L, cur_y + (size_t)fi * stride, w, h, x0, y0, sl, lane);
   if (lane == 0) {
     p64_me_rec o;
     o.mx = me.mx;
