@@ -312,18 +312,25 @@ __device__ __forceinline__ int sad_zero(const MbLds &L, int lane) {
 // row i of the lane's half meets current row r at candidate d = i - r, so a
 // row of window bytes, aligned once, feeds up to 15 candidates.
 //
-//  1. rows 0..7 of every candidate (half the SAD work)
+//  1. rows 0..MP-1 of every candidate (MP = 6: 3/8 of the SAD work)
 //  2. c* = the valid candidate with the least partial sum (first in scan order);
 //     its full SAD, and SAD(0,0), bound the answer: T = min(SAD(c*), SAD(0,0))
 //  3. a candidate whose partial sum already exceeds T can neither win nor tie
-//     (its SAD only grows), so rows 8..15 are summed only for the survivors:
+//     (its SAD only grows), so rows MP..15 are summed only for the survivors:
 //     compacted into an LDS list and finished one per lane when there are few
 //     (textured content: a handful), densely otherwise (flat content, where
 //     nothing prunes)
 //  4. the winner is the least (SAD, scan order) key among c*, the survivors and
 //     (0,0), which wins ties because FastBME evaluates it first (me.c:203, 220).
 // The result is identical to the exhaustive search for every input.
-constexpr int ME_LIST_MAX = 128;  // above this many survivors, finish densely
+#ifndef ME_PARTIAL_ROWS
+#define ME_PARTIAL_ROWS 6
+#endif
+#ifndef ME_LIST_MAX
+#define ME_LIST_MAX 256
+#endif
+constexpr int MP = ME_PARTIAL_ROWS;  // rows of every candidate in the pre-pass
+static_assert(ME_LIST_MAX <= 6 * BLK_STRIDE, "survivor list lives in the DCT scratch");
 
 // rows [R0, R1) of the current block against window rows [I0, I1) of the lane
 template <int R0, int R1, int I0, int I1>
@@ -397,10 +404,10 @@ __device__ __forceinline__ void me_full(MbLds &L, const uint8_t *cur_blk, int w,
   }
 
   uint32_t cs[64];
-  load_cur_rows<0, 8>(cur_blk, w, cs);
-  // 1. rows 0..7
-  full_rows<0, 8, 0, 22>(wrow, sh, cs, acc);
-  load_cur_rows<8, 8>(cur_blk, w, cs);
+  load_cur_rows<0, MP>(cur_blk, w, cs);
+  // 1. rows 0..MP-1
+  full_rows<0, MP, 0, MP + 14>(wrow, sh, cs, acc);
+  load_cur_rows<MP, 16 - MP>(cur_blk, w, cs);
 
   // key = SUM<<11 | (1 + scan order); scan order (dx+15)*30+(dy+15)
   const unsigned base = (unsigned)(dxi * 30 + 15 * half + 1);
@@ -414,8 +421,9 @@ __device__ __forceinline__ void me_full(MbLds &L, const uint8_t *cur_blk, int w,
     const int ord = (int)(pk & 2047u) - 1;
     const int cdx = ord / 30 - 15, cdy = ord % 30 - 15;
     const int cb = WIN_OX + cdx + 4 * (lane & 3);
-    const uint32_t *p = L.win + (WIN_OY + cdy + 8 + ((lane >> 2) & 7)) * WIN_WORDS + (cb >> 2);
-    const uint32_t s = lane < 32 ? sad4(align4(p[1], p[0], cb & 3), L.cur[32 + lane], 0u) : 0u;
+    const uint32_t *p = L.win + (WIN_OY + cdy + MP + (lane >> 2)) * WIN_WORDS + (cb >> 2);
+    const uint32_t s =
+        lane < 4 * (16 - MP) ? sad4(align4(p[1], p[0], cb & 3), L.cur[4 * MP + lane], 0u) : 0u;
     ckey = pk + ((unsigned)uni(wave_sum((int)s)) << 11);
   }
   const unsigned T = min(ckey >> 11, (unsigned)sad0);
@@ -428,7 +436,7 @@ __device__ __forceinline__ void me_full(MbLds &L, const uint8_t *cur_blk, int w,
 
   unsigned bk = 0xFFFFFFFFu;
   if (nsurv > ME_LIST_MAX) {  // little pruned: finish every candidate densely
-    full_rows<8, 16, 8, 30>(wrow, sh, cs, acc);
+    full_rows<MP, 16, MP, 30>(wrow, sh, cs, acc);
 #pragma unroll
     for (int d = 0; d < 15; d++) bk = min(bk, (acc[d] << 11) + base + d);
   } else {
@@ -454,11 +462,11 @@ __device__ __forceinline__ void me_full(MbLds &L, const uint8_t *cur_blk, int w,
         const int ord = (int)(pk_i & 2047u) - 1;
         const int cdx = ord / 30 - 15, cdy = ord % 30 - 15;
         const int cb = WIN_OX + cdx, csh = cb & 3;
-        const uint32_t *p0 = L.win + (WIN_OY + cdy + 8) * WIN_WORDS + (cb >> 2);
+        const uint32_t *p0 = L.win + (WIN_OY + cdy + MP) * WIN_WORDS + (cb >> 2);
         uint32_t a = 0;
 #pragma unroll
-        for (int r = 8; r < 16; r++) {
-          const uint32_t *p = p0 + (r - 8) * WIN_WORDS;
+        for (int r = MP; r < 16; r++) {
+          const uint32_t *p = p0 + (r - MP) * WIN_WORDS;
           const uint32_t a0 = p[0], a1 = p[1], a2 = p[2], a3 = p[3], a4 = p[4];
           a = sad4(align4(a1, a0, csh), cs[4 * r + 0], a);
           a = sad4(align4(a2, a1, csh), cs[4 * r + 1], a);
