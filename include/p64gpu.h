@@ -159,6 +159,13 @@ typedef struct {
 } p64gpu_encode_args;
 
 int p64gpu_encode_frames(const p64gpu_encode_args *args, void *stream);
+/* The same for one picture (args->nframes == 1) restricted to the count
+ * macroblocks listed in mb_list (device array of raster indices; entries out
+ * of range are skipped).  Hosts that decide per GOB -- rate control sets
+ * GQUANT from the bits written so far (p64.c:697-712) -- encode a picture GOB
+ * by GOB with it; outputs of MBs not listed are left untouched. */
+int p64gpu_encode_mb_list(const p64gpu_encode_args *args, const int32_t *mb_list, int count,
+                          void *stream);
 
 /* ---- decoder-side reconstruction (device pointers) ---------------------- */
 /* recon must already hold the previous picture where MBs are not coded

@@ -61,6 +61,17 @@ void p64s_writer_close(p64s_writer *w);
  * carries coefficients, exactly as WriteMDU. */
 int p64s_write_picture(p64s_writer *w, int format, int tr, const uint8_t *gquant,
                        const uint8_t *quant_mb, const p64_mb_rec *mb, const int16_t *coef);
+/* The same at finer grain, for hosts that decide per GOB or per MB while
+ * writing (rate control, p64.c:697-786): a picture header, then per GOB its
+ * header (resets the MBA/MVD predictors) and its macroblocks in increasing MDU
+ * order (MDUs skipped are absent from the stream).  mquant is used only for
+ * MTYPEs 1/3/6/9.  coef = the macroblock's 6x64 zigzag levels. */
+int p64s_write_picture_header(p64s_writer *w, int format, int tr);
+int p64s_write_gob_header(p64s_writer *w, int gob, int gquant);
+int p64s_write_mb(p64s_writer *w, int mdu, const p64_mb_rec *mb, const int16_t *coef, int mquant);
+/* Raster macroblock index of MDU m (0..32) of GOB g (Bpos, io.c:757), -1 if
+ * out of range. */
+int p64s_raster_mb(int format, int gob, int mdu);
 /* Trailing picture header (tr = frame after the last, mod 32) and final
  * ones-padding.  The writer accepts no more pictures afterwards. */
 int p64s_write_end(p64s_writer *w, int format, int tr);

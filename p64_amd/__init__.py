@@ -137,6 +137,19 @@ def lib() -> ctypes.CDLL:
     L.p64s_reader_close.restype = None
     L.p64s_reader_info.argtypes = [vp, vp]
     L.p64s_read_picture.argtypes = [vp, vp, vp, vp, vp, vp]
+    # sequence encoder (include/p64seq.h), host C over the GPU path
+    L.p64seq_default_config.argtypes = [vp]
+    L.p64seq_default_config.restype = None
+    L.p64seq_open.argtypes = [vp, ctypes.POINTER(vp)]
+    L.p64seq_close.argtypes = [vp]
+    L.p64seq_close.restype = None
+    L.p64seq_more.argtypes = [vp]
+    L.p64seq_encode.argtypes = [vp, vp]
+    L.p64seq_finish.argtypes = [vp]
+    L.p64seq_writer.argtypes = [vp]
+    L.p64seq_writer.restype = vp
+    L.p64seq_get_stats.argtypes = [vp, vp]
+    L.p64gpu_encode_mb_list.argtypes = [ctypes.POINTER(EncodeArgs), vp, i32, vp]
     if L.p64gpu_abi_version() != 1:
         raise P64GpuError("libp64gpu.so ABI version mismatch")
     _lib = L

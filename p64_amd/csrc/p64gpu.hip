@@ -845,12 +845,20 @@ __device__ __forceinline__ CbpOut cbp_decide(const int lev[6]) {
 // MODE: 0 intra picture, 1 TSS, 2 FULL.
 
 template <int MODE>
-__global__ __launch_bounds__(64) void k_encode(p64gpu_encode_args a) {
+__global__ __launch_bounds__(64) void k_encode(p64gpu_encode_args a, const int32_t *mb_list) {
   __shared__ MbLds L;
   const int lane = threadIdx.x;
   const int w = a.width, h = a.height, mbw = w >> 4, nmb = mbw * (h >> 4);
-  const unsigned gid = xcd_remap(blockIdx.x, gridDim.x);
-  const int fi = (int)(gid / (unsigned)nmb), mb = (int)(gid - (unsigned)fi * nmb);
+  int fi, mb;
+  if (mb_list) {  // one picture, listed macroblocks only (p64gpu_encode_mb_list)
+    fi = 0;
+    mb = mb_list[blockIdx.x];
+    if (mb < 0 || mb >= nmb) return;  // whole workgroup
+  } else {
+    const unsigned gid = xcd_remap(blockIdx.x, gridDim.x);
+    fi = (int)(gid / (unsigned)nmb);
+    mb = (int)(gid - (unsigned)fi * nmb);
+  }
   const int mbx = mb % mbw, mby = mb / mbw, x0 = 16 * mbx, y0 = 16 * mby;
   const size_t gmb = (size_t)fi * nmb + mb;
   const Picture cur = picture_at(a.cur + (size_t)fi * a.frame_stride, w, h);
@@ -1284,7 +1292,25 @@ int p64gpu_motion_estimation(int w, int h, int nframes, int64_t stride, const ui
   return P64GPU_OK;
 }
 
+static int encode_launch(const p64gpu_encode_args *a, const int32_t *mb_list, int count,
+                         void *stream);
+
 int p64gpu_encode_frames(const p64gpu_encode_args *a, void *stream) {
+  return encode_launch(a, nullptr, 0, stream);
+}
+
+int p64gpu_encode_mb_list(const p64gpu_encode_args *a, const int32_t *mb_list, int count,
+                          void *stream) {
+  if (!a) return fail(P64GPU_E_INVALID, "args is NULL");
+  if (a->nframes != 1) return fail(P64GPU_E_INVALID, "mb list needs nframes = 1");
+  if (!mb_list || count < 0 || count > (a->width / 16) * (a->height / 16))
+    return fail(P64GPU_E_INVALID, "mb list %p count %d", (const void *)mb_list, count);
+  if (count == 0) return P64GPU_OK;
+  return encode_launch(a, mb_list, count, stream);
+}
+
+static int encode_launch(const p64gpu_encode_args *a, const int32_t *mb_list, int count,
+                         void *stream) {
   if (!a) return fail(P64GPU_E_INVALID, "args is NULL");
   int s = check_geometry(a->width, a->height, a->nframes, a->frame_stride);
   if (s) return s;
@@ -1300,14 +1326,15 @@ int p64gpu_encode_frames(const p64gpu_encode_args *a, void *stream) {
   if (a->search_limit < 1 || a->search_limit > 31)
     return fail(P64GPU_E_INVALID, "search_limit %d not in 1..31", a->search_limit);
   if (a->reserved != 0) return fail(P64GPU_E_INVALID, "reserved must be 0");
-  const unsigned grid = (unsigned)((int64_t)a->nframes * (a->width / 16) * (a->height / 16));
+  const unsigned grid =
+      mb_list ? (unsigned)count : (unsigned)((int64_t)a->nframes * (a->width / 16) * (a->height / 16));
   hipStream_t st = (hipStream_t)stream;
   if (a->intra)
-    hipLaunchKernelGGL(k_encode<0>, dim3(grid), dim3(64), 0, st, *a);
+    hipLaunchKernelGGL(k_encode<0>, dim3(grid), dim3(64), 0, st, *a, mb_list);
   else if (a->me_mode == P64GPU_ME_FULL)
-    hipLaunchKernelGGL(k_encode<2>, dim3(grid), dim3(64), 0, st, *a);
+    hipLaunchKernelGGL(k_encode<2>, dim3(grid), dim3(64), 0, st, *a, mb_list);
   else
-    hipLaunchKernelGGL(k_encode<1>, dim3(grid), dim3(64), 0, st, *a);
+    hipLaunchKernelGGL(k_encode<1>, dim3(grid), dim3(64), 0, st, *a, mb_list);
   HIP_TRY(hipGetLastError());
   return P64GPU_OK;
 }

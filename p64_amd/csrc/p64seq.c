@@ -1,0 +1,343 @@
+/*
+ * p64seq.c -- sequence loop and rate control of the reference encoder over the
+ * GPU hot path (include/p64seq.h).  Host C on the public C ABI only.
+ *
+ * Integer arithmetic follows the reference's C `int` expressions, including
+ * their 32-bit wrap-around (computed in uint32_t and converted back), so the
+ * bit budget and the quantiser choices match for every -r / -x / -k / -f.
+ */
+#include <stdarg.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../../include/p64seq.h"
+
+int p64gpu_fail_(int status, const char *msg); /* p64gpu.hip: sets last error */
+
+static int fail(int status, const char *fmt, ...) __attribute__((format(printf, 2, 3)));
+static int fail(int status, const char *fmt, ...) {
+  char buf[256];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  return p64gpu_fail_(status, buf);
+}
+
+/* C int arithmetic with the wrap-around the reference's expressions have */
+static int32_t imul(int32_t a, int32_t b) { return (int32_t)((uint32_t)a * (uint32_t)b); }
+static int32_t idiv(int32_t a, int32_t b) { return b ? a / b : 0; }
+
+struct p64seq {
+  p64seq_config c;
+  int w, h, ngob, nmb;
+  size_t pic;
+  /* device */
+  uint8_t *d_cur, *d_rec[2], *d_li, *d_q, *d_mask;
+  int16_t *d_coef;
+  p64_mb_rec *d_mb;
+  int32_t *d_lists; /* [ngob][33] raster MB indices of each GOB */
+  int cur;          /* d_rec[cur] receives this picture; d_rec[cur ^ 1] = CFS */
+  /* host */
+  int16_t *h_coef;
+  p64_mb_rec *h_mb;
+  uint8_t *h_li_old, *h_li, *h_mask, *h_q;
+  int32_t *h_lists;
+  p64s_writer *wr;
+  /* reference state (p64.c globals) */
+  int current_frame, rate, qdfact, qoffs, gquant, buffer_offset, novfl, frames, finished;
+  int64_t total_bits, last_bits, first_frame_bits;
+  int hist[10];
+};
+
+void p64seq_default_config(p64seq_config *c) {
+  memset(c, 0, sizeof *c);
+  c->search_limit = 15;
+  c->frame_skip = 1;
+  c->frame_rate = 30000;
+  c->frame_rate_div = 1001;
+}
+
+void p64seq_close(p64seq *s) {
+  if (!s) return;
+  p64gpu_free(s->d_cur);
+  p64gpu_free(s->d_rec[0]);
+  p64gpu_free(s->d_rec[1]);
+  p64gpu_free(s->d_li);
+  p64gpu_free(s->d_q);
+  p64gpu_free(s->d_mask);
+  p64gpu_free(s->d_coef);
+  p64gpu_free(s->d_mb);
+  p64gpu_free(s->d_lists);
+  free(s->h_coef);
+  free(s->h_mb);
+  free(s->h_li_old);
+  free(s->h_li);
+  free(s->h_mask);
+  free(s->h_q);
+  free(s->h_lists);
+  p64s_writer_close(s->wr);
+  free(s);
+}
+
+int p64seq_open(const p64seq_config *cfg, p64seq **out) {
+  int st;
+  if (!cfg || !out) return fail(P64GPU_E_INVALID, "p64seq_open: NULL argument");
+  const p64seq_config *c = cfg;
+  if (c->me_mode != P64GPU_ME_TSS && c->me_mode != P64GPU_ME_FULL)
+    return fail(P64GPU_E_INVALID, "me mode %d", c->me_mode);
+  if (c->search_limit < 1 || c->search_limit > 31 || c->quant < 0 || c->quant > 31 || c->rate < 0 ||
+      c->file_size_bits < 0 || c->frame_skip < 1 || c->frame_rate < 1 || c->frame_rate_div < 1 ||
+      c->start_frame < 0 || c->last_frame < c->start_frame)
+    return fail(P64GPU_E_INVALID, "p64seq config out of range");
+  p64seq *s = (p64seq *)calloc(1, sizeof *s);
+  if (!s) return fail(P64GPU_E_NOMEM, "p64seq: calloc");
+  s->c = *c;
+  if ((st = p64s_geometry(c->format, &s->w, &s->h, &s->ngob))) {
+    free(s);
+    return st;
+  }
+  s->nmb = s->ngob * 33;
+  s->pic = (size_t)s->w * s->h * 3 / 2;
+  const size_t nmb = (size_t)s->nmb;
+  if ((st = p64gpu_set_device(c->device))) goto bad;
+  if ((st = p64gpu_alloc((void **)&s->d_cur, s->pic)) || (st = p64gpu_alloc((void **)&s->d_rec[0], s->pic)) ||
+      (st = p64gpu_alloc((void **)&s->d_rec[1], s->pic)) || (st = p64gpu_alloc((void **)&s->d_li, nmb)) ||
+      (st = p64gpu_alloc((void **)&s->d_q, nmb)) || (st = p64gpu_alloc((void **)&s->d_mask, nmb)) ||
+      (st = p64gpu_alloc((void **)&s->d_coef, nmb * 384 * sizeof(int16_t))) ||
+      (st = p64gpu_alloc((void **)&s->d_mb, nmb * sizeof(p64_mb_rec))) ||
+      (st = p64gpu_alloc((void **)&s->d_lists, nmb * sizeof(int32_t))))
+    goto bad;
+  s->h_coef = (int16_t *)calloc(nmb * 384, sizeof(int16_t));
+  s->h_mb = (p64_mb_rec *)calloc(nmb, sizeof(p64_mb_rec));
+  s->h_li_old = (uint8_t *)calloc(nmb, 1);
+  s->h_li = (uint8_t *)calloc(nmb, 1);
+  s->h_mask = (uint8_t *)calloc(nmb, 1);
+  s->h_q = (uint8_t *)calloc(nmb, 1);
+  s->h_lists = (int32_t *)calloc(nmb, sizeof(int32_t));
+  uint8_t *zero = (uint8_t *)calloc(s->pic, 1);
+  if (!s->h_coef || !s->h_mb || !s->h_li_old || !s->h_li || !s->h_mask || !s->h_q || !s->h_lists || !zero) {
+    free(zero);
+    st = fail(P64GPU_E_NOMEM, "p64seq: host buffers");
+    goto bad;
+  }
+  for (int g = 0; g < s->ngob; g++)
+    for (int m = 0; m < 33; m++) s->h_lists[g * 33 + m] = p64s_raster_mb(c->format, g, m);
+  /* InitFS + ClearFS (p64.c:531-534): both frame stores start at zero;
+   * LastIntra starts at zero (calloc, p64.c:1522-1526) */
+  if ((st = p64gpu_copy_to_device(s->d_rec[0], zero, s->pic, NULL)) ||
+      (st = p64gpu_copy_to_device(s->d_rec[1], zero, s->pic, NULL)) ||
+      (st = p64gpu_copy_to_device(s->d_li, zero, nmb, NULL)) ||
+      (st = p64gpu_copy_to_device(s->d_lists, s->h_lists, nmb * sizeof(int32_t), NULL)) ||
+      (st = p64gpu_synchronize(NULL))) {
+    free(zero);
+    goto bad;
+  }
+  free(zero);
+  if ((st = p64s_writer_open(&s->wr))) goto bad;
+
+  /* p64EncodeSequence p64.c:566-595 */
+  s->current_frame = c->start_frame;
+  int rate = c->rate, iq = c->quant;
+  if (c->file_size_bits)
+    rate = idiv(idiv(imul(c->file_size_bits, c->frame_rate), c->frame_rate_div),
+                imul(c->frame_skip, c->last_frame - c->start_frame + 1));
+  if (rate) {
+    s->qdfact = rate / 320;
+    s->qoffs = 1;
+    if (s->qdfact == 0) { /* the reference divides by QDFact (p64.c:463) */
+      st = fail(P64GPU_E_INVALID, "rate %d below 320 bits/s (QDFact would be 0)", rate);
+      goto bad;
+    }
+    if (!iq) {
+      iq = 10000000 / rate;
+      if (iq > 31) iq = 31;
+      else if (iq < 1) iq = 1;
+    }
+  }
+  if (!iq) iq = 8; /* DEFAULT_QUANTIZATION p64.c:145 */
+  s->rate = rate;
+  s->gquant = iq;
+  s->cur = 0;
+  *out = s;
+  return 0;
+bad:
+  p64seq_close(s);
+  return st;
+}
+
+int p64seq_more(const p64seq *s) { return s && !s->finished && s->current_frame <= s->c.last_frame; }
+
+p64s_writer *p64seq_writer(p64seq *s) { return s ? s->wr : NULL; }
+
+static int64_t bits_written(const p64seq *s) {
+  int64_t b;
+  p64s_writer_data(s->wr, NULL, &b);
+  return b;
+}
+
+/* BufferContents() p64.c:233-236 at GOB g, MDU m */
+static int64_t buffer_contents(const p64seq *s, int g, int m) {
+  const int32_t budget = idiv(imul(imul(g * 33 + m, s->rate), s->c.frame_skip),
+                              idiv(imul(s->ngob * 33, s->c.frame_rate), s->c.frame_rate_div));
+  return bits_written(s) + s->buffer_offset - budget;
+}
+
+/* ExecuteQuantization p64.c:458-481 without -o */
+static int rate_gquant(const p64seq *s, int g) {
+  const int cs = (int)buffer_contents(s, g, 0);
+  int q = cs / s->qdfact + s->qoffs;
+  if (q < 1) q = 1;
+  if (q > 31) q = 31;
+  return q;
+}
+
+static p64gpu_encode_args picture_args(p64seq *s, int intra) {
+  p64gpu_encode_args a;
+  memset(&a, 0, sizeof a);
+  a.width = s->w;
+  a.height = s->h;
+  a.nframes = 1;
+  a.intra = intra;
+  a.quant = s->gquant;
+  a.me_mode = s->c.me_mode;
+  a.search_limit = s->c.search_limit;
+  a.frame_stride = (int64_t)s->pic;
+  a.cur = s->d_cur;
+  a.ref = s->d_rec[s->cur ^ 1];
+  a.recon = s->d_rec[s->cur];
+  a.last_intra = s->d_li;
+  a.coef = s->d_coef;
+  a.mb = s->d_mb;
+  return a;
+}
+
+/* device -> host copy of the records of GOB g (three runs of 11 MBs for
+ * CIF/NTSC, one run of 33 for QCIF) */
+static int fetch_gob(p64seq *s, int g) {
+  int st;
+  const int runs = s->c.format == P64S_QCIF ? 1 : 3, len = 33 / runs;
+  for (int r = 0; r < runs; r++) {
+    const int k = s->h_lists[g * 33 + r * len];
+    if ((st = p64gpu_copy_to_host(s->h_mb + k, s->d_mb + k, len * sizeof(p64_mb_rec), NULL)) ||
+        (st = p64gpu_copy_to_host(s->h_coef + (size_t)k * 384, s->d_coef + (size_t)k * 384,
+                                  (size_t)len * 384 * sizeof(int16_t), NULL)))
+      return st;
+  }
+  return p64gpu_synchronize(NULL);
+}
+
+int p64seq_encode(p64seq *s, const uint8_t *picture) {
+  int st;
+  if (!s || !picture) return fail(P64GPU_E_INVALID, "p64seq_encode: NULL argument");
+  if (!p64seq_more(s)) return fail(P64GPU_E_INVALID, "p64seq_encode past the last frame");
+  const int first = s->current_frame == s->c.start_frame;
+  const size_t nmb = (size_t)s->nmb;
+  p64gpu_encode_args a = picture_args(s, first);
+  if ((st = p64gpu_copy_to_device(s->d_cur, picture, s->pic, NULL))) return st;
+  if ((st = p64s_write_picture_header(s->wr, s->c.format, s->current_frame % 32))) return st;
+
+  if (!s->rate) { /* one launch for the picture, then the VLC */
+    if ((st = p64gpu_encode_frames(&a, NULL)) ||
+        (st = p64gpu_copy_to_host(s->h_mb, s->d_mb, nmb * sizeof(p64_mb_rec), NULL)) ||
+        (st = p64gpu_copy_to_host(s->h_coef, s->d_coef, nmb * 384 * sizeof(int16_t), NULL)) ||
+        (st = p64gpu_synchronize(NULL)))
+      return st;
+    for (int g = 0; g < s->ngob; g++) {
+      if ((st = p64s_write_gob_header(s->wr, g, s->gquant))) return st;
+      for (int m = 0; m < 33; m++) {
+        const int k = s->h_lists[g * 33 + m];
+        if ((st = p64s_write_mb(s->wr, m, &s->h_mb[k], s->h_coef + (size_t)k * 384, 0))) return st;
+        s->hist[s->h_mb[k].mtype]++;
+      }
+    }
+  } else { /* rate control: GOB by GOB, GQUANT from the bits written so far */
+    int novfl = 0;
+    memset(s->h_mask, 0, nmb);
+    if ((st = p64gpu_copy_to_host(s->h_li_old, s->d_li, nmb, NULL)) || (st = p64gpu_synchronize(NULL)))
+      return st;
+    for (int g = 0; g < s->ngob; g++) {
+      if (!first) s->gquant = rate_gquant(s, g); /* p64.c:697-701 */
+      a.quant = s->gquant;
+      if ((st = p64s_write_gob_header(s->wr, g, s->gquant)) ||
+          (st = p64gpu_encode_mb_list(&a, s->d_lists + g * 33, 33, NULL)) || (st = fetch_gob(s, g)))
+        return st;
+      for (int m = 0; m < 33; m++) {
+        const int k = s->h_lists[g * 33 + m];
+        s->h_q[k] = (uint8_t)s->gquant;
+        /* buffer overflow: MTYPE 4, zero vector, no coefficients (p64.c:776-783) */
+        if (buffer_contents(s, g, m) > s->rate / 4) {
+          s->h_mb[k].mtype = 4;
+          s->h_mb[k].cbp = 0x3f;
+          s->h_mb[k].mvx = s->h_mb[k].mvy = 0;
+          memset(s->h_coef + (size_t)k * 384, 0, 384 * sizeof(int16_t));
+          s->h_mask[k] = 1;
+          novfl++;
+        }
+        if ((st = p64s_write_mb(s->wr, m, &s->h_mb[k], s->h_coef + (size_t)k * 384, 0))) return st;
+        s->hist[s->h_mb[k].mtype]++;
+      }
+    }
+    if (novfl) {
+      /* the GPU coded those MBs as it decided; redo their reconstruction as
+       * MTYPE 4 at (0,0) from the previous picture, and their LastIntra as a
+       * non-intra MB (p64.c:909-910) */
+      if ((st = p64gpu_copy_to_device(s->d_mb, s->h_mb, nmb * sizeof(p64_mb_rec), NULL)) ||
+          (st = p64gpu_copy_to_device(s->d_mask, s->h_mask, nmb, NULL)) ||
+          (st = p64gpu_copy_to_device(s->d_q, s->h_q, nmb, NULL)) ||
+          (st = p64gpu_decode_recon(s->w, s->h, 1, (int64_t)s->pic, a.ref, a.recon, s->d_coef, s->d_mb,
+                                    s->d_q, s->d_mask, NULL)) ||
+          (st = p64gpu_copy_to_host(s->h_li, s->d_li, nmb, NULL)) || (st = p64gpu_synchronize(NULL)))
+        return st;
+      for (size_t k = 0; k < nmb; k++)
+        if (s->h_mask[k]) s->h_li[k] = (uint8_t)(s->h_li_old[k] + 1);
+      if ((st = p64gpu_copy_to_device(s->d_li, s->h_li, nmb, NULL)) || (st = p64gpu_synchronize(NULL)))
+        return st;
+      s->novfl += novfl;
+    }
+  }
+
+  /* p64EncodeFrame p64.c:653-682 */
+  const int64_t x = bits_written(s);
+  s->last_bits = x - s->total_bits;
+  s->total_bits = x;
+  if (s->rate) {
+    if (first) {
+      s->first_frame_bits = s->total_bits;
+      /* CurrentGOB = NumberGOB, CurrentMDU = 0 once the GOB loop is done */
+      s->buffer_offset = (int)((s->rate / 4) / 2 - buffer_contents(s, s->ngob, 0));
+    }
+    s->buffer_offset -= idiv(imul(imul(s->rate, s->c.frame_skip), s->c.frame_rate_div), s->c.frame_rate);
+  } else if (first) {
+    s->first_frame_bits = s->total_bits;
+  }
+  s->cur ^= 1; /* SwapFS(CFS, OFS) p64.c:661 */
+  s->frames++;
+  s->current_frame += s->c.frame_skip;
+  return 0;
+}
+
+int p64seq_finish(p64seq *s) {
+  if (!s) return fail(P64GPU_E_INVALID, "p64seq_finish: NULL");
+  if (s->finished) return fail(P64GPU_E_INVALID, "p64seq_finish called twice");
+  int f = s->current_frame; /* p64.c:606-608 */
+  if (f > s->c.last_frame + 1) f = s->c.last_frame + 1;
+  s->finished = 1;
+  return p64s_write_end(s->wr, s->c.format, f % 32);
+}
+
+int p64seq_get_stats(const p64seq *s, p64seq_stats *st) {
+  if (!s || !st) return fail(P64GPU_E_INVALID, "p64seq_get_stats: NULL");
+  memset(st, 0, sizeof *st);
+  st->frames = s->frames;
+  st->next_frame = s->current_frame;
+  st->gquant = s->gquant;
+  st->rate = s->rate;
+  st->bits = bits_written(s);
+  st->last_bits = s->last_bits;
+  st->first_frame_bits = s->first_frame_bits;
+  st->overflows = s->novfl;
+  memcpy(st->mtype_hist, s->hist, sizeof s->hist);
+  return 0;
+}

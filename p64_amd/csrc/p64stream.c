@@ -57,6 +57,11 @@ int p64s_format_of(int width, int height) {
 }
 
 /* GOB g, MDU m -> raster macroblock index (Bpos/MoveTo io.c:719-783). */
+int p64s_raster_mb(int format, int g, int m) {
+  if (format < 0 || format > 2 || g < 0 || m < 0 || m >= 33) return -1;
+  return (format == P64S_QCIF) ? (3 * g + m / 11) * 11 + m % 11
+                               : ((g >> 1) * 3 + m / 11) * 22 + (g & 1) * 11 + m % 11;
+}
 static int raster_mb(int format, int g, int m) {
   if (format == P64S_QCIF) return (3 * g + m / 11) * 11 + m % 11;
   return ((g >> 1) * 3 + m / 11) * 22 + (g & 1) * 11 + m % 11;
@@ -239,6 +244,9 @@ struct p64s_writer {
   int nacc;
   int64_t bits;
   int ended, oom;
+  /* position in the picture: format, GOB (-2 none yet, -1 header only) and the
+   * MBA/MTYPE/MVD predictors of WriteMBHeader */
+  int format, gob, last_mba, last_mt, pmx, pmy;
 };
 
 /* n <= 24 bits, MSB first (mputv stream.c:180-190) */
@@ -270,7 +278,9 @@ int p64s_writer_open(p64s_writer **out) {
   int s = tables();
   if (s) return s;
   *out = (p64s_writer *)calloc(1, sizeof(p64s_writer));
-  return *out ? 0 : fail(P64GPU_E_NOMEM, "writer: calloc failed");
+  if (!*out) return fail(P64GPU_E_NOMEM, "writer: calloc failed");
+  (*out)->gob = -2;
+  return 0;
 }
 
 void p64s_writer_close(p64s_writer *w) {
@@ -351,6 +361,90 @@ static void write_block(p64s_writer *w, const int16_t *z, int intra) {
   put_vlc(w, E_EOB);
 }
 
+static int check_mb(const p64_mb_rec *r, int mquant, int k) {
+  const int mt = r->mtype;
+  if (mt < 0 || mt > 9) return fail(P64GPU_E_INVALID, "mb %d: mtype %d", k, mt);
+  if (CBP_MT[mt] && (r->cbp < 1 || r->cbp > 63))
+    return fail(P64GPU_E_INVALID, "mb %d: mtype %d with cbp %d", k, mt, r->cbp);
+  if (QUANT_MT[mt] && (mquant < 1 || mquant > 31))
+    return fail(P64GPU_E_INVALID, "mb %d: mtype %d needs MQUANT in 1..31, got %d", k, mt, mquant);
+  return 0;
+}
+
+int p64s_write_picture_header(p64s_writer *w, int format, int tr) {
+  int s;
+  if (!w) return fail(P64GPU_E_INVALID, "write_picture_header: NULL writer");
+  if (w->ended) return fail(P64GPU_E_INVALID, "write after write_end");
+  if ((s = p64s_geometry(format, NULL, NULL, NULL))) return s;
+  write_picture_header(w, format, tr);
+  w->format = format;
+  w->gob = -1;
+  return 0;
+}
+
+/* WriteGOBHeader marker.c:171-198: GBSC, GN = GRead+1 (QCIF GRead = 2g,
+ * p64.c:703-712), GQUANT, GEI = 0; resets the MBA/MVD predictors (p64.c:716) */
+int p64s_write_gob_header(p64s_writer *w, int gob, int gquant) {
+  int ngob;
+  if (!w) return fail(P64GPU_E_INVALID, "write_gob_header: NULL writer");
+  if (w->ended || w->gob == -2) return fail(P64GPU_E_INVALID, "GOB header outside a picture");
+  p64s_geometry(w->format, NULL, NULL, &ngob);
+  if (gob < 0 || gob >= ngob) return fail(P64GPU_E_INVALID, "gob %d of %d", gob, ngob);
+  if (gquant < 1 || gquant > 31) return fail(P64GPU_E_INVALID, "gquant %d", gquant);
+  put(w, 16, 1);
+  put(w, 4, (uint32_t)(w->format == P64S_QCIF ? 2 * gob + 1 : gob + 1));
+  put(w, 5, (uint32_t)gquant);
+  put(w, 1, 0);
+  w->gob = gob;
+  w->last_mba = -1;
+  w->last_mt = 0;
+  w->pmx = w->pmy = 0;
+  return w->oom ? fail(P64GPU_E_NOMEM, "writer: out of memory") : 0;
+}
+
+/* WriteMBHeader marker.c:288-357 + the coefficient half of WriteMDU p64.c:929-944 */
+static void write_mb(p64s_writer *w, int mdu, const p64_mb_rec *r, const int16_t *coef, int mquant) {
+  const int mt = r->mtype, mba = mdu - w->last_mba;
+  put_vlc(w, E_MBA[mba]);
+  put_vlc(w, E_MTYPE[mt]);
+  if (QUANT_MT[mt]) put(w, 5, (uint32_t)mquant);
+  if (MF_MT[mt]) {
+    int dh = r->mvx, dv = r->mvy;
+    if (MF_MT[w->last_mt] && mba == 1 && w->last_mba != -1 && w->last_mba != 10 && w->last_mba != 21) {
+      dh -= w->pmx;
+      dv -= w->pmy;
+      if (dh < -16) dh += 32;
+      if (dh > 15) dh -= 32;
+      if (dv < -16) dv += 32;
+      if (dv > 15) dv -= 32;
+    }
+    put_vlc(w, E_MVD[dh & 0x1f]);
+    put_vlc(w, E_MVD[dv & 0x1f]);
+    w->pmx = r->mvx;
+    w->pmy = r->mvy;
+  } else {
+    w->pmx = w->pmy = 0;
+  }
+  const int cbp = CBP_MT[mt] ? r->cbp : 0x3f;
+  if (CBP_MT[mt]) put_vlc(w, E_CBP[cbp]);
+  w->last_mba = mdu;
+  if (TC_MT[mt])
+    for (int c = 0; c < 6; c++)
+      if (cbp & (1 << (5 - c))) write_block(w, coef + c * 64, !CBP_MT[mt]);
+  w->last_mt = mt;
+}
+
+int p64s_write_mb(p64s_writer *w, int mdu, const p64_mb_rec *mb, const int16_t *coef, int mquant) {
+  int s;
+  if (!w || !mb || !coef) return fail(P64GPU_E_INVALID, "write_mb: NULL argument");
+  if (w->ended || w->gob < 0) return fail(P64GPU_E_INVALID, "macroblock outside a GOB");
+  if (mdu <= w->last_mba || mdu >= 33 || mdu - w->last_mba > 33)
+    return fail(P64GPU_E_INVALID, "mdu %d after %d", mdu, w->last_mba);
+  if ((s = check_mb(mb, mquant, mdu))) return s;
+  write_mb(w, mdu, mb, coef, mquant);
+  return w->oom ? fail(P64GPU_E_NOMEM, "writer: out of memory") : 0;
+}
+
 int p64s_write_picture(p64s_writer *w, int format, int tr, const uint8_t *gquant,
                        const uint8_t *quant_mb, const p64_mb_rec *mb, const int16_t *coef) {
   int ngob, s;
@@ -360,56 +454,14 @@ int p64s_write_picture(p64s_writer *w, int format, int tr, const uint8_t *gquant
   for (int g = 0; g < ngob; g++)
     if (gquant[g] < 1 || gquant[g] > 31) return fail(P64GPU_E_INVALID, "gquant[%d] = %d", g, gquant[g]);
   /* validate before writing so a failed call leaves the stream unchanged */
-  for (int k = 0; k < ngob * 33; k++) {
-    const int mt = mb[k].mtype;
-    if (mt < 0 || mt > 9) return fail(P64GPU_E_INVALID, "mb %d: mtype %d", k, mt);
-    if (CBP_MT[mt] && (mb[k].cbp < 1 || mb[k].cbp > 63))
-      return fail(P64GPU_E_INVALID, "mb %d: mtype %d with cbp %d", k, mt, mb[k].cbp);
-    if (QUANT_MT[mt] && (!quant_mb || quant_mb[k] < 1 || quant_mb[k] > 31))
-      return fail(P64GPU_E_INVALID, "mb %d: mtype %d needs MQUANT in 1..31", k, mt);
-  }
-  write_picture_header(w, format, tr);
+  for (int k = 0; k < ngob * 33; k++)
+    if ((s = check_mb(&mb[k], quant_mb ? quant_mb[k] : 0, k))) return s;
+  p64s_write_picture_header(w, format, tr);
   for (int g = 0; g < ngob; g++) {
-    /* WriteGOBHeader marker.c:171-198: GBSC, GN = GRead+1 (QCIF GRead = 2g,
-     * p64.c:703-712), GQUANT, GEI = 0 */
-    put(w, 16, 1);
-    put(w, 4, (uint32_t)(format == P64S_QCIF ? 2 * g + 1 : g + 1));
-    put(w, 5, gquant[g]);
-    put(w, 1, 0);
-    int last_mba = -1, last_mt = 0, pmx = 0, pmy = 0; /* p64.c:716 */
+    p64s_write_gob_header(w, g, gquant[g]);
     for (int m = 0; m < 33; m++) {
       const int k = raster_mb(format, g, m);
-      const p64_mb_rec *r = &mb[k];
-      const int mt = r->mtype, mba = m - last_mba;
-      /* WriteMBHeader marker.c:288-357 */
-      put_vlc(w, E_MBA[mba]);
-      put_vlc(w, E_MTYPE[mt]);
-      if (QUANT_MT[mt]) put(w, 5, quant_mb[k]);
-      if (MF_MT[mt]) {
-        int dh = r->mvx, dv = r->mvy;
-        if (MF_MT[last_mt] && mba == 1 && last_mba != -1 && last_mba != 10 && last_mba != 21) {
-          dh -= pmx;
-          dv -= pmy;
-          if (dh < -16) dh += 32;
-          if (dh > 15) dh -= 32;
-          if (dv < -16) dv += 32;
-          if (dv > 15) dv -= 32;
-        }
-        put_vlc(w, E_MVD[dh & 0x1f]);
-        put_vlc(w, E_MVD[dv & 0x1f]);
-        pmx = r->mvx;
-        pmy = r->mvy;
-      } else {
-        pmx = pmy = 0;
-      }
-      const int cbp = CBP_MT[mt] ? r->cbp : 0x3f;
-      if (CBP_MT[mt]) put_vlc(w, E_CBP[cbp]);
-      last_mba = m;
-      /* WriteMDU p64.c:929-944 */
-      if (TC_MT[mt])
-        for (int c = 0; c < 6; c++)
-          if (cbp & (1 << (5 - c))) write_block(w, coef + (size_t)k * 384 + c * 64, !CBP_MT[mt]);
-      last_mt = mt;
+      write_mb(w, m, &mb[k], coef + (size_t)k * 384, quant_mb ? quant_mb[k] : 0);
     }
   }
   return w->oom ? fail(P64GPU_E_NOMEM, "writer: out of memory") : 0;

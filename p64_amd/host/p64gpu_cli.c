@@ -2,9 +2,9 @@
  * p64gpu_cli.c -- the reference CLI's encode and decode modes over the C ABI.
  *
  * Encode (p64EncodeSequence p64.c:524 / p64EncodeFrame p64.c:622):
- *   y4m in -> p64gpu_encoder_frame (GPU: ME, decision, DCT/quant, closed-loop
- *   reconstruction kept on the device) -> p64s_write_picture (host VLC) -> .p64,
- *   byte-identical to the reference's for the same flags.
+ *   y4m in -> p64seq (GPU: ME, decision, DCT/quant, closed-loop reconstruction
+ *   kept on the device; host: VLC and rate control) -> .p64, byte-identical to
+ *   the reference's for the same flags.
  * Decode (p64DecodeSequence p64.c:1022):
  *   .p64 -> p64s_read_picture (host VLC parse) -> p64gpu_decode_recon (GPU:
  *   IQ/IDCT/prediction/filter) -> component files "<prefix><n>.Y/.U/.V"
@@ -15,13 +15,16 @@
  *   -y4m                    y4m input (encode) / output (decode)
  *   -a n  -b n  -k n        first / last frame, frame skip (TR = frame mod 32)
  *   -q n  -i n              quantiser 1..31, search limit 1..31 (BoundValue)
+ *   -r bits/s  -x bits      rate control (buffer-driven GQUANT per GOB, MTYPE 4
+ *                           on overflow) from a rate or a total file size
+ *   -f rate                 frame rate (30000/1001 default; enters -r/-x)
  *   -s file                 stream file (default <prefix>.p64)
  *   -z suffix               component file suffix (default .y4m with -y4m)
  *   -d                      decode
  *   -                       y4m from stdin
  * Additions: -full / -tss (FastBME vs the shipped StepBME), -D device.
- * Not supported here (CPU policy rows of SURVEY.md 8(f)4): -r/-x rate control,
- * -o interpreter, -p parity, -y reference DCT, raw component-file input.
+ * Not supported here: -o interpreter, -p parity (VERSION_1_0 only), -y reference
+ * DCT, raw component-file input.
  *
  * Differences from the reference: a y4m that ends before -b finishes the
  * stream (trailer written) instead of exit(ERROR_BOUNDS) with an unterminated
@@ -32,6 +35,7 @@
 #include <string.h>
 
 #include "../../include/p64gpu.h"
+#include "../../include/p64seq.h"
 #include "../../include/p64stream.h"
 
 static const char *const FMT_NAME[3] = {"QCIF", "CIF", "NTSC"};
@@ -69,21 +73,22 @@ static int drain(p64s_writer *wr, FILE *o) {
 
 typedef struct {
   int format, y4m, first, last, skip, quant, sl, mode, device, decode, from_stdin;
+  int rate, file_size_bits, frame_rate, frame_rate_div;
   const char *prefix, *suffix, *stream;
 } opts;
 
 static int encode(const opts *o) {
   char path[4096];
   FILE *f;
-  if (o->from_stdin) {
-    f = stdin;
-  } else {
-    snprintf(path, sizeof path, "%s%s", o->prefix, o->suffix ? o->suffix : (o->y4m ? ".y4m" : ""));
-    f = fopen(path, "rb");
-  }
   if (!o->y4m) {
     fprintf(stderr, "p64gpu: only -y4m input is supported\n");
     return 1;
+  }
+  if (o->from_stdin) {
+    f = stdin;
+  } else {
+    snprintf(path, sizeof path, "%s%s", o->prefix, o->suffix ? o->suffix : ".y4m");
+    f = fopen(path, "rb");
   }
   int w, h, s;
   if (!f || read_y4m_header(f, &w, &h)) {
@@ -92,18 +97,12 @@ static int encode(const opts *o) {
   }
   const int fmt = p64s_format_of(w, h);
   if (fmt < 0 || (o->format >= 0 && fmt != o->format)) {
-    fprintf(stderr, "p64gpu: y4m is %dx%d, not %s\n", w, h, o->format >= 0 ? FMT_NAME[o->format] : "QCIF/CIF/NTSC");
+    fprintf(stderr, "p64gpu: y4m is %dx%d, not %s\n", w, h,
+            o->format >= 0 ? FMT_NAME[o->format] : "QCIF/CIF/NTSC");
     return 1;
   }
-  int ngob;
-  p64s_geometry(fmt, NULL, NULL, &ngob);
   const size_t pic = (size_t)w * h * 3 / 2;
-  const int nmb = ngob * 33;
   unsigned char *buf = malloc(pic);
-  int16_t *coef = malloc((size_t)nmb * 384 * sizeof(int16_t));
-  p64_mb_rec *mb = malloc((size_t)nmb * sizeof(p64_mb_rec));
-  uint8_t gq[12];
-  for (int g = 0; g < ngob; g++) gq[g] = (uint8_t)o->quant;
   /* seek to StartFrame (p64.c:562-565) */
   for (int i = 0; i < o->first; i++)
     if (read_frame(f, buf, pic) != 1) {
@@ -118,49 +117,56 @@ static int encode(const opts *o) {
     fprintf(stderr, "p64gpu: cannot open %s\n", spath);
     return 1;
   }
-  p64gpu_encoder *enc = NULL;
-  p64s_writer *wr = NULL;
-  if ((s = p64gpu_encoder_open(o->device, w, h, o->mode, o->sl, &enc))) return die("encoder_open", s);
-  if ((s = p64s_writer_open(&wr))) return die("writer_open", s);
-  int hist[10] = {0}, coded = 0, cur = o->first;
-  int64_t bits0 = 0;
+  p64seq_config cfg;
+  p64seq_default_config(&cfg);
+  cfg.format = fmt;
+  cfg.me_mode = o->mode;
+  cfg.search_limit = o->sl;
+  cfg.quant = o->quant;
+  cfg.rate = o->rate;
+  cfg.file_size_bits = o->file_size_bits;
+  cfg.start_frame = o->first;
+  cfg.last_frame = o->last < o->first ? o->first : o->last;
+  cfg.frame_skip = o->skip;
+  cfg.frame_rate = o->frame_rate;
+  cfg.frame_rate_div = o->frame_rate_div;
+  cfg.device = o->device;
+  p64seq *sq = NULL;
+  if ((s = p64seq_open(&cfg, &sq))) return die("p64seq_open", s);
+  p64seq_stats st;
+  p64seq_get_stats(sq, &st);
+  if (st.rate) printf("Rate: %d   QDFact: %d  QOffs: %d\nStarting Quantization: %d\n", st.rate, st.rate / 320, 1, st.gquant);
   printf("START>SEQUENCE\n");
-  for (; cur <= o->last; cur += o->skip) {
+  while (p64seq_more(sq)) {
+    p64seq_get_stats(sq, &st);
     const int r = read_frame(f, buf, pic);
     if (r <= 0) {
-      if (r < 0) fprintf(stderr, "p64gpu: bad y4m frame at %d\n", cur);
+      if (r < 0) fprintf(stderr, "p64gpu: bad y4m frame at %d\n", st.next_frame);
       break;
     }
-    if ((s = p64gpu_encoder_frame(enc, buf, cur == o->first, o->quant, NULL, coef, mb, NULL, NULL)))
-      return die("encode", s);
-    if ((s = p64s_write_picture(wr, fmt, cur % 32, gq, NULL, mb, coef))) return die("write", s);
-    int64_t bits;
-    p64s_writer_data(wr, NULL, &bits);
-    for (int k = 0; k < nmb; k++) hist[mb[k].mtype]++;
-    printf("END>Frame: %d  bits %lld\n", cur, (long long)(bits - bits0));
-    bits0 = bits;
-    if (drain(wr, out)) {
+    if ((s = p64seq_encode(sq, buf))) return die("encode", s);
+    p64seq_get_stats(sq, &st);
+    printf("END>Frame: %d  bits %lld  GQuant %d\n", st.next_frame - o->skip, (long long)st.last_bits, st.gquant);
+    if (drain(p64seq_writer(sq), out)) {
       fprintf(stderr, "p64gpu: write error on %s\n", spath);
       return 1;
     }
-    coded++;
   }
-  /* trailer: p64.c:606-610 */
-  if (cur > o->last + 1) cur = o->last + 1;
-  if ((s = p64s_write_end(wr, fmt, cur % 32))) return die("write_end", s);
-  if (drain(wr, out) || fclose(out)) {
+  if ((s = p64seq_finish(sq))) return die("finish", s);
+  if (drain(p64seq_writer(sq), out) || fclose(out)) {
     fprintf(stderr, "p64gpu: write error on %s\n", spath);
     return 1;
   }
-  printf("END>SEQUENCE\nframes %d  MTYPE histogram:", coded);
-  for (int k = 0; k < 10; k++) printf(" %d", hist[k]);
+  p64seq_get_stats(sq, &st);
+  printf("END>SEQUENCE\n");
+  printf("Bits for first frame: %lld   Number of buffer overflows: %d\n", (long long)st.first_frame_bits,
+         st.overflows);
+  printf("frames %d  MTYPE histogram:", st.frames);
+  for (int k = 0; k < 10; k++) printf(" %d", st.mtype_hist[k]);
   printf("\n");
-  p64s_writer_close(wr);
-  p64gpu_encoder_close(enc);
+  p64seq_close(sq);
   if (f != stdin) fclose(f);
   free(buf);
-  free(coef);
-  free(mb);
   return 0;
 }
 
@@ -270,8 +276,8 @@ static int decode(const opts *o) {
 }
 
 int main(int argc, char **argv) {
-  opts o = {.format = -1, .first = 0, .last = 0, .skip = 1, .quant = 8, .sl = 15,
-            .mode = P64GPU_ME_TSS};
+  opts o = {.format = -1, .first = 0, .last = 0, .skip = 1, .quant = 0, .sl = 15,
+            .mode = P64GPU_ME_TSS, .frame_rate = 30000, .frame_rate_div = 1001};
   for (int i = 1; i < argc; i++) {
     const char *a = argv[i];
     const int more = i + 1 < argc;
@@ -285,11 +291,31 @@ int main(int argc, char **argv) {
     else if (!strcmp(a, "-a") && more) o.first = atoi(argv[++i]);
     else if (!strcmp(a, "-b") && more) o.last = atoi(argv[++i]);
     else if (!strcmp(a, "-k") && more) o.skip = atoi(argv[++i]);
-    else if (!strcmp(a, "-q") && more) o.quant = atoi(argv[++i]);
+    else if (!strcmp(a, "-q") && more) {
+      o.quant = atoi(argv[++i]); /* BoundValue(InitialQuant, 1, 31) p64.c:357-358 */
+      if (o.quant < 1) o.quant = 1;
+      if (o.quant > 31) o.quant = 31;
+    }
     else if (!strcmp(a, "-i") && more) o.sl = atoi(argv[++i]);
     else if (!strcmp(a, "-s") && more) o.stream = argv[++i];
     else if (!strcmp(a, "-z") && more) o.suffix = argv[++i];
     else if (!strcmp(a, "-d")) o.decode = 1;
+    else if (!strcmp(a, "-r") && more) o.rate = atoi(argv[++i]);
+    else if (!strcmp(a, "-x") && more) o.file_size_bits = atoi(argv[++i]);
+    else if (!strcmp(a, "-f") && more) {
+      /* -f rate[.frac | /div | :div] (p64.c:314-339) */
+      const char *v = argv[++i];
+      const size_t numlen = strcspn(v, "./:");
+      o.frame_rate = atoi(v);
+      o.frame_rate_div = 1;
+      if (v[numlen] == '.') {
+        for (size_t k = strlen(v + numlen + 1); k > 0; --k) o.frame_rate_div *= 10;
+        o.frame_rate = o.frame_rate * o.frame_rate_div + atoi(v + numlen + 1);
+      } else if (v[numlen]) {
+        o.frame_rate_div = atoi(v + numlen + 1);
+        if (o.frame_rate_div < 1) o.frame_rate_div = 1;
+      }
+    }
     else if (!strcmp(a, "-")) {
       o.from_stdin = 1;
       o.prefix = "stdin";
@@ -307,9 +333,7 @@ int main(int argc, char **argv) {
             "       p64gpu -d [-y4m] -s in.p64 [-z suffix] prefix\n");
     return 1;
   }
-  /* BoundValue (p64.c:341-352) */
-  if (o.quant < 1) o.quant = 1;
-  if (o.quant > 31) o.quant = 31;
+  /* BoundValue (p64.c:341-352); -q absent leaves 0 (default / rate-derived) */
   if (o.sl < 1) o.sl = 1;
   if (o.sl > 31) o.sl = 31;
   if (o.skip < 1) o.skip = 1;

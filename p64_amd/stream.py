@@ -177,25 +177,101 @@ def _cmod(a: int, m: int) -> int:
 # ---------------------------------------------------------------------------
 # whole-sequence helpers: GPU hot path + host bitstream (the CLI's two modes)
 
-def encode_sequence(frames, width: int, height: int, *, quant: int = 8, me_mode: int = 0,
-                    search_limit: int = 15, first: int = 0, skip: int = 1,
-                    device: int = 0) -> bytes:
-    """p64EncodeSequence (p64.c:524): frames[i] is coded as frame first+i*skip
-    (TR mod 32), the first intra, then closed-loop inter on the GPU."""
-    from . import Encoder
-    fmt = format_of(width, height)
-    enc = Encoder(width, height, me_mode=me_mode, search_limit=search_limit, device=device)
-    w = Writer(fmt)
-    cur = first
+class SeqConfig(ctypes.Structure):
+    """p64seq_config (include/p64seq.h)."""
+    _fields_ = [(n, ctypes.c_int) for n in
+                ("format", "me_mode", "search_limit", "quant", "rate", "file_size_bits",
+                 "start_frame", "last_frame", "frame_skip", "frame_rate", "frame_rate_div",
+                 "device")]
+
+
+class SeqStats(ctypes.Structure):
+    _fields_ = [("frames", ctypes.c_int), ("next_frame", ctypes.c_int), ("gquant", ctypes.c_int),
+                ("rate", ctypes.c_int), ("bits", ctypes.c_int64), ("last_bits", ctypes.c_int64),
+                ("first_frame_bits", ctypes.c_int64), ("overflows", ctypes.c_int),
+                ("mtype_hist", ctypes.c_int * 10)]
+
+
+class SequenceEncoder:
+    """p64EncodeSequence (p64.c:524) over include/p64seq.h: GPU per-macroblock
+    compute, host VLC and the reference's rate control (-r / -x)."""
+
+    def __init__(self, width: int, height: int, *, quant: int = 0, me_mode: int = 0,
+                 search_limit: int = 15, first: int = 0, last: int | None = None, skip: int = 1,
+                 rate: int = 0, file_size_bits: int = 0, frame_rate: int = 30000,
+                 frame_rate_div: int = 1001, device: int = 0, nframes: int | None = None):
+        L = lib()
+        c = SeqConfig()
+        L.p64seq_default_config(ctypes.byref(c))
+        c.format = format_of(width, height)
+        c.me_mode, c.search_limit, c.quant = me_mode, search_limit, quant
+        c.rate, c.file_size_bits = rate, file_size_bits
+        c.start_frame = first
+        c.last_frame = last if last is not None else first + skip * ((nframes or 1) - 1)
+        c.frame_skip, c.frame_rate, c.frame_rate_div, c.device = skip, frame_rate, frame_rate_div, device
+        self.width, self.height = width, height
+        self._h = ctypes.c_void_p()
+        _check(L.p64seq_open(ctypes.byref(c), ctypes.byref(self._h)))
+        self._chunks = []
+
+    def more(self) -> bool:
+        return bool(lib().p64seq_more(self._h))
+
+    def encode(self, picture) -> None:
+        pic = np.ascontiguousarray(picture, dtype=np.uint8)
+        if pic.size != self.width * self.height * 3 // 2:
+            raise P64GpuError("picture has the wrong size")
+        _check(lib().p64seq_encode(self._h, pic.ctypes.data))
+        self._drain()
+
+    def finish(self) -> bytes:
+        _check(lib().p64seq_finish(self._h))
+        self._drain()
+        return b"".join(self._chunks)
+
+    def stats(self) -> SeqStats:
+        st = SeqStats()
+        _check(lib().p64seq_get_stats(self._h, ctypes.byref(st)))
+        return st
+
+    def _drain(self):
+        L = lib()
+        w = L.p64seq_writer(self._h)
+        n = ctypes.c_size_t()
+        p = L.p64s_writer_data(w, ctypes.byref(n), None)
+        if n.value:
+            self._chunks.append(ctypes.string_at(p, n.value))
+            _check(L.p64s_writer_consume(w, n.value))
+
+    def close(self):
+        if self._h:
+            lib().p64seq_close(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def encode_sequence(frames, width: int, height: int, *, quant: int = 0, me_mode: int = 0,
+                    search_limit: int = 15, first: int = 0, skip: int = 1, rate: int = 0,
+                    file_size_bits: int = 0, device: int = 0) -> bytes:
+    """Encode frames[i] as frame first+i*skip: the reference CLI's `-a first
+    -b last -k skip [-q] [-r|-x]` over the same pictures."""
+    frames = list(frames)
+    enc = SequenceEncoder(width, height, quant=quant, me_mode=me_mode, search_limit=search_limit,
+                          first=first, skip=skip, rate=rate, file_size_bits=file_size_bits,
+                          device=device, nframes=len(frames))
     try:
-        for i, f in enumerate(frames):
-            coef, mb, _, _ = enc.frame(f, intra=(i == 0), quant=quant)
-            w.write_picture(cur % 32, mb, coef, quant)
-            cur += skip
-        return w.end(cur % 32)  # trailer, p64.c:606-610
+        for f in frames:
+            if not enc.more():
+                break
+            enc.encode(f)
+        return enc.finish()
     finally:
         enc.close()
-        w.close()
 
 
 def decode_sequence(data: bytes, start_frame: int = 0) -> list[np.ndarray]:

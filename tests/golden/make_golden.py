@@ -242,7 +242,11 @@ def raster_index(fmt, g, m):
     return mby * 22 + mbx
 
 
-def run_sequence(name, fmt, nframes, seed, *, me="tss", sl=15, q=8, oracle_prog=None):
+def run_sequence(name, fmt, nframes, seed, *, me="tss", sl=15, q=8, oracle_prog=None, rate=0,
+                 filesize=0):
+    """q=0 leaves -q off (rate control then derives InitialQuant, p64.c:579-586)."""
+    if ONLY and name not in ONLY:
+        return None
     w, h = FMT[fmt]
     frames = [p64_amd.synth_frame(seed, t, w, h) for t in range(nframes)]
     nmb = (w // 16) * (h // 16)
@@ -252,7 +256,13 @@ def run_sequence(name, fmt, nframes, seed, *, me="tss", sl=15, q=8, oracle_prog=
         if me == "full":
             env["P64REF_ME"] = "full"
         cmd = [os.path.join(REF_OUT, "p64hook"), "-" + fmt, "-y4m", "-a", "0", "-b",
-               str(nframes - 1), "-q", str(q), "-i", str(sl)]
+               str(nframes - 1), "-i", str(sl)]
+        if q:
+            cmd += ["-q", str(q)]
+        if rate:
+            cmd += ["-r", str(rate)]
+        if filesize:
+            cmd += ["-x", str(filesize)]
         if oracle_prog:
             cmd.append("-o")
         cmd += [os.path.join(td, "in"), "-z", ".y4m", "-s", os.path.join(td, "out.p64")]
@@ -290,7 +300,7 @@ def run_sequence(name, fmt, nframes, seed, *, me="tss", sl=15, q=8, oracle_prog=
         extra = dict(frames=np.array(frames), recon=rec)
     np.savez_compressed(os.path.join(HERE, f"seq_{name}.npz"), fmt=fmt, width=w, height=h,
                         seed=seed, nframes=nframes, me=me, sl=sl, q=q,
-                        oracle=oracle_prog or "", mb=mbrec, usequant=usequant, coef=coef,
+                        oracle=oracle_prog or "", rate=rate, filesize=filesize, mb=mbrec, usequant=usequant, coef=coef,
                         merec=merecs, frames_sha256=np.array([sha(f) for f in frames]),
                         recon_sha256=np.array([sha(r) for r in rec]),
                         stream_sha256=hashlib.sha256(stream).hexdigest(), stream_len=len(stream),
@@ -311,13 +321,18 @@ def decode_md5():
         json.dump(out, f, indent=1, sort_keys=True)
 
 
+ONLY = set()
+
+
 def main():
+    ONLY.update(sys.argv[1:])
     if not os.path.exists(os.path.join(REF_OUT, "p64hook")):
         subprocess.run(["make", "-C", os.path.join(REPO, "oracle"), "ref"], check=True)
     rng = np.random.default_rng(20261015)
     L = reflib()
-    make_blocks(L, rng)
-    make_me(L, rng)
+    if not ONLY:
+        make_blocks(L, rng)
+        make_me(L, rng)
     run_sequence("qcif_tss", "QCIF", 8, 3)
     run_sequence("qcif_full31", "QCIF", 6, 4, me="full", sl=31)
     run_sequence("qcif_full15", "QCIF", 4, 13, me="full", sl=15)
@@ -333,7 +348,14 @@ def main():
     run_sequence("cif_tss", "CIF", 3, 2)
     run_sequence("ntsc_tss", "NTSC", 3, 9)
     run_sequence("cif_scene_full31", "CIF", 14, 5, me="full", sl=31, q=12)
-    decode_md5()
+    # rate control (-r / -x, p64.c:458-481, 569-587, 697-786): per-GOB GQUANT
+    # from the bits written, buffer-overflow MTYPE 4 (also in the intra picture)
+    run_sequence("qcif_rate", "QCIF", 8, 3, q=0, rate=30000)
+    run_sequence("qcif_rate_q6", "QCIF", 6, 11, q=6, rate=120000)
+    run_sequence("cif_rate_full31", "CIF", 5, 2, me="full", sl=31, q=12, rate=300000)
+    run_sequence("qcif_filesize", "QCIF", 6, 13, q=0, filesize=60000)
+    if not ONLY:
+        decode_md5()
 
 
 if __name__ == "__main__":

@@ -11,14 +11,14 @@ import pytest
 
 from conftest import REPO
 
-HEADERS = [os.path.join(REPO, "include", h) for h in ("p64gpu.h", "p64stream.h")]
+HEADERS = [os.path.join(REPO, "include", h) for h in ("p64gpu.h", "p64stream.h", "p64seq.h")]
 
 
 def declared_functions():
     names = set()
     for hdr in HEADERS:
         text = re.sub(r"/\*.*?\*/", "", open(hdr).read(), flags=re.S)
-        names |= set(re.findall(r"\b(p64(?:gpu|s)?_\w+)\s*\(", text))
+        names |= set(re.findall(r"\b(p64(?:gpu|seq|s)?_\w+)\s*\(", text))
     return sorted(names)
 
 
@@ -28,7 +28,8 @@ def test_header_declares_expected_entry_points():
               "p64gpu_decode_recon", "p64gpu_encoder_open", "p64gpu_encoder_frame",
               "p64gpu_encoder_close", "p64gpu_synth_frames", "p64_synth_frame",
               "p64gpu_copy_on_device", "p64s_write_picture", "p64s_write_end",
-              "p64s_read_picture", "p64s_reader_open"):
+              "p64s_read_picture", "p64s_reader_open", "p64gpu_encode_mb_list",
+              "p64s_write_mb", "p64seq_open", "p64seq_encode", "p64seq_finish"):
         assert n in names
 
 

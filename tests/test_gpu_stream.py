@@ -10,7 +10,7 @@ import numpy as np
 import pytest
 
 from conftest import GOLDEN, REPO
-from test_oracle_golden import SEQS, load, sequence_frames
+from test_oracle_golden import RATE_SEQS, SEQS, load, sequence_frames
 
 pytestmark = pytest.mark.gpu
 
@@ -25,30 +25,45 @@ def write_y4m(path, frames, w, h):
             f.write(b"FRAME\n" + fr.tobytes())
 
 
-@pytest.mark.parametrize("name", PLAIN)
-def test_cli_encode_byte_identical(p64, torch_dev, tmp_path, name):
-    """`p64gpu -FMT -y4m -a 0 -b N-1 -q Q -i SL [-full]` == the reference CLI's .p64."""
-    z = load(f"seq_{name}.npz")
-    w, h, n = int(z["width"]), int(z["height"]), int(z["nframes"])
-    write_y4m(tmp_path / "in.y4m", sequence_frames(p64, z), w, h)
-    cmd = [CLI, "-" + str(z["fmt"]), "-y4m", "-a", "0", "-b", str(n - 1), "-q", str(int(z["q"])),
-           "-i", str(int(z["sl"])), str(tmp_path / "in"), "-z", ".y4m", "-s", str(tmp_path / "o.p64")]
+def cli_flags(z):
+    """The reference CLI flags the fixture was made with (make_golden.run_sequence)."""
+    n = int(z["nframes"])
+    f = ["-" + str(z["fmt"]), "-y4m", "-a", "0", "-b", str(n - 1), "-i", str(int(z["sl"]))]
+    if int(z["q"]):
+        f += ["-q", str(int(z["q"]))]
+    for key, flag in (("rate", "-r"), ("filesize", "-x")):
+        if key in z.files and int(z[key]):
+            f += [flag, str(int(z[key]))]
     if str(z["me"]) == "full":
-        cmd.append("-full")
+        f.append("-full")
+    return f
+
+
+@pytest.mark.parametrize("name", PLAIN + RATE_SEQS)
+def test_cli_encode_byte_identical(p64, torch_dev, tmp_path, name):
+    """`p64gpu -FMT -y4m -a 0 -b N-1 [-q Q] -i SL [-r R | -x X] [-full]` == the
+    reference CLI's .p64 (rate control included: per-GOB GQUANT, MTYPE 4 on
+    buffer overflow)."""
+    z = load(f"seq_{name}.npz")
+    w, h = int(z["width"]), int(z["height"])
+    write_y4m(tmp_path / "in.y4m", sequence_frames(p64, z), w, h)
+    cmd = [CLI] + cli_flags(z) + [str(tmp_path / "in"), "-z", ".y4m", "-s", str(tmp_path / "o.p64")]
     subprocess.run(cmd, check=True, stdout=subprocess.DEVNULL, timeout=300)
     data = (tmp_path / "o.p64").read_bytes()
     assert len(data) == int(z["stream_len"])
     assert hashlib.sha256(data).hexdigest() == str(z["stream_sha256"])
 
 
-@pytest.mark.parametrize("name", ["qcif_tss", "cif_full31", "ntsc_tss"])
+@pytest.mark.parametrize("name", ["qcif_tss", "cif_full31", "ntsc_tss", "qcif_rate",
+                                  "cif_rate_full31", "qcif_filesize"])
 def test_python_encode_sequence_byte_identical(p64, torch_dev, name):
     from p64_amd import stream
     z = load(f"seq_{name}.npz")
     w, h = int(z["width"]), int(z["height"])
-    data = stream.encode_sequence(sequence_frames(p64, z), w, h, quant=int(z["q"]),
+    g = lambda k: int(z[k]) if k in z.files else 0  # noqa: E731
+    data = stream.encode_sequence(sequence_frames(p64, z), w, h, quant=g("q"),
                                   me_mode=1 if str(z["me"]) == "full" else 0,
-                                  search_limit=int(z["sl"]))
+                                  search_limit=g("sl"), rate=g("rate"), file_size_bits=g("filesize"))
     assert hashlib.sha256(data).hexdigest() == str(z["stream_sha256"])
 
 
@@ -72,17 +87,16 @@ def test_python_decode_short_p64_md5(p64, torch_dev):
             assert hashlib.md5(a.tobytes()).hexdigest() == exp[f"short{i}.{c}"]
 
 
-@pytest.mark.parametrize("name", ["qcif_tss", "qcif_full31", "qcif_q31", "qcif_flat_tss"])
+@pytest.mark.parametrize("name", ["qcif_tss", "qcif_full31", "qcif_q31", "qcif_flat_tss",
+                                  "qcif_rate", "qcif_filesize"])
 def test_decode_of_encoded_stream_is_encoder_recon(p64, torch_dev, tmp_path, name):
     """encode -> .p64 -> decode (y4m) reproduces the encoder's closed-loop
-    reconstruction, which the fixtures hold from the reference encoder."""
+    reconstruction, which the fixtures hold from the reference encoder
+    (including MBs forced to MTYPE 4 by a buffer overflow)."""
     z = load(f"seq_{name}.npz")
     w, h, n = int(z["width"]), int(z["height"]), int(z["nframes"])
     write_y4m(tmp_path / "in.y4m", sequence_frames(p64, z), w, h)
-    enc = [CLI, "-QCIF", "-y4m", "-a", "0", "-b", str(n - 1), "-q", str(int(z["q"])), "-i",
-           str(int(z["sl"])), str(tmp_path / "in"), "-z", ".y4m", "-s", str(tmp_path / "o.p64")]
-    if str(z["me"]) == "full":
-        enc.append("-full")
+    enc = [CLI] + cli_flags(z) + [str(tmp_path / "in"), "-z", ".y4m", "-s", str(tmp_path / "o.p64")]
     subprocess.run(enc, check=True, stdout=subprocess.DEVNULL, timeout=300)
     subprocess.run([CLI, "-d", "-y4m", "-s", str(tmp_path / "o.p64"), str(tmp_path / "dec")],
                    check=True, stdout=subprocess.DEVNULL, timeout=300)
@@ -90,8 +104,8 @@ def test_decode_of_encoded_stream_is_encoder_recon(p64, torch_dev, tmp_path, nam
     hdr, body = raw.split(b"\n", 1)
     assert hdr.startswith(b"YUV4MPEG2 W176 H144")
     pic = w * h * 3 // 2
-    chunks = body.split(b"FRAME\n")[1:]
-    assert len(chunks) == n
-    for t, c in enumerate(chunks):
-        assert len(c) == pic
-        np.testing.assert_array_equal(np.frombuffer(c, np.uint8), z["recon"][t], err_msg=f"t{t}")
+    assert len(body) == n * (6 + pic)
+    for t in range(n):
+        c = body[t * (6 + pic):(t + 1) * (6 + pic)]
+        assert c[:6] == b"FRAME\n"
+        np.testing.assert_array_equal(np.frombuffer(c[6:], np.uint8), z["recon"][t], err_msg=f"t{t}")

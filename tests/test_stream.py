@@ -18,7 +18,7 @@ import numpy as np
 import pytest
 
 from conftest import GOLDEN
-from test_oracle_golden import SEQS, load
+from test_oracle_golden import ALL_SEQS, load
 
 FMTS = {"QCIF": 0, "CIF": 1, "NTSC": 2}
 
@@ -47,7 +47,7 @@ def write_fixture_stream(st, z):
     return w.end(n % 32)
 
 
-@pytest.mark.parametrize("name", SEQS)
+@pytest.mark.parametrize("name", ALL_SEQS)
 def test_writer_byte_identical_to_reference(st, name):
     z = load(f"seq_{name}.npz")
     data = write_fixture_stream(st, z)
