@@ -14,9 +14,14 @@
  *       (p64gpu_encode_frames / p64gpu_encode_mb_list, one launch per picture,
  *       or per GOB under rate control), the VLC on the host (p64stream.h).
  *
- * Not covered here: the -o interpreter (program-driven MTYPE/quant) and the
- * MQUANT path it enables (OracleMQuantEnable is otherwise never set, so the
- * reference never sends MQUANT without -o).
+ *   With a -o program (p64prog.h): program 0 picks each macroblock's MTYPE
+ *   from the ME statistics (p64.c:761-768) and program 1 the quantiser under
+ *   rate control (p64.c:469-474), called in the reference's order.  When
+ *   program 0 cannot see the bits written (no BUFFERCONTENTS read, no rate
+ *   control) the decisions are made for the whole picture first and the GPU
+ *   codes it in one launch; otherwise macroblock by macroblock.  MTYPEs
+ *   1/3/6/9 chosen by a program send MQUANT (= the initial quantiser: the
+ *   reference never changes MQuant) and make it the GOB quantiser.
  */
 #ifndef P64SEQ_H
 #define P64SEQ_H
@@ -45,6 +50,9 @@ typedef struct {
   int frame_rate;        /* -f numerator   (30000 = reference default)         */
   int frame_rate_div;    /* -f denominator (1001)                              */
   int device;            /* HIP device                                         */
+  void *program;         /* p64prog* (-o, p64prog.h) or NULL; borrowed, must
+                            outlive the encoder; its top-level settings are the
+                            caller's to apply to this config                  */
 } p64seq_config;
 
 typedef struct {

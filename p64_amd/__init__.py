@@ -150,6 +150,16 @@ def lib() -> ctypes.CDLL:
     L.p64seq_writer.restype = vp
     L.p64seq_get_stats.argtypes = [vp, vp]
     L.p64gpu_encode_mb_list.argtypes = [ctypes.POINTER(EncodeArgs), vp, i32, vp]
+    # -o program interpreter (include/p64prog.h), host C
+    L.p64prog_load.argtypes = [ctypes.c_char_p, ctypes.c_size_t, vp, ctypes.POINTER(vp)]
+    L.p64prog_free.argtypes = [vp]
+    L.p64prog_free.restype = None
+    L.p64prog_settings_get.argtypes = [vp, vp]
+    L.p64prog_defined.argtypes = [vp, i32]
+    L.p64prog_reads.argtypes = [vp, i32, i32]
+    L.p64prog_execute.argtypes = [vp, i32]
+    L.p64prog_memory.argtypes = [vp]
+    L.p64prog_memory.restype = ctypes.POINTER(ctypes.c_double)
     if L.p64gpu_abi_version() != 1:
         raise P64GpuError("libp64gpu.so ABI version mismatch")
     _lib = L

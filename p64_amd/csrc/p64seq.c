@@ -7,10 +7,12 @@
  * bit budget and the quantiser choices match for every -r / -x / -k / -f.
  */
 #include <stdarg.h>
+#include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
+#include "../../include/p64prog.h"
 #include "../../include/p64seq.h"
 
 int p64gpu_fail_(int status, const char *msg); /* p64gpu.hip: sets last error */
@@ -43,10 +45,14 @@ struct p64seq {
   int16_t *h_coef;
   p64_mb_rec *h_mb;
   uint8_t *h_li_old, *h_li, *h_mask, *h_q;
+  int8_t *h_ov, *d_ov;
+  p64_me_rec *h_me, *d_me;
   int32_t *h_lists;
   p64s_writer *wr;
+  p64prog *prog; /* -o program, or NULL */
   /* reference state (p64.c globals) */
-  int current_frame, rate, qdfact, qoffs, gquant, buffer_offset, novfl, frames, finished;
+  int current_frame, rate, qdfact, qoffs, gquant, mquant, mtype, buffer_offset, novfl, pic_ovfl;
+  int frames, finished;
   int64_t total_bits, last_bits, first_frame_bits;
   int hist[10];
 };
@@ -70,6 +76,10 @@ void p64seq_close(p64seq *s) {
   p64gpu_free(s->d_coef);
   p64gpu_free(s->d_mb);
   p64gpu_free(s->d_lists);
+  p64gpu_free(s->d_ov);
+  p64gpu_free(s->d_me);
+  free(s->h_ov);
+  free(s->h_me);
   free(s->h_coef);
   free(s->h_mb);
   free(s->h_li_old);
@@ -107,7 +117,9 @@ int p64seq_open(const p64seq_config *cfg, p64seq **out) {
       (st = p64gpu_alloc((void **)&s->d_q, nmb)) || (st = p64gpu_alloc((void **)&s->d_mask, nmb)) ||
       (st = p64gpu_alloc((void **)&s->d_coef, nmb * 384 * sizeof(int16_t))) ||
       (st = p64gpu_alloc((void **)&s->d_mb, nmb * sizeof(p64_mb_rec))) ||
-      (st = p64gpu_alloc((void **)&s->d_lists, nmb * sizeof(int32_t))))
+      (st = p64gpu_alloc((void **)&s->d_lists, nmb * sizeof(int32_t))) ||
+      (st = p64gpu_alloc((void **)&s->d_ov, nmb)) ||
+      (st = p64gpu_alloc((void **)&s->d_me, nmb * sizeof(p64_me_rec))))
     goto bad;
   s->h_coef = (int16_t *)calloc(nmb * 384, sizeof(int16_t));
   s->h_mb = (p64_mb_rec *)calloc(nmb, sizeof(p64_mb_rec));
@@ -116,8 +128,11 @@ int p64seq_open(const p64seq_config *cfg, p64seq **out) {
   s->h_mask = (uint8_t *)calloc(nmb, 1);
   s->h_q = (uint8_t *)calloc(nmb, 1);
   s->h_lists = (int32_t *)calloc(nmb, sizeof(int32_t));
+  s->h_ov = (int8_t *)calloc(nmb, 1);
+  s->h_me = (p64_me_rec *)calloc(nmb, sizeof(p64_me_rec));
   uint8_t *zero = (uint8_t *)calloc(s->pic, 1);
-  if (!s->h_coef || !s->h_mb || !s->h_li_old || !s->h_li || !s->h_mask || !s->h_q || !s->h_lists || !zero) {
+  if (!s->h_coef || !s->h_mb || !s->h_li_old || !s->h_li || !s->h_mask || !s->h_q || !s->h_lists ||
+      !s->h_ov || !s->h_me || !zero) {
     free(zero);
     st = fail(P64GPU_E_NOMEM, "p64seq: host buffers");
     goto bad;
@@ -158,7 +173,9 @@ int p64seq_open(const p64seq_config *cfg, p64seq **out) {
   }
   if (!iq) iq = 8; /* DEFAULT_QUANTIZATION p64.c:145 */
   s->rate = rate;
-  s->gquant = iq;
+  if (!rate) s->qdfact = s->qoffs = 1; /* p64.c:137-138 */
+  s->gquant = s->mquant = iq;        /* GQuant = MQuant = InitialQuant p64.c:589 */
+  s->prog = (p64prog *)c->program;
   s->cur = 0;
   *out = s;
   return 0;
@@ -184,13 +201,66 @@ static int64_t buffer_contents(const p64seq *s, int g, int m) {
   return bits_written(s) + s->buffer_offset - budget;
 }
 
-/* ExecuteQuantization p64.c:458-481 without -o */
-static int rate_gquant(const p64seq *s, int g) {
-  const int cs = (int)buffer_contents(s, g, 0);
-  int q = cs / s->qdfact + s->qoffs;
-  if (q < 1) q = 1;
-  if (q > 31) q = 31;
-  return q;
+/* (int) of a double as the reference's casts do on x86 (out of range -> INT_MIN) */
+static int dtoi(double v) { return (v > -2147483649.0 && v < 2147483648.0) ? (int)v : INT32_MIN; }
+static int clampq(int q) { return q < 1 ? 1 : q > 31 ? 31 : q; }
+
+/* CallOracle p64.c:489-515: the encoder state into Memory[1..14], then run
+ * program v.  k = the macroblock at (CurrentGOB, CurrentMDU). */
+static int call_program(p64seq *s, int v, int mtype, int k, int64_t bc) {
+  double *m = p64prog_memory(s->prog);
+  const p64_me_rec *e = &s->h_me[k];
+  m[P64PROG_GQUANT] = s->gquant;
+  m[P64PROG_MQUANT] = s->mquant;
+  m[P64PROG_MQUANTENABLE] = 0; /* MQuantEnable: never set (OracleMQuantEnable is 0) */
+  m[P64PROG_MTYPE] = mtype;
+  m[P64PROG_BD] = e->sad0;
+  m[P64PROG_DBD] = e->sad;
+  m[P64PROG_VAROR] = e->varor;
+  m[P64PROG_VAR] = e->var;
+  m[P64PROG_MWOR] = e->mwor;
+  m[P64PROG_RATE] = s->rate;
+  m[P64PROG_BUFFERSIZE] = s->rate / 4;
+  m[P64PROG_BUFFERCONTENTS] = (double)(int)bc;
+  m[P64PROG_QDFACT] = s->qdfact;
+  m[P64PROG_QOFFS] = s->qoffs;
+  return p64prog_execute(s->prog, v);
+}
+
+/* ExecuteQuantization p64.c:458-481 at GOB g, MDU m: the new GQUANT (the
+ * MQUANT half has no effect: OracleMQuantEnable is never set) */
+static int execute_quantization(p64seq *s, int g, int m, int *gq) {
+  const int64_t bc = buffer_contents(s, g, m);
+  int q = (int)bc / s->qdfact + s->qoffs;
+  if (s->prog) {
+    const int st = call_program(s, 1, s->mtype, s->h_lists[g * 33 + m], bc);
+    if (st) return st;
+    q = dtoi(p64prog_memory(s->prog)[P64PROG_GQUANT]);
+  }
+  *gq = clampq(q);
+  return 0;
+}
+
+/* the MTYPE decision of p64EncodeGOB p64.c:734-756 (suggested type for -o) */
+static int decide(const p64_me_rec *e) {
+  const double x = (double)e->sad0 / 256, y = (double)e->sad / 256;
+  if (e->var < 64 || e->varor > e->var) {
+    if (x < 1.0 || (x < 3.0 && y > x * 0.5) || y > x / 1.1) return 2;
+    return e->var < 6.0 ? 5 : 8;
+  }
+  return 0;
+}
+
+static const unsigned char QUANT_MT[10] = {0, 1, 0, 1, 0, 0, 1, 0, 0, 1};
+
+/* program 0 for macroblock k (non-first pictures): the MTYPE it stores */
+static int program_mtype(p64seq *s, int k, int64_t bc, int *mt) {
+  const int st = call_program(s, 0, decide(&s->h_me[k]), k, bc);
+  if (st) return st;
+  const int v = dtoi(p64prog_memory(s->prog)[P64PROG_MTYPE]);
+  if (v < 0 || v > 9) return fail(P64GPU_E_INVALID, "program 0 chose MTYPE %d (not 0..9)", v);
+  *mt = v;
+  return 0;
 }
 
 static p64gpu_encode_args picture_args(p64seq *s, int intra) {
@@ -228,6 +298,158 @@ static int fetch_gob(p64seq *s, int g) {
   return p64gpu_synchronize(NULL);
 }
 
+static int fetch_all(p64seq *s) {
+  int st;
+  const size_t nmb = (size_t)s->nmb;
+  if ((st = p64gpu_copy_to_host(s->h_mb, s->d_mb, nmb * sizeof(p64_mb_rec), NULL)) ||
+      (st = p64gpu_copy_to_host(s->h_coef, s->d_coef, nmb * 384 * sizeof(int16_t), NULL)))
+    return st;
+  return p64gpu_synchronize(NULL);
+}
+
+/* buffer overflow (p64.c:776-783): MTYPE 4 at (0,0), no coefficients; the
+ * GPU's reconstruction and LastIntra of the MB are redone after the picture */
+static void overflow_mb(p64seq *s, int k) {
+  s->h_mb[k].mtype = 4;
+  s->h_mb[k].cbp = 0x3f;
+  s->h_mb[k].mvx = s->h_mb[k].mvy = 0;
+  memset(s->h_coef + (size_t)k * 384, 0, 384 * sizeof(int16_t));
+  s->h_mask[k] = 1;
+  s->pic_ovfl++;
+}
+
+static int write_mb(p64seq *s, int m, int k) {
+  const int st = p64s_write_mb(s->wr, m, &s->h_mb[k], s->h_coef + (size_t)k * 384, s->mquant);
+  if (st) return st;
+  s->hist[s->h_mb[k].mtype]++;
+  s->mtype = s->h_mb[k].mtype; /* the MType global after the macroblock */
+  return 0;
+}
+
+static int fix_overflows(p64seq *s, const p64gpu_encode_args *a) {
+  int st;
+  const size_t nmb = (size_t)s->nmb;
+  if (!s->pic_ovfl) return 0;
+  if ((st = p64gpu_copy_to_device(s->d_mb, s->h_mb, nmb * sizeof(p64_mb_rec), NULL)) ||
+      (st = p64gpu_copy_to_device(s->d_mask, s->h_mask, nmb, NULL)) ||
+      (st = p64gpu_copy_to_device(s->d_q, s->h_q, nmb, NULL)) ||
+      (st = p64gpu_decode_recon(s->w, s->h, 1, (int64_t)s->pic, a->ref, a->recon, s->d_coef, s->d_mb,
+                                s->d_q, s->d_mask, NULL)) ||
+      (st = p64gpu_copy_to_host(s->h_li, s->d_li, nmb, NULL)) || (st = p64gpu_synchronize(NULL)))
+    return st;
+  for (size_t k = 0; k < nmb; k++)
+    if (s->h_mask[k]) s->h_li[k] = (uint8_t)(s->h_li_old[k] + 1);
+  if ((st = p64gpu_copy_to_device(s->d_li, s->h_li, nmb, NULL)) || (st = p64gpu_synchronize(NULL)))
+    return st;
+  s->novfl += s->pic_ovfl;
+  return 0;
+}
+
+/* fixed quantiser, no program: one launch for the picture, then the VLC */
+static int encode_batch(p64seq *s, p64gpu_encode_args *a) {
+  int st;
+  if ((st = p64gpu_encode_frames(a, NULL)) || (st = fetch_all(s))) return st;
+  for (int g = 0; g < s->ngob; g++) {
+    if ((st = p64s_write_gob_header(s->wr, g, s->gquant))) return st;
+    for (int m = 0; m < 33; m++)
+      if ((st = write_mb(s, m, s->h_lists[g * 33 + m]))) return st;
+  }
+  return 0;
+}
+
+/* rate control, no program: GOB by GOB */
+static int encode_per_gob(p64seq *s, p64gpu_encode_args *a, int first) {
+  int st;
+  for (int g = 0; g < s->ngob; g++) {
+    if (!first && (st = execute_quantization(s, g, 0, &s->gquant))) return st; /* p64.c:697-701 */
+    a->quant = s->gquant;
+    if ((st = p64s_write_gob_header(s->wr, g, s->gquant)) ||
+        (st = p64gpu_encode_mb_list(a, s->d_lists + g * 33, 33, NULL)) || (st = fetch_gob(s, g)))
+      return st;
+    for (int m = 0; m < 33; m++) {
+      const int k = s->h_lists[g * 33 + m];
+      s->h_q[k] = (uint8_t)s->gquant;
+      if (buffer_contents(s, g, m) > s->rate / 4) overflow_mb(s, k);
+      if ((st = write_mb(s, m, k))) return st;
+    }
+  }
+  return 0;
+}
+
+/* -o program, decisions independent of the bits written: program 0 for every
+ * macroblock in stream order, then one launch with the chosen types */
+static int encode_program_batch(p64seq *s, p64gpu_encode_args *a) {
+  int st;
+  const size_t nmb = (size_t)s->nmb;
+  uint8_t gq[12];
+  const int64_t bc = buffer_contents(s, 0, 0);
+  for (int g = 0; g < s->ngob; g++) {
+    gq[g] = (uint8_t)s->gquant;
+    for (int m = 0; m < 33; m++) {
+      const int k = s->h_lists[g * 33 + m];
+      int mt;
+      if ((st = program_mtype(s, k, bc, &mt))) return st;
+      if (s->h_li_old[k] > 131) mt = 0; /* p64.c:772-773 */
+      if (QUANT_MT[mt]) s->gquant = s->mquant; /* ReadCompressMDU p64.c:835-840 */
+      s->h_ov[k] = (int8_t)mt;
+      s->h_q[k] = (uint8_t)(QUANT_MT[mt] ? s->mquant : s->gquant);
+    }
+  }
+  a->mtype_override = s->d_ov;
+  a->quant_mb = s->d_q;
+  if ((st = p64gpu_copy_to_device(s->d_ov, s->h_ov, nmb, NULL)) ||
+      (st = p64gpu_copy_to_device(s->d_q, s->h_q, nmb, NULL)) || (st = p64gpu_encode_frames(a, NULL)) ||
+      (st = fetch_all(s)))
+    return st;
+  for (int g = 0; g < s->ngob; g++) {
+    if ((st = p64s_write_gob_header(s->wr, g, gq[g]))) return st;
+    for (int m = 0; m < 33; m++)
+      if ((st = write_mb(s, m, s->h_lists[g * 33 + m]))) return st;
+  }
+  return 0;
+}
+
+/* -o program whose decisions depend on the bits written (BUFFERCONTENTS, or
+ * rate control with program 1 between macroblocks): macroblock by macroblock
+ * in stream order, the exact order of p64EncodeGOB p64.c:692-786 */
+static int encode_program_serial(p64seq *s, p64gpu_encode_args *a, int first) {
+  int st;
+  a->mtype_override = s->d_ov;
+  a->quant_mb = s->d_q;
+  for (int g = 0; g < s->ngob; g++) {
+    if (s->rate && !first && (st = execute_quantization(s, g, 0, &s->gquant))) return st;
+    if ((st = p64s_write_gob_header(s->wr, g, s->gquant))) return st;
+    s->mtype = 0; /* p64.c:716 */
+    for (int m = 0; m < 33; m++) {
+      const int k = s->h_lists[g * 33 + m];
+      int mt = 0, unused;
+      if (s->rate && m && !(m % 11) && !first && (st = execute_quantization(s, g, m, &unused)))
+        return st;
+      if (!first && (st = program_mtype(s, k, buffer_contents(s, g, m), &mt))) return st;
+      if (s->h_li_old[k] > 131) mt = 0;
+      if (s->rate && buffer_contents(s, g, m) > s->rate / 4) {
+        s->h_q[k] = (uint8_t)s->gquant;
+        overflow_mb(s, k);
+      } else {
+        if (QUANT_MT[mt]) s->gquant = s->mquant;
+        const int8_t ov = (int8_t)mt;
+        const uint8_t q = (uint8_t)(QUANT_MT[mt] ? s->mquant : s->gquant);
+        s->h_q[k] = q;
+        if ((st = p64gpu_copy_to_device(s->d_ov + k, &ov, 1, NULL)) ||
+            (st = p64gpu_copy_to_device(s->d_q + k, &q, 1, NULL)) ||
+            (st = p64gpu_encode_mb_list(a, s->d_lists + g * 33 + m, 1, NULL)) ||
+            (st = p64gpu_copy_to_host(s->h_mb + k, s->d_mb + k, sizeof(p64_mb_rec), NULL)) ||
+            (st = p64gpu_copy_to_host(s->h_coef + (size_t)k * 384, s->d_coef + (size_t)k * 384,
+                                      384 * sizeof(int16_t), NULL)) ||
+            (st = p64gpu_synchronize(NULL)))
+          return st;
+      }
+      if ((st = write_mb(s, m, k))) return st;
+    }
+  }
+  return 0;
+}
+
 int p64seq_encode(p64seq *s, const uint8_t *picture) {
   int st;
   if (!s || !picture) return fail(P64GPU_E_INVALID, "p64seq_encode: NULL argument");
@@ -235,68 +457,27 @@ int p64seq_encode(p64seq *s, const uint8_t *picture) {
   const int first = s->current_frame == s->c.start_frame;
   const size_t nmb = (size_t)s->nmb;
   p64gpu_encode_args a = picture_args(s, first);
+  s->pic_ovfl = 0;
+  memset(s->h_mask, 0, nmb);
   if ((st = p64gpu_copy_to_device(s->d_cur, picture, s->pic, NULL))) return st;
+  if ((st = p64gpu_copy_to_host(s->h_li_old, s->d_li, nmb, NULL)) || (st = p64gpu_synchronize(NULL)))
+    return st;
   if ((st = p64s_write_picture_header(s->wr, s->c.format, s->current_frame % 32))) return st;
 
-  if (!s->rate) { /* one launch for the picture, then the VLC */
-    if ((st = p64gpu_encode_frames(&a, NULL)) ||
-        (st = p64gpu_copy_to_host(s->h_mb, s->d_mb, nmb * sizeof(p64_mb_rec), NULL)) ||
-        (st = p64gpu_copy_to_host(s->h_coef, s->d_coef, nmb * 384 * sizeof(int16_t), NULL)) ||
+  if (s->prog && !first) { /* GlobalMC (io.c:129): the records program 0 reads */
+    if ((st = p64gpu_motion_estimation(s->w, s->h, 1, (int64_t)s->pic, a.ref, s->d_cur, s->c.me_mode,
+                                       s->c.search_limit, s->d_me, NULL)) ||
+        (st = p64gpu_copy_to_host(s->h_me, s->d_me, nmb * sizeof(p64_me_rec), NULL)) ||
         (st = p64gpu_synchronize(NULL)))
       return st;
-    for (int g = 0; g < s->ngob; g++) {
-      if ((st = p64s_write_gob_header(s->wr, g, s->gquant))) return st;
-      for (int m = 0; m < 33; m++) {
-        const int k = s->h_lists[g * 33 + m];
-        if ((st = p64s_write_mb(s->wr, m, &s->h_mb[k], s->h_coef + (size_t)k * 384, 0))) return st;
-        s->hist[s->h_mb[k].mtype]++;
-      }
-    }
-  } else { /* rate control: GOB by GOB, GQUANT from the bits written so far */
-    int novfl = 0;
-    memset(s->h_mask, 0, nmb);
-    if ((st = p64gpu_copy_to_host(s->h_li_old, s->d_li, nmb, NULL)) || (st = p64gpu_synchronize(NULL)))
-      return st;
-    for (int g = 0; g < s->ngob; g++) {
-      if (!first) s->gquant = rate_gquant(s, g); /* p64.c:697-701 */
-      a.quant = s->gquant;
-      if ((st = p64s_write_gob_header(s->wr, g, s->gquant)) ||
-          (st = p64gpu_encode_mb_list(&a, s->d_lists + g * 33, 33, NULL)) || (st = fetch_gob(s, g)))
-        return st;
-      for (int m = 0; m < 33; m++) {
-        const int k = s->h_lists[g * 33 + m];
-        s->h_q[k] = (uint8_t)s->gquant;
-        /* buffer overflow: MTYPE 4, zero vector, no coefficients (p64.c:776-783) */
-        if (buffer_contents(s, g, m) > s->rate / 4) {
-          s->h_mb[k].mtype = 4;
-          s->h_mb[k].cbp = 0x3f;
-          s->h_mb[k].mvx = s->h_mb[k].mvy = 0;
-          memset(s->h_coef + (size_t)k * 384, 0, 384 * sizeof(int16_t));
-          s->h_mask[k] = 1;
-          novfl++;
-        }
-        if ((st = p64s_write_mb(s->wr, m, &s->h_mb[k], s->h_coef + (size_t)k * 384, 0))) return st;
-        s->hist[s->h_mb[k].mtype]++;
-      }
-    }
-    if (novfl) {
-      /* the GPU coded those MBs as it decided; redo their reconstruction as
-       * MTYPE 4 at (0,0) from the previous picture, and their LastIntra as a
-       * non-intra MB (p64.c:909-910) */
-      if ((st = p64gpu_copy_to_device(s->d_mb, s->h_mb, nmb * sizeof(p64_mb_rec), NULL)) ||
-          (st = p64gpu_copy_to_device(s->d_mask, s->h_mask, nmb, NULL)) ||
-          (st = p64gpu_copy_to_device(s->d_q, s->h_q, nmb, NULL)) ||
-          (st = p64gpu_decode_recon(s->w, s->h, 1, (int64_t)s->pic, a.ref, a.recon, s->d_coef, s->d_mb,
-                                    s->d_q, s->d_mask, NULL)) ||
-          (st = p64gpu_copy_to_host(s->h_li, s->d_li, nmb, NULL)) || (st = p64gpu_synchronize(NULL)))
-        return st;
-      for (size_t k = 0; k < nmb; k++)
-        if (s->h_mask[k]) s->h_li[k] = (uint8_t)(s->h_li_old[k] + 1);
-      if ((st = p64gpu_copy_to_device(s->d_li, s->h_li, nmb, NULL)) || (st = p64gpu_synchronize(NULL)))
-        return st;
-      s->novfl += novfl;
-    }
   }
+  if (!s->prog)
+    st = s->rate ? encode_per_gob(s, &a, first) : encode_batch(s, &a);
+  else if (!s->rate && (first || !p64prog_reads(s->prog, 0, P64PROG_BUFFERCONTENTS)))
+    st = first ? encode_batch(s, &a) : encode_program_batch(s, &a);
+  else
+    st = encode_program_serial(s, &a, first);
+  if (st || (st = fix_overflows(s, &a))) return st;
 
   /* p64EncodeFrame p64.c:653-682 */
   const int64_t x = bits_written(s);

@@ -23,8 +23,9 @@
  *   -d                      decode
  *   -                       y4m from stdin
  * Additions: -full / -tss (FastBME vs the shipped StepBME), -D device.
- * Not supported here: -o interpreter, -p parity (VERSION_1_0 only), -y reference
- * DCT, raw component-file input.
+ *   -o                      program interpreter: program text on stdin (p64prog.h)
+ * Not supported here: -p parity (VERSION_1_0 only), -y reference DCT, raw
+ * component-file input.
  *
  * Differences from the reference: a y4m that ends before -b finishes the
  * stream (trailer written) instead of exit(ERROR_BOUNDS) with an unterminated
@@ -35,10 +36,12 @@
 #include <string.h>
 
 #include "../../include/p64gpu.h"
+#include "../../include/p64prog.h"
 #include "../../include/p64seq.h"
 #include "../../include/p64stream.h"
 
 static const char *const FMT_NAME[3] = {"QCIF", "CIF", "NTSC"};
+static p64prog *g_prog; /* -o program */
 
 static int die(const char *what, int s) {
   fprintf(stderr, "p64gpu: %s: %s (%s)\n", what, p64gpu_strerror(s), p64gpu_last_error());
@@ -73,7 +76,7 @@ static int drain(p64s_writer *wr, FILE *o) {
 
 typedef struct {
   int format, y4m, first, last, skip, quant, sl, mode, device, decode, from_stdin;
-  int rate, file_size_bits, frame_rate, frame_rate_div;
+  int rate, file_size_bits, frame_rate, frame_rate_div, oracle;
   const char *prefix, *suffix, *stream;
 } opts;
 
@@ -131,6 +134,7 @@ static int encode(const opts *o) {
   cfg.frame_rate = o->frame_rate;
   cfg.frame_rate_div = o->frame_rate_div;
   cfg.device = o->device;
+  cfg.program = g_prog;
   p64seq *sq = NULL;
   if ((s = p64seq_open(&cfg, &sq))) return die("p64seq_open", s);
   p64seq_stats st;
@@ -300,6 +304,7 @@ int main(int argc, char **argv) {
     else if (!strcmp(a, "-s") && more) o.stream = argv[++i];
     else if (!strcmp(a, "-z") && more) o.suffix = argv[++i];
     else if (!strcmp(a, "-d")) o.decode = 1;
+    else if (!strcmp(a, "-o")) o.oracle = 1;
     else if (!strcmp(a, "-r") && more) o.rate = atoi(argv[++i]);
     else if (!strcmp(a, "-x") && more) o.file_size_bits = atoi(argv[++i]);
     else if (!strcmp(a, "-f") && more) {
@@ -337,5 +342,29 @@ int main(int argc, char **argv) {
   if (o.sl < 1) o.sl = 1;
   if (o.sl > 31) o.sl = 31;
   if (o.skip < 1) o.skip = 1;
+  if (o.oracle && !o.decode) {
+    /* -o: the program is read from stdin and its top-level statements run
+     * after the command line, so they override it (p64.c:409-413) */
+    size_t cap = 1 << 16, len = 0;
+    char *text = malloc(cap);
+    for (size_t n; (n = fread(text + len, 1, cap - len, stdin)) > 0;) {
+      len += n;
+      if (len == cap) text = realloc(text, cap *= 2);
+    }
+    int s = p64prog_load(text, len, stdout, &g_prog);
+    free(text);
+    if (s) return die("program", s);
+    p64prog_settings ps;
+    p64prog_settings_get(g_prog, &ps);
+    if (ps.quantization >= 0) o.quant = ps.quantization;
+    if (ps.search_limit >= 0) o.sl = ps.search_limit;
+    if (ps.frame_rate >= 0) o.frame_rate = ps.frame_rate, o.frame_rate_div = 1;
+    if (ps.frame_skip >= 0) o.skip = ps.frame_skip;
+    if (ps.image_type >= 0) o.format = ps.image_type;
+    if (o.from_stdin) {
+      fprintf(stderr, "p64gpu: -o reads the program from stdin; give the y4m as a file\n");
+      return 1;
+    }
+  }
   return o.decode ? decode(&o) : encode(&o);
 }

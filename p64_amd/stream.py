@@ -182,7 +182,50 @@ class SeqConfig(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int) for n in
                 ("format", "me_mode", "search_limit", "quant", "rate", "file_size_bits",
                  "start_frame", "last_frame", "frame_skip", "frame_rate", "frame_rate_div",
-                 "device")]
+                 "device")] + [("program", ctypes.c_void_p)]
+
+
+class ProgSettings(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int) for n in
+                ("quantization", "search_limit", "frame_rate", "frame_skip", "image_type",
+                 "abort_code")]
+
+
+class Program:
+    """The -o program interpreter (include/p64prog.h, lexer.l): loading runs the
+    top-level statements; programs 0 (MTYPE) and 1 (quantiser) are then called
+    by the sequence encoder."""
+
+    def __init__(self, text: str | bytes):
+        data = text.encode() if isinstance(text, str) else bytes(text)
+        self._h = ctypes.c_void_p()
+        _check(lib().p64prog_load(data, len(data), None, ctypes.byref(self._h)))
+        st = ProgSettings()
+        _check(lib().p64prog_settings_get(self._h, ctypes.byref(st)))
+        self.settings = st
+
+    def memory(self):
+        return np.ctypeslib.as_array(lib().p64prog_memory(self._h), shape=(1024,))
+
+    def execute(self, n: int) -> None:
+        _check(lib().p64prog_execute(self._h, n))
+
+    def reads(self, n: int, loc: int) -> bool:
+        return bool(lib().p64prog_reads(self._h, n, loc))
+
+    def defined(self, n: int) -> bool:
+        return bool(lib().p64prog_defined(self._h, n))
+
+    def close(self):
+        if self._h:
+            lib().p64prog_free(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 class SeqStats(ctypes.Structure):
@@ -199,8 +242,22 @@ class SequenceEncoder:
     def __init__(self, width: int, height: int, *, quant: int = 0, me_mode: int = 0,
                  search_limit: int = 15, first: int = 0, last: int | None = None, skip: int = 1,
                  rate: int = 0, file_size_bits: int = 0, frame_rate: int = 30000,
-                 frame_rate_div: int = 1001, device: int = 0, nframes: int | None = None):
+                 frame_rate_div: int = 1001, device: int = 0, nframes: int | None = None,
+                 program: "Program | str | bytes | None" = None):
         L = lib()
+        if program is not None and not isinstance(program, Program):
+            program = Program(program)
+        self.program = program  # kept alive for the encoder's lifetime
+        if program is not None:  # top-level settings override the arguments (p64.c:409-413)
+            ps = program.settings
+            if ps.quantization >= 0:
+                quant = ps.quantization
+            if ps.search_limit >= 0:
+                search_limit = ps.search_limit
+            if ps.frame_rate >= 0:
+                frame_rate, frame_rate_div = ps.frame_rate, 1
+            if ps.frame_skip >= 0:
+                skip = ps.frame_skip
         c = SeqConfig()
         L.p64seq_default_config(ctypes.byref(c))
         c.format = format_of(width, height)
@@ -209,6 +266,7 @@ class SequenceEncoder:
         c.start_frame = first
         c.last_frame = last if last is not None else first + skip * ((nframes or 1) - 1)
         c.frame_skip, c.frame_rate, c.frame_rate_div, c.device = skip, frame_rate, frame_rate_div, device
+        c.program = program._h if program is not None else None
         self.width, self.height = width, height
         self._h = ctypes.c_void_p()
         _check(L.p64seq_open(ctypes.byref(c), ctypes.byref(self._h)))
@@ -257,13 +315,13 @@ class SequenceEncoder:
 
 def encode_sequence(frames, width: int, height: int, *, quant: int = 0, me_mode: int = 0,
                     search_limit: int = 15, first: int = 0, skip: int = 1, rate: int = 0,
-                    file_size_bits: int = 0, device: int = 0) -> bytes:
+                    file_size_bits: int = 0, device: int = 0, program=None) -> bytes:
     """Encode frames[i] as frame first+i*skip: the reference CLI's `-a first
     -b last -k skip [-q] [-r|-x]` over the same pictures."""
     frames = list(frames)
     enc = SequenceEncoder(width, height, quant=quant, me_mode=me_mode, search_limit=search_limit,
                           first=first, skip=skip, rate=rate, file_size_bits=file_size_bits,
-                          device=device, nframes=len(frames))
+                          device=device, nframes=len(frames), program=program)
     try:
         for f in frames:
             if not enc.more():

@@ -242,6 +242,12 @@ def raster_index(fmt, g, m):
     return mby * 22 + mbx
 
 
+def prog_path(name):
+    """-o program files: the reference's own (test.*) or ours under progs/."""
+    ours = os.path.join(HERE, "progs", name)
+    return ours if os.path.exists(ours) else os.path.join(REFDIR, name)
+
+
 def run_sequence(name, fmt, nframes, seed, *, me="tss", sl=15, q=8, oracle_prog=None, rate=0,
                  filesize=0):
     """q=0 leaves -q off (rate control then derives InitialQuant, p64.c:579-586)."""
@@ -266,7 +272,7 @@ def run_sequence(name, fmt, nframes, seed, *, me="tss", sl=15, q=8, oracle_prog=
         if oracle_prog:
             cmd.append("-o")
         cmd += [os.path.join(td, "in"), "-z", ".y4m", "-s", os.path.join(td, "out.p64")]
-        stdin = open(os.path.join(REFDIR, oracle_prog)) if oracle_prog else subprocess.DEVNULL
+        stdin = open(prog_path(oracle_prog)) if oracle_prog else subprocess.DEVNULL
         subprocess.run(cmd, env=env, stdin=stdin, stdout=subprocess.DEVNULL, check=True)
         mbs, mes, recons = parse_dump(os.path.join(td, "dump.bin"), w, h)
         stream = open(os.path.join(td, "out.p64"), "rb").read()
@@ -354,6 +360,14 @@ def main():
     run_sequence("qcif_rate_q6", "QCIF", 6, 11, q=6, rate=120000)
     run_sequence("cif_rate_full31", "CIF", 5, 2, me="full", sl=31, q=12, rate=300000)
     run_sequence("qcif_filesize", "QCIF", 6, 13, q=0, filesize=60000)
+    # -o program interpreter (lexer.l): per-MB MTYPE (program 0), rate (program 1)
+    run_sequence("qcif_mtype", "QCIF", 6, 4, oracle_prog="test.mtype")
+    run_sequence("cif_fil_full31", "CIF", 3, 1, me="full", sl=31, oracle_prog="test.fil")
+    run_sequence("qcif_nof", "QCIF", 4, 12, oracle_prog="test.nof")
+    run_sequence("qcif_orate", "QCIF", 8, 3, q=0, rate=40000, oracle_prog="test.rate")
+    run_sequence("qcif_prog_mq", "QCIF", 5, 5, q=10, oracle_prog="mquant_bc.prog")
+    run_sequence("qcif_prog_mq_rate", "QCIF", 5, 6, q=10, rate=60000, oracle_prog="mquant_bc.prog")
+    run_sequence("qcif_prog_words", "QCIF", 4, 9, me="full", sl=31, oracle_prog="words.prog")
     if not ONLY:
         decode_md5()
 

@@ -10,7 +10,7 @@ import numpy as np
 import pytest
 
 from conftest import GOLDEN, REPO
-from test_oracle_golden import RATE_SEQS, SEQS, load, sequence_frames
+from test_oracle_golden import PROG_SEQS, RATE_SEQS, SEQS, load, sequence_frames
 
 pytestmark = pytest.mark.gpu
 
@@ -36,10 +36,19 @@ def cli_flags(z):
             f += [flag, str(int(z[key]))]
     if str(z["me"]) == "full":
         f.append("-full")
+    if str(z["oracle"]):
+        f.append("-o")
     return f
 
 
-@pytest.mark.parametrize("name", PLAIN + RATE_SEQS)
+def cli_stdin(z):
+    """-o reads the program from stdin (the reference's own test.* files are
+    kept as data under tests/golden/progs/)."""
+    prog = str(z["oracle"])
+    return open(os.path.join(GOLDEN, "progs", prog), "rb") if prog else subprocess.DEVNULL
+
+
+@pytest.mark.parametrize("name", PLAIN + RATE_SEQS + PROG_SEQS + ["qcif_intra"])
 def test_cli_encode_byte_identical(p64, torch_dev, tmp_path, name):
     """`p64gpu -FMT -y4m -a 0 -b N-1 [-q Q] -i SL [-r R | -x X] [-full]` == the
     reference CLI's .p64 (rate control included: per-GOB GQUANT, MTYPE 4 on
@@ -48,22 +57,26 @@ def test_cli_encode_byte_identical(p64, torch_dev, tmp_path, name):
     w, h = int(z["width"]), int(z["height"])
     write_y4m(tmp_path / "in.y4m", sequence_frames(p64, z), w, h)
     cmd = [CLI] + cli_flags(z) + [str(tmp_path / "in"), "-z", ".y4m", "-s", str(tmp_path / "o.p64")]
-    subprocess.run(cmd, check=True, stdout=subprocess.DEVNULL, timeout=300)
+    subprocess.run(cmd, check=True, stdin=cli_stdin(z), stdout=subprocess.DEVNULL, timeout=300)
     data = (tmp_path / "o.p64").read_bytes()
     assert len(data) == int(z["stream_len"])
     assert hashlib.sha256(data).hexdigest() == str(z["stream_sha256"])
 
 
 @pytest.mark.parametrize("name", ["qcif_tss", "cif_full31", "ntsc_tss", "qcif_rate",
-                                  "cif_rate_full31", "qcif_filesize"])
+                                  "cif_rate_full31", "qcif_filesize", "qcif_prog_mq_rate",
+                                  "qcif_orate", "qcif_prog_words"])
 def test_python_encode_sequence_byte_identical(p64, torch_dev, name):
     from p64_amd import stream
     z = load(f"seq_{name}.npz")
     w, h = int(z["width"]), int(z["height"])
     g = lambda k: int(z[k]) if k in z.files else 0  # noqa: E731
+    prog = str(z["oracle"])
+    program = open(os.path.join(GOLDEN, "progs", prog)).read() if prog else None
     data = stream.encode_sequence(sequence_frames(p64, z), w, h, quant=g("q"),
                                   me_mode=1 if str(z["me"]) == "full" else 0,
-                                  search_limit=g("sl"), rate=g("rate"), file_size_bits=g("filesize"))
+                                  search_limit=g("sl"), rate=g("rate"), file_size_bits=g("filesize"),
+                                  program=program)
     assert hashlib.sha256(data).hexdigest() == str(z["stream_sha256"])
 
 
@@ -88,7 +101,7 @@ def test_python_decode_short_p64_md5(p64, torch_dev):
 
 
 @pytest.mark.parametrize("name", ["qcif_tss", "qcif_full31", "qcif_q31", "qcif_flat_tss",
-                                  "qcif_rate", "qcif_filesize"])
+                                  "qcif_rate", "qcif_filesize", "qcif_prog_mq_rate", "qcif_orate"])
 def test_decode_of_encoded_stream_is_encoder_recon(p64, torch_dev, tmp_path, name):
     """encode -> .p64 -> decode (y4m) reproduces the encoder's closed-loop
     reconstruction, which the fixtures hold from the reference encoder
@@ -97,7 +110,7 @@ def test_decode_of_encoded_stream_is_encoder_recon(p64, torch_dev, tmp_path, nam
     w, h, n = int(z["width"]), int(z["height"]), int(z["nframes"])
     write_y4m(tmp_path / "in.y4m", sequence_frames(p64, z), w, h)
     enc = [CLI] + cli_flags(z) + [str(tmp_path / "in"), "-z", ".y4m", "-s", str(tmp_path / "o.p64")]
-    subprocess.run(enc, check=True, stdout=subprocess.DEVNULL, timeout=300)
+    subprocess.run(enc, check=True, stdin=cli_stdin(z), stdout=subprocess.DEVNULL, timeout=300)
     subprocess.run([CLI, "-d", "-y4m", "-s", str(tmp_path / "o.p64"), str(tmp_path / "dec")],
                    check=True, stdout=subprocess.DEVNULL, timeout=300)
     raw = (tmp_path / "dec.y4m").read_bytes()

@@ -78,8 +78,15 @@ def _rate_controlled(name):
 # fixed-quantiser runs: every picture at -q; the oracle and the batched GPU API
 # reproduce them directly.  Rate-controlled runs (-r/-x) choose GQUANT per GOB
 # from the bits written; they pin the sequence encoder (p64seq) instead.
-SEQS = [s for s in ALL_SEQS if _rate_controlled(s) == (0, 0)]
-RATE_SEQS = [s for s in ALL_SEQS if _rate_controlled(s) != (0, 0)]
+def _program(name):
+    return str(np.load(os.path.join(GOLDEN, f"seq_{name}.npz"))["oracle"])
+
+
+# -o runs other than test.intra (a constant MTYPE) are driven by the program
+# interpreter and pin the sequence encoder as well
+SEQS = [s for s in ALL_SEQS if _rate_controlled(s) == (0, 0) and _program(s) in ("", "test.intra")]
+RATE_SEQS = [s for s in ALL_SEQS if _rate_controlled(s) != (0, 0) and not _program(s)]
+PROG_SEQS = [s for s in ALL_SEQS if _program(s) not in ("", "test.intra")]
 
 
 def check_sequence_outputs(z, outs, label):

@@ -43,7 +43,8 @@ def write_fixture_stream(st, z):
     n = int(z["nframes"])
     for t in range(n):
         w.write_picture(t % 32, z["mb"][t].astype(np.int8), z["coef"][t],
-                        gob_quant(st, fmt, z["usequant"][t]))
+                        gob_quant(st, fmt, z["usequant"][t]),
+                        quant_mb=z["usequant"][t].astype(np.uint8))  # MQUANT of types 1/3/6/9
     return w.end(n % 32)
 
 
