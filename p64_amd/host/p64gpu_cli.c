@@ -24,12 +24,15 @@
  *   -                       y4m from stdin
  * Additions: -full / -tss (FastBME vs the shipped StepBME), -D device.
  *   -o                      program interpreter: program text on stdin (p64prog.h)
- * Not supported here: -p parity (VERSION_1_0 only), -y reference DCT, raw
- * component-file input.
+ *   (no -y4m)               raw component files <prefix><n>.Y/.U/.V per picture
+ * Not supported here: -p parity (VERSION_1_0 only), -y floating-point reference
+ * DCT (a test option).
  *
  * Differences from the reference: a y4m that ends before -b finishes the
  * stream (trailer written) instead of exit(ERROR_BOUNDS) with an unterminated
- * file; every failure exits non-zero with a message, never a segfault.
+ * file; raw-file input ends with a complete stream (the reference crashes in
+ * video_input_close before swclose, SURVEY.md 0.8, leaving it unflushed); every
+ * failure exits non-zero with a message, never a segfault.
  */
 #include <stdio.h>
 #include <stdlib.h>
@@ -80,23 +83,41 @@ typedef struct {
   const char *prefix, *suffix, *stream;
 } opts;
 
+/* raw component files <prefix><frame><suffix>, suffixes .Y .U .V by default
+ * (MakeFileNames p64.c:1581, LoadMem mem.c) -- one file per plane and picture */
+static int read_raw(const opts *o, int frame, int w, int h, unsigned char *buf) {
+  static const char *const sfx[3] = {".Y", ".U", ".V"};
+  const size_t n[3] = {(size_t)w * h, (size_t)w * h / 4, (size_t)w * h / 4};
+  size_t off = 0;
+  for (int c = 0; c < 3; c++) {
+    char path[4096];
+    snprintf(path, sizeof path, "%s%d%s", o->prefix, frame, sfx[c]);
+    FILE *f = fopen(path, "rb");
+    const size_t got = f ? fread(buf + off, 1, n[c], f) : 0;
+    if (f) fclose(f);
+    if (got != n[c]) return 0;
+    off += n[c];
+  }
+  return 1;
+}
+
 static int encode(const opts *o) {
   char path[4096];
-  FILE *f;
-  if (!o->y4m) {
-    fprintf(stderr, "p64gpu: only -y4m input is supported\n");
-    return 1;
-  }
-  if (o->from_stdin) {
-    f = stdin;
-  } else {
-    snprintf(path, sizeof path, "%s%s", o->prefix, o->suffix ? o->suffix : ".y4m");
-    f = fopen(path, "rb");
-  }
+  FILE *f = NULL;
   int w, h, s;
-  if (!f || read_y4m_header(f, &w, &h)) {
-    fprintf(stderr, "p64gpu: cannot read y4m input\n");
-    return 1;
+  if (o->y4m) {
+    if (o->from_stdin) {
+      f = stdin;
+    } else {
+      snprintf(path, sizeof path, "%s%s", o->prefix, o->suffix ? o->suffix : ".y4m");
+      f = fopen(path, "rb");
+    }
+    if (!f || read_y4m_header(f, &w, &h)) {
+      fprintf(stderr, "p64gpu: cannot read y4m input\n");
+      return 1;
+    }
+  } else { /* raw planes: the format comes from the flags (ImageType default NTSC, p64.c:114) */
+    p64s_geometry(o->format >= 0 ? o->format : P64S_NTSC, &w, &h, NULL);
   }
   const int fmt = p64s_format_of(w, h);
   if (fmt < 0 || (o->format >= 0 && fmt != o->format)) {
@@ -107,7 +128,7 @@ static int encode(const opts *o) {
   const size_t pic = (size_t)w * h * 3 / 2;
   unsigned char *buf = malloc(pic);
   /* seek to StartFrame (p64.c:562-565) */
-  for (int i = 0; i < o->first; i++)
+  for (int i = 0; f && i < o->first; i++)
     if (read_frame(f, buf, pic) != 1) {
       fprintf(stderr, "p64gpu: input ends before frame %d\n", o->first);
       return 1;
@@ -143,9 +164,11 @@ static int encode(const opts *o) {
   printf("START>SEQUENCE\n");
   while (p64seq_more(sq)) {
     p64seq_get_stats(sq, &st);
-    const int r = read_frame(f, buf, pic);
+    /* y4m pictures are read in sequence whatever -k says (ReadIob io.c:629-645);
+     * raw files are named by the frame number */
+    const int r = f ? read_frame(f, buf, pic) : read_raw(o, st.next_frame, w, h, buf);
     if (r <= 0) {
-      if (r < 0) fprintf(stderr, "p64gpu: bad y4m frame at %d\n", st.next_frame);
+      if (r < 0 || !f) fprintf(stderr, "p64gpu: cannot read frame %d\n", st.next_frame);
       break;
     }
     if ((s = p64seq_encode(sq, buf))) return die("encode", s);
@@ -169,7 +192,7 @@ static int encode(const opts *o) {
   for (int k = 0; k < 10; k++) printf(" %d", st.mtype_hist[k]);
   printf("\n");
   p64seq_close(sq);
-  if (f != stdin) fclose(f);
+  if (f && f != stdin) fclose(f);
   free(buf);
   return 0;
 }

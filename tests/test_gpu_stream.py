@@ -122,3 +122,19 @@ def test_decode_of_encoded_stream_is_encoder_recon(p64, torch_dev, tmp_path, nam
         c = body[t * (6 + pic):(t + 1) * (6 + pic)]
         assert c[:6] == b"FRAME\n"
         np.testing.assert_array_equal(np.frombuffer(c[6:], np.uint8), z["recon"][t], err_msg=f"t{t}")
+
+
+@pytest.mark.parametrize("name", ["qcif_tss", "cif_full31"])
+def test_cli_raw_component_input(p64, torch_dev, tmp_path, name):
+    """Without -y4m the CLI reads <prefix><n>.Y/.U/.V per picture (MakeFileNames
+    p64.c:1581); the same pictures give the reference's y4m-run stream."""
+    z = load(f"seq_{name}.npz")
+    w, h = int(z["width"]), int(z["height"])
+    for t, fr in enumerate(sequence_frames(p64, z)):
+        for c, (a, b) in zip("YUV", ((0, w * h), (w * h, w * h * 5 // 4), (w * h * 5 // 4, w * h * 3 // 2))):
+            (tmp_path / f"raw{t}.{c}").write_bytes(fr[a:b].tobytes())
+    flags = [f for f in cli_flags(z) if f != "-y4m"]
+    subprocess.run([CLI] + flags + [str(tmp_path / "raw"), "-s", str(tmp_path / "o.p64")],
+                   check=True, stdout=subprocess.DEVNULL, timeout=300)
+    data = (tmp_path / "o.p64").read_bytes()
+    assert hashlib.sha256(data).hexdigest() == str(z["stream_sha256"])

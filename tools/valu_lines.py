@@ -20,7 +20,7 @@ for l in text:
         files[int(m.group(1))] = m.group(3)
     if re.match(r"^_Z\w*" + ".*:", l) and sys.argv[1] in l.split(":")[0]:
         on = True
-    elif on and "s_endpgm" in l:
+    elif on and l.startswith(".Lfunc_end"):
         on = False
     if on:
         body.append(l)
