@@ -31,8 +31,11 @@ p64_amd/csrc/p64seq.o: p64_amd/csrc/p64seq.c include/p64seq.h include/p64stream.
 p64_amd/csrc/p64prog.o: p64_amd/csrc/p64prog.c include/p64prog.h include/p64gpu.h
 	$(CC) -O2 -fPIC -Wall -Wextra -c $< -o $@
 
+p64_amd/csrc/p64vlc.o: p64_amd/csrc/p64vlc.hip include/p64gpu.h include/p64stream.h
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
 $(LIB): p64_amd/csrc/p64gpu.o p64_amd/csrc/synth.o p64_amd/csrc/p64stream.o p64_amd/csrc/p64seq.o \
-        p64_amd/csrc/p64prog.o
+        p64_amd/csrc/p64prog.o p64_amd/csrc/p64vlc.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $^
 
 p64_amd/p64gpu: p64_amd/host/p64gpu_cli.c $(LIB) include/p64gpu.h include/p64stream.h include/p64seq.h

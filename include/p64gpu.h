@@ -178,6 +178,31 @@ int p64gpu_decode_recon(int width, int height, int nframes, int64_t frame_stride
                         const p64_mb_rec *mb, const uint8_t *quant_mb,
                         const uint8_t *coded_mask, void *stream);
 
+/* ---- entropy coding on the device (p64vlc.hip) -------------------------- */
+/* The H.261 bits of nframes coded pictures (QCIF/CIF/NTSC), identical to
+ * p64s_write_picture (p64stream.h) and thus to the reference's WriteMDU/
+ * WriteMBHeader/WriteGOBHeader/WritePictureHeader output.  Picture i is
+ * written into out + i*out_stride starting at bit phase[i] (0..7) of its first
+ * byte -- the bit position the sequence's stream has reached -- so the host
+ * appends it by OR-ing the first byte into its pending byte.  bits[i] receives
+ * the bit count including the phase, or 0xFFFFFFFF if a record was invalid.
+ * All pointers are device pointers; scratch holds 2*nframes*nmb uint32. */
+typedef struct {
+  int width, height, nframes, reserved;
+  const p64_mb_rec *mb;     /* [nframes][nmb] raster order (encoder output)   */
+  const int16_t *coef;      /* [nframes][nmb][6][64] zigzag levels            */
+  const uint8_t *gquant;    /* [nframes][ngob] GQUANT of each GOB header      */
+  const uint8_t *mquant;    /* NULL or [nframes][nmb] MQUANT (types 1/3/6/9)  */
+  const int32_t *tr;        /* [nframes] temporal references                  */
+  const uint8_t *phase;     /* NULL (all 0) or [nframes] start bit 0..7       */
+  uint8_t *out;             /* [nframes][out_stride], zeroed by the call      */
+  int64_t out_stride;       /* >= p64gpu_vlc_max_bytes, multiple of 4         */
+  uint32_t *bits;           /* [nframes]                                      */
+  uint32_t *scratch;        /* [2][nframes][nmb]                              */
+} p64gpu_vlc_args;
+int64_t p64gpu_vlc_max_bytes(int width, int height);
+int p64gpu_vlc_pictures(const p64gpu_vlc_args *args, void *stream);
+
 /* ---- host-buffer encoder context (drop-in for a C host loop) ------------ */
 typedef struct p64gpu_encoder p64gpu_encoder;
 int p64gpu_encoder_open(int device, int width, int height, int me_mode,

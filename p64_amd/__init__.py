@@ -150,6 +150,9 @@ def lib() -> ctypes.CDLL:
     L.p64seq_writer.restype = vp
     L.p64seq_get_stats.argtypes = [vp, vp]
     L.p64gpu_encode_mb_list.argtypes = [ctypes.POINTER(EncodeArgs), vp, i32, vp]
+    L.p64gpu_vlc_max_bytes.argtypes = [i32, i32]
+    L.p64gpu_vlc_max_bytes.restype = i64
+    L.p64gpu_vlc_pictures.argtypes = [vp, vp]
     # -o program interpreter (include/p64prog.h), host C
     L.p64prog_load.argtypes = [ctypes.c_char_p, ctypes.c_size_t, vp, ctypes.POINTER(vp)]
     L.p64prog_free.argtypes = [vp]

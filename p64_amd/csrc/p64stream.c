@@ -236,6 +236,25 @@ static int tables(void) {
   return g_tables_ok ? 0 : fail(P64GPU_E_STREAM, "VLC tables are not prefix-free");
 }
 
+/* internal (p64vlc.hip): the encode tables as code | len << 16 words --
+ * mtype[10], mvd[32], cbp[64], tcoeff[27][16], then EOB, ESCAPE, first-(0,1) */
+int p64s_vlc_tables_(uint32_t *t) {
+  int s = tables();
+  if (s) return s;
+  uint32_t *p = t;
+#define PUT(e) (*p++ = (uint32_t)(e).code | (uint32_t)(e).len << 16)
+  for (int i = 0; i < 10; i++) PUT(E_MTYPE[i]);
+  for (int i = 0; i < 32; i++) PUT(E_MVD[i]);
+  for (int i = 0; i < 64; i++) PUT(E_CBP[i]);
+  for (int r = 0; r < TC_RUNS; r++)
+    for (int l = 0; l < TC_LEVELS; l++) PUT(E_TC[r][l]);
+  PUT(E_EOB);
+  PUT(E_ESC);
+  PUT(E_TC_FIRST01);
+#undef PUT
+  return 0;
+}
+
 /* ---- writer -------------------------------------------------------------- */
 struct p64s_writer {
   uint8_t *buf;

@@ -355,3 +355,91 @@ def decode_sequence(data: bytes, start_frame: int = 0) -> list[np.ndarray]:
         prev ^= 1
     counts = output_schedule(trs, r.end_tr, start_frame)
     return [pic for pic, n in zip(pics, counts) for _ in range(n)]
+
+
+# ---------------------------------------------------------------------------
+# entropy coding on the device (p64gpu_vlc_pictures, p64vlc.hip)
+
+class VlcArgs(ctypes.Structure):
+    _fields_ = [("width", ctypes.c_int), ("height", ctypes.c_int), ("nframes", ctypes.c_int),
+                ("reserved", ctypes.c_int), ("mb", ctypes.c_void_p), ("coef", ctypes.c_void_p),
+                ("gquant", ctypes.c_void_p), ("mquant", ctypes.c_void_p), ("tr", ctypes.c_void_p),
+                ("phase", ctypes.c_void_p), ("out", ctypes.c_void_p), ("out_stride", ctypes.c_int64),
+                ("bits", ctypes.c_void_p), ("scratch", ctypes.c_void_p)]
+
+
+def vlc_pictures(mb, coef, gquant, tr, *, width: int, height: int, phase=None, mquant=None):
+    """H.261 bits of a batch of pictures on the GPU.  All inputs are CUDA(HIP)
+    tensors: mb [n, nmb, 4] int8, coef [n, nmb, 6, 64] int16, gquant [n, ngob]
+    uint8, tr [n] int32, phase [n] uint8 or None, mquant [n, nmb] uint8 or None.
+    Returns (out [n, stride] uint8 tensor, bits [n] list of ints)."""
+    import torch
+
+    from . import _stream, _torch
+    _torch()
+    L = lib()
+    n = int(tr.numel())
+    _, _, ngob = geometry(format_of(width, height))
+    nmb = ngob * 33
+    if mb.numel() != n * nmb * 4 or coef.numel() != n * nmb * 384 or gquant.numel() != n * ngob:
+        raise P64GpuError("vlc_pictures: buffer sizes do not match the picture format")
+    stride = int(L.p64gpu_vlc_max_bytes(width, height))
+    stride = (stride + 3) // 4 * 4
+    out = torch.empty((n, stride), dtype=torch.uint8, device="cuda")
+    bits = torch.empty(n, dtype=torch.int32, device="cuda")
+    scratch = torch.empty(2 * n * nmb, dtype=torch.int32, device="cuda")
+    a = VlcArgs(width=width, height=height, nframes=n, reserved=0, mb=mb.data_ptr(),
+                coef=coef.data_ptr(), gquant=gquant.data_ptr(),
+                mquant=mquant.data_ptr() if mquant is not None else None, tr=tr.data_ptr(),
+                phase=phase.data_ptr() if phase is not None else None, out=out.data_ptr(),
+                out_stride=stride, bits=bits.data_ptr(), scratch=scratch.data_ptr())
+    _check(L.p64gpu_vlc_pictures(ctypes.byref(a), _stream(torch)))
+    b = [int(x) & 0xFFFFFFFF for x in bits.cpu().tolist()]
+    if any(x == 0xFFFFFFFF for x in b):
+        raise P64GpuError("vlc_pictures: invalid macroblock record or buffer overflow")
+    return out, b
+
+
+class BitAssembler:
+    """Concatenates pictures coded at a bit phase (vlc_pictures) into one
+    stream, and closes it like p64s_write_end (trailer header + ones)."""
+
+    def __init__(self):
+        self.buf = bytearray()
+        self.nbits = 0
+
+    @property
+    def phase(self) -> int:
+        return self.nbits % 8
+
+    def append(self, data: bytes, bits: int) -> None:
+        """data was produced at phase == self.phase; bits includes the phase."""
+        p = self.phase
+        nbytes = (bits + 7) // 8
+        chunk = bytes(data[:nbytes])
+        if p:
+            self.buf[-1] |= chunk[0]
+            chunk = chunk[1:]
+        self.buf += chunk
+        self.nbits += bits - p
+
+    def end(self, fmt: int, tr: int) -> bytes:
+        hdr = (0x10 << 12) | ((tr & 31) << 7) | ((0 if fmt == QCIF else 4) << 1)
+        n = 32
+        if fmt == NTSC:
+            hdr = (hdr >> 1 << 10) | (0x18c << 1)
+            n = 41
+        v, nb = hdr, n
+        pad = (-(self.nbits + nb)) % 8
+        v = (v << pad) | ((1 << pad) - 1)
+        nb += pad
+        p = self.phase
+        total = p + nb
+        word = v  # place at bit phase p within (p + nb) bits
+        data = word.to_bytes(total // 8, "big")
+        if p:
+            self.buf[-1] |= data[0]
+            data = data[1:]
+        self.buf += data
+        self.nbits += nb
+        return bytes(self.buf)

@@ -138,3 +138,71 @@ def test_cli_raw_component_input(p64, torch_dev, tmp_path, name):
                    check=True, stdout=subprocess.DEVNULL, timeout=300)
     data = (tmp_path / "o.p64").read_bytes()
     assert hashlib.sha256(data).hexdigest() == str(z["stream_sha256"])
+
+
+# ---------------------------------------------------------------------------
+# entropy coding on the GPU (p64gpu_vlc_pictures)
+
+def fixture_records(z, fmt_code):
+    from test_stream import gob_quant
+    from p64_amd import stream
+    n = int(z["nframes"])
+    gq = np.stack([gob_quant(stream, fmt_code, z["usequant"][t]) for t in range(n)])
+    return z["mb"].astype(np.int8), z["coef"].astype(np.int16), gq, z["usequant"].astype(np.uint8)
+
+
+@pytest.mark.parametrize("name", ["qcif_tss", "qcif_q1", "qcif_intra", "cif_full31", "ntsc_tss",
+                                  "qcif_rate", "qcif_prog_mq", "qcif_prog_words", "cif_scene_full31"])
+def test_gpu_vlc_byte_identical(p64, torch_dev, name):
+    """GPU entropy coding of the fixture's records, picture by picture at the
+    stream's running bit phase, reassembled == the reference's .p64."""
+    from p64_amd import stream
+    torch = torch_dev
+    z = load(f"seq_{name}.npz")
+    w, h, n = int(z["width"]), int(z["height"]), int(z["nframes"])
+    fmt = stream.format_of(w, h)
+    mb, coef, gq, uq = fixture_records(z, fmt)
+    d = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()  # noqa: E731
+    asm = stream.BitAssembler()
+    for t in range(n):
+        out, bits = stream.vlc_pictures(d(mb[t:t + 1]), d(coef[t:t + 1]), d(gq[t:t + 1]),
+                                        d(np.array([t % 32], np.int32)), width=w, height=h,
+                                        phase=d(np.array([asm.phase], np.uint8)),
+                                        mquant=d(uq[t:t + 1]))
+        asm.append(out[0].cpu().numpy().tobytes(), bits[0])
+    data = asm.end(fmt, n % 32)
+    assert len(data) == int(z["stream_len"])
+    assert hashlib.sha256(data).hexdigest() == str(z["stream_sha256"])
+
+
+def test_gpu_vlc_batch_matches_host_writer(p64, torch_dev):
+    """One launch over pictures of several sequences, each at its own phase,
+    equals the host writer's bits for every picture."""
+    from p64_amd import stream
+    torch = torch_dev
+    names = ["qcif_tss", "qcif_q31", "qcif_full31", "qcif_prog_words"]
+    recs, pics = [], []
+    for name in names:
+        z = load(f"seq_{name}.npz")
+        fmt = stream.format_of(176, 144)
+        mb, coef, gq, uq = fixture_records(z, fmt)
+        for t in range(int(z["nframes"])):
+            recs.append((mb[t], coef[t], gq[t], uq[t], t % 32))
+    rng = np.random.default_rng(1)
+    phases = rng.integers(0, 8, len(recs)).astype(np.uint8)
+    d = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()  # noqa: E731
+    out, bits = stream.vlc_pictures(d(np.stack([r[0] for r in recs])), d(np.stack([r[1] for r in recs])),
+                                    d(np.stack([r[2] for r in recs])),
+                                    d(np.array([r[4] for r in recs], np.int32)), width=176, height=144,
+                                    phase=d(phases), mquant=d(np.stack([r[3] for r in recs])))
+    out = out.cpu().numpy()
+    for i, (mb, coef, gq, uq, tr) in enumerate(recs):
+        wr = stream.Writer(stream.QCIF)
+        wr.write_picture(tr, mb, coef, gq, quant_mb=uq)
+        host_bits = wr.bits()
+        full = wr.data()  # the complete bytes; the last partial byte is pending
+        nb = (bits[i] + 7) // 8
+        gpu = int.from_bytes(out[i, :nb].tobytes(), "big") >> (nb * 8 - bits[i])
+        assert bits[i] - int(phases[i]) == host_bits
+        assert gpu >> host_bits == 0  # the leading phase bits are zero
+        assert gpu >> (host_bits - 8 * len(full)) == int.from_bytes(full, "big")
