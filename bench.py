@@ -63,6 +63,7 @@ def parse():
     p.add_argument("--cpu-procs", type=int, default=8)
     p.add_argument("--cpu-frames", type=int, default=120)
     p.add_argument("--no-verify", action="store_true")
+    p.add_argument("--no-vlc", action="store_true", help="skip the encode+entropy-coding measurement")
     p.add_argument("--pmc-json", default=os.path.join(REPO, "profiles", "pmc_traffic.json"))
     return p.parse_args()
 
@@ -246,6 +247,40 @@ def main():
         if not verified:
             raise SystemExit("bench: GPU output differs from the oracle -- refusing to report")
 
+    # the same steps followed by entropy coding on the device (p64vlc.hip): the
+    # whole-encoder rate to .p64 bits, measured after the metric and after the
+    # verification (it re-runs steps, so the closed-loop state is not reused)
+    with_vlc = None
+    if not args.no_vlc:
+        try:
+            from p64_amd import stream as p64s
+            ngob = nmb // 33
+            gq = torch.full((S, ngob), args.quant, dtype=torch.uint8, device="cuda")
+            vlc_ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+            bits_tot = 0
+            vsteps = min(args.steps, 8)
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            for k in range(vsteps):
+                t = 1 + args.warmup + k
+                vlc_ev[0].record()
+                step(t)
+                vlc_ev[1].record()
+                trs = torch.full((S,), t % 32, dtype=torch.int32, device="cuda")
+                _, bits = p64s.vlc_pictures(out.mb, out.coef, gq, trs, width=w, height=h)
+                vlc_ev[2].record()
+                bits_tot += sum(bits)
+            torch.cuda.synchronize()
+            dt = time.perf_counter() - t1
+            with_vlc = {"macroblocks_per_s": round(S * nmb * vsteps / dt, 1),
+                        "ms_per_step": round(dt / vsteps * 1e3, 4),
+                        "vlc_ms_last_step": round(vlc_ev[1].elapsed_time(vlc_ev[2]), 4),
+                        "avg_bits_per_mb": round(bits_tot / (S * nmb * vsteps), 2),
+                        "note": "encode launch + GPU entropy coding (count, scan, emit) per step, "
+                                "bits copied to the host; not part of `value`"}
+        except Exception as e:  # never let the extra measurement cost the bench line
+            with_vlc = {"error": str(e)[:200]}
+
     if world > 1:
         dist.destroy_process_group()
     if rank != 0:
@@ -294,6 +329,7 @@ def main():
                                  "per MB; the FULL kernel executes fewer (exact partial-"
                                  "distortion pruning, DESIGN.md)"},
         "cpu_baseline": cpu,
+        "with_vlc": with_vlc,
         "verified_vs_oracle": verified,
     }
     print(json.dumps(line), flush=True)
