@@ -53,6 +53,9 @@ typedef struct {
   void *program;         /* p64prog* (-o, p64prog.h) or NULL; borrowed, must
                             outlive the encoder; its top-level settings are the
                             caller's to apply to this config                  */
+  int host_vlc;          /* 1: entropy-code on the host (p64stream.h) always;
+                            0 (default): pictures coded in one launch are
+                            entropy-coded on the GPU (p64gpu_vlc_pictures)     */
 } p64seq_config;
 
 typedef struct {

@@ -69,6 +69,11 @@ int p64s_write_picture(p64s_writer *w, int format, int tr, const uint8_t *gquant
 int p64s_write_picture_header(p64s_writer *w, int format, int tr);
 int p64s_write_gob_header(p64s_writer *w, int gob, int gquant);
 int p64s_write_mb(p64s_writer *w, int mdu, const p64_mb_rec *mb, const int16_t *coef, int mquant);
+/* Appends bits coded elsewhere (p64gpu_vlc_pictures): data holds `bits` bits
+ * of which the first `phase` are the writer's pending partial byte, so phase
+ * must equal p64s_writer_phase(). */
+int p64s_write_bits(p64s_writer *w, const uint8_t *data, int64_t bits, int phase);
+int p64s_writer_phase(const p64s_writer *w);
 /* Raster macroblock index of MDU m (0..32) of GOB g (Bpos, io.c:757), -1 if
  * out of range. */
 int p64s_raster_mb(int format, int gob, int mdu);

@@ -50,6 +50,11 @@ struct p64seq {
   int32_t *h_lists;
   p64s_writer *wr;
   p64prog *prog; /* -o program, or NULL */
+  /* device entropy coding of whole pictures (p64gpu_vlc_pictures) */
+  uint8_t *d_vout, *d_vgq, *d_vphase, *h_vout;
+  uint32_t *d_vbits, *d_vscratch;
+  int32_t *d_vtr;
+  int64_t vstride;
   /* reference state (p64.c globals) */
   int current_frame, rate, qdfact, qoffs, gquant, mquant, mtype, buffer_offset, novfl, pic_ovfl;
   int frames, finished;
@@ -78,6 +83,13 @@ void p64seq_close(p64seq *s) {
   p64gpu_free(s->d_lists);
   p64gpu_free(s->d_ov);
   p64gpu_free(s->d_me);
+  p64gpu_free(s->d_vout);
+  p64gpu_free(s->d_vgq);
+  p64gpu_free(s->d_vphase);
+  p64gpu_free(s->d_vbits);
+  p64gpu_free(s->d_vscratch);
+  p64gpu_free(s->d_vtr);
+  free(s->h_vout);
   free(s->h_ov);
   free(s->h_me);
   free(s->h_coef);
@@ -151,6 +163,18 @@ int p64seq_open(const p64seq_config *cfg, p64seq **out) {
   }
   free(zero);
   if ((st = p64s_writer_open(&s->wr))) goto bad;
+  if (!c->host_vlc) {
+    s->vstride = (p64gpu_vlc_max_bytes(s->w, s->h) + 3) & ~(int64_t)3;
+    if ((st = p64gpu_alloc((void **)&s->d_vout, (size_t)s->vstride)) ||
+        (st = p64gpu_alloc((void **)&s->d_vgq, 12)) || (st = p64gpu_alloc((void **)&s->d_vphase, 1)) ||
+        (st = p64gpu_alloc((void **)&s->d_vbits, 4)) || (st = p64gpu_alloc((void **)&s->d_vtr, 4)) ||
+        (st = p64gpu_alloc((void **)&s->d_vscratch, 2 * nmb * sizeof(uint32_t))))
+      goto bad;
+    if (!(s->h_vout = (uint8_t *)malloc((size_t)s->vstride))) {
+      st = fail(P64GPU_E_NOMEM, "p64seq: host buffers");
+      goto bad;
+    }
+  }
 
   /* p64EncodeSequence p64.c:566-595 */
   s->current_frame = c->start_frame;
@@ -348,6 +372,43 @@ static int fix_overflows(p64seq *s, const p64gpu_encode_args *a) {
 /* fixed quantiser, no program: one launch for the picture, then the VLC */
 static int encode_batch(p64seq *s, p64gpu_encode_args *a) {
   int st;
+  if (s->d_vout) { /* GPU entropy coding: only the picture's bits cross PCIe */
+    const int phase = p64s_writer_phase(s->wr);
+    const int32_t tr = s->current_frame % 32;
+    const uint8_t ph = (uint8_t)phase;
+    uint8_t gq[12];
+    uint32_t bits = 0;
+    memset(gq, s->gquant, sizeof gq);
+    p64gpu_vlc_args v;
+    memset(&v, 0, sizeof v);
+    v.width = s->w;
+    v.height = s->h;
+    v.nframes = 1;
+    v.mb = s->d_mb;
+    v.coef = s->d_coef;
+    v.gquant = s->d_vgq;
+    v.tr = s->d_vtr;
+    v.phase = s->d_vphase;
+    v.out = s->d_vout;
+    v.out_stride = s->vstride;
+    v.bits = s->d_vbits;
+    v.scratch = s->d_vscratch;
+    if ((st = p64gpu_encode_frames(a, NULL)) || (st = p64gpu_copy_to_device(s->d_vgq, gq, 12, NULL)) ||
+        (st = p64gpu_copy_to_device(s->d_vtr, &tr, 4, NULL)) ||
+        (st = p64gpu_copy_to_device(s->d_vphase, &ph, 1, NULL)) || (st = p64gpu_vlc_pictures(&v, NULL)) ||
+        (st = p64gpu_copy_to_host(&bits, s->d_vbits, 4, NULL)) ||
+        (st = p64gpu_copy_to_host(s->h_mb, s->d_mb, (size_t)s->nmb * sizeof(p64_mb_rec), NULL)) ||
+        (st = p64gpu_synchronize(NULL)))
+      return st;
+    if (bits == 0xFFFFFFFFu) return fail(P64GPU_E_STREAM, "GPU entropy coder rejected the picture");
+    if ((st = p64gpu_copy_to_host(s->h_vout, s->d_vout, (bits + 7) / 8, NULL)) ||
+        (st = p64gpu_synchronize(NULL)) || (st = p64s_write_bits(s->wr, s->h_vout, bits, phase)))
+      return st;
+    for (int k = 0; k < s->nmb; k++) s->hist[s->h_mb[k].mtype]++;
+    s->mtype = s->h_mb[s->h_lists[s->nmb - 1]].mtype;
+    return 0;
+  }
+  if ((st = p64s_write_picture_header(s->wr, s->c.format, s->current_frame % 32))) return st;
   if ((st = p64gpu_encode_frames(a, NULL)) || (st = fetch_all(s))) return st;
   for (int g = 0; g < s->ngob; g++) {
     if ((st = p64s_write_gob_header(s->wr, g, s->gquant))) return st;
@@ -462,7 +523,10 @@ int p64seq_encode(p64seq *s, const uint8_t *picture) {
   if ((st = p64gpu_copy_to_device(s->d_cur, picture, s->pic, NULL))) return st;
   if ((st = p64gpu_copy_to_host(s->h_li_old, s->d_li, nmb, NULL)) || (st = p64gpu_synchronize(NULL)))
     return st;
-  if ((st = p64s_write_picture_header(s->wr, s->c.format, s->current_frame % 32))) return st;
+  /* encode_batch writes (or has the GPU write) its own picture header */
+  if ((s->rate || (s->prog && !first)) &&
+      (st = p64s_write_picture_header(s->wr, s->c.format, s->current_frame % 32)))
+    return st;
 
   if (s->prog && !first) { /* GlobalMC (io.c:129): the records program 0 reads */
     if ((st = p64gpu_motion_estimation(s->w, s->h, 1, (int64_t)s->pic, a.ref, s->d_cur, s->c.me_mode,

@@ -321,6 +321,28 @@ int p64s_writer_consume(p64s_writer *w, size_t n) {
   return 0;
 }
 
+int p64s_writer_phase(const p64s_writer *w) { return w ? w->nacc : 0; }
+
+int p64s_write_bits(p64s_writer *w, const uint8_t *data, int64_t bits, int phase) {
+  if (!w || (!data && bits) || phase < 0 || phase > 7 || bits < phase)
+    return fail(P64GPU_E_INVALID, "write_bits: bad arguments");
+  if (w->ended) return fail(P64GPU_E_INVALID, "write after write_end");
+  if (phase != w->nacc) return fail(P64GPU_E_INVALID, "write_bits: phase %d, writer at %d", phase, w->nacc);
+  /* the coded picture continues the stream at bit `phase` of data[0] */
+  int64_t pos = phase;
+  while (pos < bits) {
+    const int n = (int)((bits - pos) < 16 ? (bits - pos) : 16);
+    const int64_t byte = pos >> 3;
+    uint32_t v = (uint32_t)data[byte] << 16;
+    if (pos + n > (byte + 1) * 8) v |= (uint32_t)data[byte + 1] << 8;
+    if (pos + n > (byte + 2) * 8) v |= data[byte + 2];
+    v = (v << (pos & 7)) >> (24 - n) & ((1u << n) - 1u);
+    put(w, n, v);
+    pos += n;
+  }
+  return w->oom ? fail(P64GPU_E_NOMEM, "writer: out of memory") : 0;
+}
+
 /* WritePictureHeader, marker.c:103-135 (non-VERSION_1_0): PSC, TR, PTYPE,
  * PSPARE for NTSC (p64.c:417-419), PEI = 0 */
 static void write_picture_header(p64s_writer *w, int format, int tr) {

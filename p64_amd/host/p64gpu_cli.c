@@ -22,7 +22,8 @@
  *   -z suffix               component file suffix (default .y4m with -y4m)
  *   -d                      decode
  *   -                       y4m from stdin
- * Additions: -full / -tss (FastBME vs the shipped StepBME), -D device.
+ * Additions: -full / -tss (FastBME vs the shipped StepBME), -D device,
+ * -hostvlc (entropy-code on the host instead of the GPU).
  *   -o                      program interpreter: program text on stdin (p64prog.h)
  *   (no -y4m)               raw component files <prefix><n>.Y/.U/.V per picture
  * Not supported here: -p parity (VERSION_1_0 only), -y floating-point reference
@@ -79,7 +80,7 @@ static int drain(p64s_writer *wr, FILE *o) {
 
 typedef struct {
   int format, y4m, first, last, skip, quant, sl, mode, device, decode, from_stdin;
-  int rate, file_size_bits, frame_rate, frame_rate_div, oracle;
+  int rate, file_size_bits, frame_rate, frame_rate_div, oracle, host_vlc;
   const char *prefix, *suffix, *stream;
 } opts;
 
@@ -156,6 +157,7 @@ static int encode(const opts *o) {
   cfg.frame_rate_div = o->frame_rate_div;
   cfg.device = o->device;
   cfg.program = g_prog;
+  cfg.host_vlc = o->host_vlc;
   p64seq *sq = NULL;
   if ((s = p64seq_open(&cfg, &sq))) return die("p64seq_open", s);
   p64seq_stats st;
@@ -328,6 +330,7 @@ int main(int argc, char **argv) {
     else if (!strcmp(a, "-z") && more) o.suffix = argv[++i];
     else if (!strcmp(a, "-d")) o.decode = 1;
     else if (!strcmp(a, "-o")) o.oracle = 1;
+    else if (!strcmp(a, "-hostvlc")) o.host_vlc = 1;
     else if (!strcmp(a, "-r") && more) o.rate = atoi(argv[++i]);
     else if (!strcmp(a, "-x") && more) o.file_size_bits = atoi(argv[++i]);
     else if (!strcmp(a, "-f") && more) {

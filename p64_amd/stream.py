@@ -182,7 +182,7 @@ class SeqConfig(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int) for n in
                 ("format", "me_mode", "search_limit", "quant", "rate", "file_size_bits",
                  "start_frame", "last_frame", "frame_skip", "frame_rate", "frame_rate_div",
-                 "device")] + [("program", ctypes.c_void_p)]
+                 "device")] + [("program", ctypes.c_void_p), ("host_vlc", ctypes.c_int)]
 
 
 class ProgSettings(ctypes.Structure):
@@ -243,7 +243,7 @@ class SequenceEncoder:
                  search_limit: int = 15, first: int = 0, last: int | None = None, skip: int = 1,
                  rate: int = 0, file_size_bits: int = 0, frame_rate: int = 30000,
                  frame_rate_div: int = 1001, device: int = 0, nframes: int | None = None,
-                 program: "Program | str | bytes | None" = None):
+                 program: "Program | str | bytes | None" = None, host_vlc: bool = False):
         L = lib()
         if program is not None and not isinstance(program, Program):
             program = Program(program)
@@ -267,6 +267,7 @@ class SequenceEncoder:
         c.last_frame = last if last is not None else first + skip * ((nframes or 1) - 1)
         c.frame_skip, c.frame_rate, c.frame_rate_div, c.device = skip, frame_rate, frame_rate_div, device
         c.program = program._h if program is not None else None
+        c.host_vlc = int(bool(host_vlc))
         self.width, self.height = width, height
         self._h = ctypes.c_void_p()
         _check(L.p64seq_open(ctypes.byref(c), ctypes.byref(self._h)))
@@ -315,13 +316,15 @@ class SequenceEncoder:
 
 def encode_sequence(frames, width: int, height: int, *, quant: int = 0, me_mode: int = 0,
                     search_limit: int = 15, first: int = 0, skip: int = 1, rate: int = 0,
-                    file_size_bits: int = 0, device: int = 0, program=None) -> bytes:
+                    file_size_bits: int = 0, device: int = 0, program=None,
+                    host_vlc: bool = False) -> bytes:
     """Encode frames[i] as frame first+i*skip: the reference CLI's `-a first
     -b last -k skip [-q] [-r|-x]` over the same pictures."""
     frames = list(frames)
     enc = SequenceEncoder(width, height, quant=quant, me_mode=me_mode, search_limit=search_limit,
                           first=first, skip=skip, rate=rate, file_size_bits=file_size_bits,
-                          device=device, nframes=len(frames), program=program)
+                          device=device, nframes=len(frames), program=program,
+                          host_vlc=host_vlc)
     try:
         for f in frames:
             if not enc.more():

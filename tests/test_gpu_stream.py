@@ -63,10 +63,11 @@ def test_cli_encode_byte_identical(p64, torch_dev, tmp_path, name):
     assert hashlib.sha256(data).hexdigest() == str(z["stream_sha256"])
 
 
+@pytest.mark.parametrize("host_vlc", [False, True])
 @pytest.mark.parametrize("name", ["qcif_tss", "cif_full31", "ntsc_tss", "qcif_rate",
                                   "cif_rate_full31", "qcif_filesize", "qcif_prog_mq_rate",
                                   "qcif_orate", "qcif_prog_words"])
-def test_python_encode_sequence_byte_identical(p64, torch_dev, name):
+def test_python_encode_sequence_byte_identical(p64, torch_dev, name, host_vlc):
     from p64_amd import stream
     z = load(f"seq_{name}.npz")
     w, h = int(z["width"]), int(z["height"])
@@ -76,7 +77,7 @@ def test_python_encode_sequence_byte_identical(p64, torch_dev, name):
     data = stream.encode_sequence(sequence_frames(p64, z), w, h, quant=g("q"),
                                   me_mode=1 if str(z["me"]) == "full" else 0,
                                   search_limit=g("sl"), rate=g("rate"), file_size_bits=g("filesize"),
-                                  program=program)
+                                  program=program, host_vlc=host_vlc)
     assert hashlib.sha256(data).hexdigest() == str(z["stream_sha256"])
 
 
