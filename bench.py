@@ -64,6 +64,10 @@ def parse():
     p.add_argument("--cpu-frames", type=int, default=120)
     p.add_argument("--no-verify", action="store_true")
     p.add_argument("--no-vlc", action="store_true", help="skip the encode+entropy-coding measurement")
+    p.add_argument("--feed", choices=("local", "root"), default="local",
+                   help="local: every rank generates its own sequences (default, no data-path "
+                        "collective); root: rank 0 holds all inputs, RCCL-scatters each step's "
+                        "pictures and gathers the levels/records back (the timed step includes both)")
     p.add_argument("--pmc-json", default=os.path.join(REPO, "profiles", "pmc_traffic.json"))
     return p.parse_args()
 
@@ -88,6 +92,33 @@ def max_over_ranks(value: float, world: int, device=None) -> float:
 def aggregate_rate(world: int, units_per_rank_step: int, steps: int, tmax: float) -> float:
     """Whole-job throughput: every rank's units over the slowest rank's time."""
     return world * units_per_rank_step * steps / tmax
+
+
+def scatter_pictures(world: int, rank: int, all_pics, recv):
+    """--feed root: rank 0 holds [world*S, pic] bytes; rank r receives rows
+    r*S..(r+1)*S-1 (its shard_seeds range) into recv [S, pic]."""
+    import torch.distributed as dist
+    if world == 1:
+        recv.copy_(all_pics)
+        return recv
+    chunks = list(all_pics.chunk(world)) if rank == 0 else None
+    dist.scatter(recv, scatter_list=chunks, src=0)
+    return recv
+
+
+def gather_outputs(world: int, rank: int, local, bufs):
+    """--feed root: every rank's output tensor is collected on rank 0 (bufs,
+    one per rank, rank 0 only)."""
+    import torch
+    import torch.distributed as dist
+    if world == 1:
+        if bufs is not None:
+            bufs[0].copy_(local)
+        return bufs
+    # as bytes: int16 levels are not an RCCL/NCCL (nor gloo) element type
+    byte = lambda t: t.contiguous().view(torch.uint8)  # noqa: E731
+    dist.gather(byte(local), gather_list=[byte(b) for b in bufs] if rank == 0 else None, dst=0)
+    return bufs
 
 
 # ---------------------------------------------------------------------------
@@ -193,7 +224,17 @@ def main():
     nslots = 1 + args.warmup + args.steps
     mode = p64_amd.ME_FULL if args.mode == "full" else p64_amd.ME_TSS
 
-    frames = p64_amd.synth_frames_device(w, h, seed0, S, 0, nslots)  # [slot][stream][pic]
+    root = args.feed == "root"
+    if root:  # rank 0 generates every rank's pictures; the others receive per step
+        all_frames = (p64_amd.synth_frames_device(w, h, 1, world * S, 0, nslots) if rank == 0
+                      else None)
+        frames = torch.empty((nslots, S, pic), dtype=torch.uint8, device="cuda")
+        coef_bufs = ([torch.empty((S, nmb, 6, 64), dtype=torch.int16, device="cuda")
+                      for _ in range(world)] if rank == 0 else None)
+        mb_bufs = ([torch.empty((S, nmb, 4), dtype=torch.int8, device="cuda") for _ in range(world)]
+                   if rank == 0 else None)
+    else:
+        frames = p64_amd.synth_frames_device(w, h, seed0, S, 0, nslots)  # [slot][stream][pic]
     rec = [torch.zeros(S * pic, dtype=torch.uint8, device="cuda") for _ in range(2)]
     li = torch.zeros(S * nmb, dtype=torch.uint8, device="cuda")
     out = p64_amd.FrameBatchOut(
@@ -202,9 +243,15 @@ def main():
         me=torch.empty((S, nmb, 7), dtype=torch.int32, device="cuda"))
 
     def step(t):
-        return p64_amd.encode_frames(frames[t].reshape(-1), rec[(t + 1) % 2], rec[t % 2], li,
-                                     width=w, height=h, intra=(t == 0), quant=args.quant,
-                                     me_mode=mode, search_limit=args.search_limit, out=out)
+        if root:
+            scatter_pictures(world, rank, all_frames[t] if rank == 0 else None, frames[t])
+        o = p64_amd.encode_frames(frames[t].reshape(-1), rec[(t + 1) % 2], rec[t % 2], li,
+                                  width=w, height=h, intra=(t == 0), quant=args.quant,
+                                  me_mode=mode, search_limit=args.search_limit, out=out)
+        if root:
+            gather_outputs(world, rank, out.coef, coef_bufs)
+            gather_outputs(world, rank, out.mb, mb_bufs)
+        return o
 
     for t in range(1 + args.warmup):  # intra picture + warmup, untimed
         step(t)
@@ -312,10 +359,12 @@ def main():
         "vs_baseline": None,
         "dtype": "u8",
         "data": "synthetic (seeded integer generator, generated on device)",
-        "config": {"workload": workload, "width": w, "height": h, "me": args.mode,
+        "config": {"workload": workload, "feed": args.feed, "width": w, "height": h, "me": args.mode,
                    "search_limit": args.search_limit, "quant": args.quant,
                    "sequences_per_gpu": S, "macroblocks_per_step_per_gpu": mbs_launch,
-                   "parallelism": f"dp{world} (independent sequences per GPU, no data-path collective)"},
+                   "parallelism": (f"dp{world} (independent sequences per GPU, no data-path collective)"
+                                   if not root else
+                                   f"dp{world} (rank 0 RCCL-scatters pictures, gathers levels + records)")},
         "roofline": {"bound": "hbm", "achieved": round(hbm_gbs, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(hbm_gbs / HBM_PEAK_GBS, 5),
                      "traffic": (pmc or {}).get("hbm_bytes_per_launch"),

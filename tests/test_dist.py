@@ -78,3 +78,61 @@ def test_two_rank_sharding_matches_single_process():
     assert digests == single
     assert tmax == 2.0
     assert np.isclose(rate, world * streams * 99 * 10 / 2.0)
+
+
+def _root_worker(rank, world, port, S, q):
+    """--feed root data path: rank 0 scatters every rank's pictures, each rank
+    encodes its shard (CPU oracle as the stand-in), rank 0 gathers the levels."""
+    import sys
+    sys.path.insert(0, REPO)
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import torch
+
+    import bench
+    import oracle
+    import p64_amd
+
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
+                            world_size=world)
+    w, h = 176, 144
+    pic = w * h * 3 // 2
+    all_pics = None
+    if rank == 0:
+        all_pics = torch.from_numpy(np.stack([p64_amd.synth_frame(1 + i, 0, w, h)
+                                              for i in range(world * S)]))
+    recv = torch.empty((S, pic), dtype=torch.uint8)
+    bench.scatter_pictures(world, rank, all_pics, recv)
+    seed0, _ = bench.shard_seeds(rank, S)
+    assert all(np.array_equal(recv[k].numpy(), p64_amd.synth_frame(seed0 + k, 0, w, h)) for k in range(S))
+    coef = torch.from_numpy(np.stack([
+        oracle.encode_frame(w, h, recv[k].numpy(), None, np.zeros(99, np.uint8), intra=True,
+                            quant=8)[0] for k in range(S)]))
+    bufs = [torch.empty_like(coef) for _ in range(world)] if rank == 0 else None
+    bench.gather_outputs(world, rank, coef, bufs)
+    if rank == 0:
+        q.put(torch.cat(bufs).numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_root_feed_scatter_gather():
+    import sys
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle
+    import p64_amd
+
+    world, S = 2, 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=_root_worker, args=(r, world, port, S, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for i in range(world * S):
+        exp = oracle.encode_frame(176, 144, p64_amd.synth_frame(1 + i, 0, 176, 144), None,
+                                  np.zeros(99, np.uint8), intra=True, quant=8)[0]
+        np.testing.assert_array_equal(got[i], exp)

@@ -6,7 +6,7 @@ F64 = re.compile(r'v_\w+_f64')
 s = open(sys.argv[1]).read()
 heads = [(m.start(), m.group(1)) for m in re.finditer(r'^(_Z\S+):\s*;\s*@', s, re.M)]
 for pos, name in heads:
-    end = s.find('s_endpgm', pos)
+    end = s.find('.Lfunc_end', pos)
     body = s[pos:end]
     ins = [l.split()[0] for l in body.splitlines() if l.startswith('\t') and l.strip() and not l.strip().startswith(('.', ';'))]
     valu = sum(1 for i in ins if i.startswith('v_'))
