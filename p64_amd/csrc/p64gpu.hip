@@ -135,16 +135,18 @@ __device__ __forceinline__ void fwd_row(const int x[8], int o[8]) {
   fwd8<N>(s, d, o);
 }
 
-// inverse butterfly (chendct.c:254-303 == 320-365)
-template <bool N>
+// inverse butterfly (chendct.c:254-303 == 320-365).  S scales the inputs: the
+// column pass takes them <<2 (chendct.c:235-243); every input only meets a
+// constant multiply, so the shift folds into the constants (same bits mod 2^32)
+template <bool N, int S = 1>
 __device__ __forceinline__ void inv8(const int x[8], int o[8]) {
-  const int p0 = ms9(kmul<N>(C7D16, x[1]) - kmul<N>(C1D16, x[7]));
-  const int p1 = ms9(kmul<N>(C3D16, x[5]) - kmul<N>(C5D16, x[3]));
-  const int p2 = ms9(kmul<N>(C3D16, x[3]) + kmul<N>(C5D16, x[5]));
-  const int p3 = ms9(kmul<N>(C1D16, x[1]) + kmul<N>(C7D16, x[7]));
-  const int q0 = ms9(kmul<N>(C1D4, x[0] + x[4])), q1 = ms9(kmul<N>(C1D4, x[0] - x[4]));
-  const int q2 = ms9(kmul<N>(C3D8, x[2]) - kmul<N>(C1D8, x[6]));
-  const int q3 = ms9(kmul<N>(C1D8, x[2]) + kmul<N>(C3D8, x[6]));
+  const int p0 = ms9(kmul<N>(S * C7D16, x[1]) - kmul<N>(S * C1D16, x[7]));
+  const int p1 = ms9(kmul<N>(S * C3D16, x[5]) - kmul<N>(S * C5D16, x[3]));
+  const int p2 = ms9(kmul<N>(S * C3D16, x[3]) + kmul<N>(S * C5D16, x[5]));
+  const int p3 = ms9(kmul<N>(S * C1D16, x[1]) + kmul<N>(S * C7D16, x[7]));
+  const int q0 = ms9(kmul<N>(S * C1D4, x[0] + x[4])), q1 = ms9(kmul<N>(S * C1D4, x[0] - x[4]));
+  const int q2 = ms9(kmul<N>(S * C3D8, x[2]) - kmul<N>(S * C1D8, x[6]));
+  const int q3 = ms9(kmul<N>(S * C1D8, x[2]) + kmul<N>(S * C3D8, x[6]));
   const int e0 = q0 + q3, e1 = q1 + q2, e2 = q1 - q2, e3 = q0 - q3;
   const int f0 = p0 + p1, f1 = p0 - p1, f2 = p3 - p2, f3 = p3 + p2;
   const int g1 = ms9(kmul<N>(C1D4, f2 - f1)), g2 = ms9(kmul<N>(C1D4, f2 + f1));
@@ -158,8 +160,11 @@ __device__ __forceinline__ void inv8(const int x[8], int o[8]) {
   o[7] = e0 - f3;
 }
 
-__device__ __forceinline__ int dct_final(int v) { return (v < 0 ? v - 4 : v + 4) / 8; }
-__device__ __forceinline__ int idct_final(int v) { return (v < 0 ? v - 8 : v + 8) / 16; }
+// (v < 0 ? v - h : v + h) / 2h with C truncation == (v + h - [v < 0]) >> k for
+// h = 2^(k-1): one add3 and two shifts instead of a select and a signed divide
+// (v >= 0: floor((v+h)/2^k); v < 0: ceil((v-h)/2^k) = floor((v+h-1)/2^k))
+__device__ __forceinline__ int dct_final(int v) { return (v + 4 + (v >> 31)) >> 3; }   // chendct.c:204
+__device__ __forceinline__ int idct_final(int v) { return (v + 8 + (v >> 31)) >> 4; }  // chendct.c:373
 __device__ __forceinline__ int clampi(int v, int lo, int hi) { return min(max(v, lo), hi); }
 
 // ---------------------------------------------------------------------------
@@ -764,11 +769,11 @@ __device__ __forceinline__ void forward_2d(MbLds &L, bool act, int b, int r, con
 // of block b's residual
 __device__ __forceinline__ void inverse_2d(MbLds &L, bool act, int b, int r, int res[8]) {
   int *B = L.blk + b * BLK_STRIDE;
-  {  // column pass: inputs <<2
+  {  // column pass: inputs <<2, folded into the constants
     int x[8], o[8];
 #pragma unroll
-    for (int k = 0; k < 8; k++) x[k] = B[k * ROW_STRIDE + r] << 2;
-    inv8<true>(x, o);
+    for (int k = 0; k < 8; k++) x[k] = B[k * ROW_STRIDE + r];
+    inv8<true, 4>(x, o);
     if (act) {
 #pragma unroll
       for (int k = 0; k < 8; k++) B[k * ROW_STRIDE + r] = o[k];
@@ -799,11 +804,12 @@ __device__ __forceinline__ int quantise(int raw, bool dc, bool qeven, unsigned m
   int v = dct_final(raw);
   v = clampi(v, dc ? -0x7fffffff : -1023, dc ? 2047 : 1023);
   const int c = qeven ? v + (v > 0 ? 1 : -1) : v;  // sign(0) = -1 (transform.c:285)
-  const int sm = c >> 31;
-  const unsigned a = (unsigned)((c ^ sm) - sm);
-  int l = (int)((mul_u24_s(a, magic) >> 20) ^ (unsigned)sm) - sm;  // trunc(c / 2q)
+  // trunc(c / 2q) = floor(c * magic / 2^20) for c >= 0 and the ceiling for
+  // c < 0: one signed 24-bit multiply, the ceiling as + (2^20 - 1) on negatives
+  const int t = __mul24(c, (int)magic);
+  int l = (t + (int)((unsigned)(c >> 31) >> 12)) >> 20;
   l = clampi(l, -127, 127);
-  if (INTRA) l = dc ? clampi(qdc_intra(v, 8), 1, 254) : l;
+  if (INTRA) l = dc ? clampi(dct_final(v), 1, 254) : l;  // (DC +- 4) / 8, transform.c:321-325
   return l;
 }
 // ICCITT(Flat)Quantize of one level (transform.c:359-451), branch-free: with

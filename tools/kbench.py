@@ -55,6 +55,14 @@ def main():
             search_limit=31, out=out), a.reps)
         res[f"me_only_{name}"] = timed(lambda: p64_amd.MotionEstimation(
             r0, fr[1].reshape(-1), w, h, mode=mode, search_limit=31), a.reps)
+    # decode-side reconstruction (config 5) of the inter picture just coded
+    qmb = torch.full((S * nmb,), 8, dtype=torch.uint8, device="cuda")
+    mask = torch.ones_like(qmb)
+    d1 = torch.empty_like(r1)
+    p64_amd.encode_frames(fr[1].reshape(-1), r0, r1, li, width=w, height=h, intra=False,
+                          me_mode=p64_amd.ME_FULL, search_limit=31, out=out)
+    res["decode_recon"] = timed(lambda: p64_amd.decode_recon(r0, d1, out.coef, out.mb, qmb, mask,
+                                                             width=w, height=h), a.reps)
     for k, (med, mn) in res.items():
         print(f"{k:16s} median {med:9.1f} us  min {mn:9.1f} us  {S * nmb / med * 1e6 / 1e6:8.1f} M MB/s")
 
