@@ -530,20 +530,18 @@ __device__ __forceinline__ void me_tss(const MbLds &L, int w, int h, int x0, int
     s += (uint32_t)__shfl_xor((int)s, 1);
     s += (uint32_t)__shfl_xor((int)s, 2);
     s += (uint32_t)__shfl_xor((int)s, 4);
-    const uint64_t okmask = __ballot(ok);
-    int nbx = bx, nby = by;
+    // the first least SAD in neighbour order: min of (SAD << 3 | k) over the
+    // eight group leaders, in scalar registers
+    const unsigned key = ok ? (s << 3) | (unsigned)k : 0xFFFFFFFFu;
+    unsigned m = 0xFFFFFFFFu;
 #pragma unroll
-    for (int j = 0; j < 8; j++) {
-      const unsigned sj = (unsigned)__shfl((int)s, 8 * j);
-      const int jj = j < 4 ? j : j + 1;
-      if (((okmask >> (8 * j)) & 1) && sj < bsad) {
-        bsad = sj;
-        nbx = bx + (jj % 3 - 1) * step;
-        nby = by + (jj / 3 - 1) * step;
-      }
+    for (int j = 0; j < 8; j++) m = min(m, (unsigned)__builtin_amdgcn_readlane((int)key, 8 * j));
+    if ((m >> 3) < bsad) {
+      bsad = m >> 3;
+      const int j = (int)(m & 7u), jj = j < 4 ? j : j + 1;
+      bx += (jj % 3 - 1) * step;
+      by += (jj / 3 - 1) * step;
     }
-    bx = nbx;
-    by = nby;
   }
   mx = bx;
   my = by;
