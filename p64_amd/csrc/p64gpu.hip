@@ -219,15 +219,32 @@ __host__ __device__ constexpr unsigned quant_magic(int q) { return (1u << 20) / 
 // ---------------------------------------------------------------------------
 // wave helpers
 
+// Wave reductions without the LDS crossbar: DPP folds each 16-lane row
+// (quad_perm [1,0,3,2], [2,3,0,1], row_half_mirror, row_mirror), then the four
+// row results are combined in scalar registers.  The result is wave-uniform.
+template <int CTRL>
+__device__ __forceinline__ unsigned dpp(unsigned v) {
+  return (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xf, 0xf, false);
+}
 __device__ __forceinline__ unsigned wave_min(unsigned v) {
-#pragma unroll
-  for (int m = 32; m >= 1; m >>= 1) v = min(v, (unsigned)__shfl_xor((int)v, m));
-  return v;
+  v = min(v, dpp<0xB1>(v));
+  v = min(v, dpp<0x4E>(v));
+  v = min(v, dpp<0x141>(v));
+  v = min(v, dpp<0x140>(v));
+  const unsigned a = (unsigned)__builtin_amdgcn_readlane((int)v, 0);
+  const unsigned b = (unsigned)__builtin_amdgcn_readlane((int)v, 16);
+  const unsigned c = (unsigned)__builtin_amdgcn_readlane((int)v, 32);
+  const unsigned d = (unsigned)__builtin_amdgcn_readlane((int)v, 48);
+  return min(min(a, b), min(c, d));
 }
 __device__ __forceinline__ int wave_sum(int v) {
-#pragma unroll
-  for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m);
-  return v;
+  unsigned u = (unsigned)v;
+  u += dpp<0xB1>(u);
+  u += dpp<0x4E>(u);
+  u += dpp<0x141>(u);
+  u += dpp<0x140>(u);
+  return __builtin_amdgcn_readlane((int)u, 0) + __builtin_amdgcn_readlane((int)u, 16) +
+         __builtin_amdgcn_readlane((int)u, 32) + __builtin_amdgcn_readlane((int)u, 48);
 }
 // wave-uniform by construction (results of wave reductions); saying so lets
 // hipcc use scalar registers and scalar branches for everything that follows
@@ -527,9 +544,9 @@ __device__ __forceinline__ void me_tss(const MbLds &L, int w, int h, int x0, int
         s = sad4(align4(a4, a3, sh), c[4 * rr + 3], s);
       }
     }
-    s += (uint32_t)__shfl_xor((int)s, 1);
-    s += (uint32_t)__shfl_xor((int)s, 2);
-    s += (uint32_t)__shfl_xor((int)s, 4);
+    s += dpp<0xB1>(s);   // sum over the lane's group of 8
+    s += dpp<0x4E>(s);
+    s += dpp<0x141>(s);
     // the first least SAD in neighbour order: min of (SAD << 3 | k) over the
     // eight group leaders, in scalar registers
     const unsigned key = ok ? (s << 3) | (unsigned)k : 0xFFFFFFFFu;
