@@ -246,6 +246,11 @@ __device__ __forceinline__ int wave_sum(int v) {
   return __builtin_amdgcn_readlane((int)u, 0) + __builtin_amdgcn_readlane((int)u, 16) +
          __builtin_amdgcn_readlane((int)u, 32) + __builtin_amdgcn_readlane((int)u, 48);
 }
+// a value the compiler cannot see through (nor hoist out of a loop)
+__device__ __forceinline__ int opaque(int v) {
+  asm volatile("" : "+v"(v));
+  return v;
+}
 // wave-uniform by construction (results of wave reductions); saying so lets
 // hipcc use scalar registers and scalar branches for everything that follows
 __device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
@@ -300,20 +305,39 @@ __device__ __forceinline__ Picture picture_at(const uint8_t *base, int w, int h)
   return p;
 }
 
-// stage the search window (zero outside the picture: such candidates are
-// never valid, me.c:212/292) and the current luma block
-__device__ __forceinline__ void stage_luma(MbLds &L, const uint8_t *ref_y, const uint8_t *cur_y,
-                                           int w, int h, int x0, int y0, int lane) {
-  for (int t = lane; t < WIN_ROWS * 3; t += 64) {
-    const int row = t / 3, seg = t - row * 3;
+// The search window (zero outside the picture: such candidates are never
+// valid, me.c:212/292) and the current luma block, fetched into registers
+// (LumaFetch) one macroblock ahead of its use, then stored to LDS (put_luma).
+constexpr int WIN_SEGS = WIN_ROWS * 3, WIN_NIT = (WIN_SEGS + 63) / 64;  // 16-byte segments
+struct LumaFetch {
+  uint4 v[WIN_NIT];
+  uint32_t c;
+};
+__device__ __forceinline__ LumaFetch fetch_luma(const uint8_t *ref_y, const uint8_t *cur_y, int w,
+                                                int h, int x0, int y0, int lane) {
+  // interior macroblocks (the whole window inside the picture) skip the
+  // per-segment bounds test
+  const bool inside = y0 >= WIN_OY && y0 - WIN_OY + WIN_ROWS <= h && x0 >= WIN_OX &&
+                      x0 - WIN_OX + WIN_BYTES <= w;
+  LumaFetch f;
+#pragma unroll
+  for (int i = 0; i < WIN_NIT; i++) {
+    const int t = lane + 64 * i, row = t / 3, seg = t - row * 3;
     const int gy = y0 - WIN_OY + row, gx = x0 - WIN_OX + seg * 16;
-    uint4 v = make_uint4(0, 0, 0, 0);
-    if (gy >= 0 && gy < h && gx >= 0 && gx < w)
-      v = *reinterpret_cast<const uint4 *>(ref_y + gy * w + gx);
-    reinterpret_cast<uint4 *>(L.win)[t] = v;
+    f.v[i] = make_uint4(0, 0, 0, 0);
+    if (t < WIN_SEGS && (inside || (gy >= 0 && gy < h && gx >= 0 && gx < w)))
+      f.v[i] = *reinterpret_cast<const uint4 *>(ref_y + gy * w + gx);
   }
-  L.cur[lane] = *reinterpret_cast<const uint32_t *>(cur_y + (y0 + (lane >> 2)) * w + x0 +
-                                                    4 * (lane & 3));
+  f.c = *reinterpret_cast<const uint32_t *>(cur_y + (y0 + (lane >> 2)) * w + x0 + 4 * (lane & 3));
+  return f;
+}
+__device__ __forceinline__ void put_luma(MbLds &L, const LumaFetch &f, int lane) {
+#pragma unroll
+  for (int i = 0; i < WIN_NIT; i++) {
+    const int t = lane + 64 * i;
+    if (t < WIN_SEGS) reinterpret_cast<uint4 *>(L.win)[t] = f.v[i];
+  }
+  L.cur[lane] = f.c;
 }
 
 struct MeOut {
@@ -339,9 +363,10 @@ __device__ __forceinline__ int sad_zero(const MbLds &L, int lane) {
 //     its full SAD, and SAD(0,0), bound the answer: T = min(SAD(c*), SAD(0,0))
 //  3. a candidate whose partial sum already exceeds T can neither win nor tie
 //     (its SAD only grows), so rows MP..15 are summed only for the survivors:
-//     compacted into an LDS list and finished one per lane when there are few
-//     (textured content: a handful), densely otherwise (flat content, where
-//     nothing prunes)
+//     compacted into an LDS list and finished 16 lanes per candidate when at
+//     most 16 survive, one per lane up to ME_LIST_MAX, densely beyond (flat
+//     content, where little prunes).  A second pruning after row 11 was
+//     measured and bought nothing: this phase is not VALU-bound.
 //  4. the winner is the least (SAD, scan order) key among c*, the survivors and
 //     (0,0), which wins ties because FastBME evaluates it first (me.c:203, 220).
 // The result is identical to the exhaustive search for every input.
@@ -396,6 +421,124 @@ __device__ __forceinline__ void load_cur_rows(const uint8_t *cur_blk, int w, uin
   }
 }
 
+// survivors' keys (partial << 11 | 1 + scan order) of the dense sums into the
+// LDS list, in lane-major order
+__device__ __forceinline__ void compact_keys(const uint32_t acc[15], unsigned T, unsigned base,
+                                             int lane, uint32_t *list) {
+  int pos = 0;
+#pragma unroll
+  for (int d = 0; d < 15; d++) {
+    const bool sv = acc[d] <= T;
+    const uint64_t bl = __ballot(sv);
+    if (bl) {
+      const int idx = pos + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bl >> 32),
+                                                           __builtin_amdgcn_mbcnt_lo((uint32_t)bl, 0u));
+      if (sv) list[idx] = (acc[d] << 11) + base + d;
+      pos += __popcll(bl);
+    }
+  }
+}
+
+// dense rows [R0, R1) in two chunks, each with its current rows in scalar
+// registers only while it runs (the window rows are aligned twice)
+template <int R0, int R1>
+__device__ __forceinline__ void full_rows_chunked(const uint32_t *wrow, int sh, const uint8_t *cur_blk,
+                                                  int w, uint32_t *cs, uint32_t *acc) {
+  constexpr int RH = (R0 + R1) / 2;
+  load_cur_rows<R0, RH - R0>(cur_blk, w, cs);
+  full_rows<R0, RH, R0, RH + 14>(wrow, sh, cs, acc);
+  load_cur_rows<RH, R1 - RH>(cur_blk, w, cs);
+  full_rows<RH, R1, RH, R1 + 14>(wrow, sh, cs, acc);
+}
+
+__device__ __forceinline__ void key_pos(unsigned key, int &cdx, int &cdy) {
+  const int ord = (int)(key & 2047u) - 1;
+  cdx = ord / 30 - 15;
+  cdy = ord % 30 - 15;
+}
+
+// rows [R0, R1) of the n listed candidates, one per lane.  R1 == 16: the
+// keys are complete and folded into bk; otherwise the candidates still <= T
+// are compacted in place (a chunk's reads precede its writes) and counted.
+template <int R0, int R1>
+__device__ __forceinline__ int list_rows(const MbLds &L, uint32_t *list, int n, unsigned T, int lane,
+                                         unsigned &bk) {
+  int pos = 0;
+  for (int c0 = 0; c0 < n; c0 += 64) {
+    const bool live = c0 + lane < n;
+    unsigned key = live ? list[c0 + lane] : 0xFFFFFFFFu;
+    if (live) {
+      int cdx, cdy;
+      key_pos(key, cdx, cdy);
+      const int cb = WIN_OX + cdx, csh = cb & 3;
+      const uint32_t *p0 = L.win + (WIN_OY + cdy + R0) * WIN_WORDS + (cb >> 2);
+      uint32_t a = 0;
+#pragma unroll
+      for (int r = R0; r < R1; r++) {
+        const uint32_t *p = p0 + (r - R0) * WIN_WORDS;
+        const uint32_t a0 = p[0], a1 = p[1], a2 = p[2], a3 = p[3], a4 = p[4];
+        // LDS broadcast, re-read per chunk (opaque index: not hoisted out of
+        // the loop into live registers)
+        const uint4 c = reinterpret_cast<const uint4 *>(L.cur)[opaque(r)];
+        a = sad4(align4(a1, a0, csh), c.x, a);
+        a = sad4(align4(a2, a1, csh), c.y, a);
+        a = sad4(align4(a3, a2, csh), c.z, a);
+        a = sad4(align4(a4, a3, csh), c.w, a);
+      }
+      key += a << 11;
+    }
+    if (R1 == 16) {
+      bk = min(bk, key);
+    } else {
+      const bool sv = live && (key >> 11) <= T;
+      const uint64_t bl = __ballot(sv);
+      const int idx = pos + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bl >> 32),
+                                                           __builtin_amdgcn_mbcnt_lo((uint32_t)bl, 0u));
+      if (sv) list[idx] = key;
+      pos += __popcll(bl);
+    }
+  }
+  if (R1 != 16) __syncthreads();
+  return uni(pos);
+}
+
+// rows [R0, 16) of n <= 16 listed candidates, four at a time, 16 lanes each:
+// lane (d, rg) sums dword d of rows R0+rg, R0+rg+4, ...; returns the least key
+template <int R0>
+__device__ __forceinline__ unsigned finish_16(const MbLds &L, const uint32_t *list, int n, int lane) {
+  constexpr int NT = (16 - R0 + 3) / 4;
+  const int d = lane & 3, rg = (lane >> 2) & 3;
+  uint32_t cw[NT];
+#pragma unroll
+  for (int t = 0; t < NT; t++) {
+    const int r = R0 + rg + 4 * t;
+    cw[t] = r < 16 ? L.cur[4 * r + d] : 0u;
+  }
+  unsigned bk = 0xFFFFFFFFu;
+  for (int c0 = 0; c0 < n; c0 += 4) {
+    const int j = c0 + (lane >> 4);
+    const unsigned key = j < n ? list[j] : 0xFFFFFFFFu;
+    int cdx, cdy;
+    key_pos(key, cdx, cdy);
+    const int cb = WIN_OX + cdx, csh = cb & 3;
+    const uint32_t *p0 = L.win + (WIN_OY + cdy + R0 + rg) * WIN_WORDS + (cb >> 2) + d;
+    uint32_t a = 0;
+#pragma unroll
+    for (int t = 0; t < NT; t++) {
+      if (R0 + rg + 4 * t < 16) {
+        const uint32_t *p = p0 + 4 * t * WIN_WORDS;
+        a = sad4(align4(p[1], p[0], csh), cw[t], a);
+      }
+    }
+    a += dpp<0xB1>(a);
+    a += dpp<0x4E>(a);
+    a += dpp<0x141>(a);
+    a += dpp<0x140>(a);
+    if (j < n) bk = min(bk, key + (a << 11));
+  }
+  return wave_min(bk);
+}
+
 __device__ __forceinline__ void me_full(MbLds &L, const uint8_t *cur_blk, int w, int h, int x0,
                                         int y0, int sl, int lane, int sad0, int &mx, int &my,
                                         int &best) {
@@ -429,7 +572,6 @@ __device__ __forceinline__ void me_full(MbLds &L, const uint8_t *cur_blk, int w,
   load_cur_rows<0, MP>(cur_blk, w, cs);
   // 1. rows 0..MP-1
   full_rows<0, MP, 0, MP + 14>(wrow, sh, cs, acc);
-  load_cur_rows<MP, 16 - MP>(cur_blk, w, cs);
 
   // key = SUM<<11 | (1 + scan order); scan order (dx+15)*30+(dy+15)
   const unsigned base = (unsigned)(dxi * 30 + 15 * half + 1);
@@ -451,6 +593,7 @@ __device__ __forceinline__ void me_full(MbLds &L, const uint8_t *cur_blk, int w,
   const unsigned T = min(ckey >> 11, (unsigned)sad0);
 
   // 3. survivors: partial <= T (c* itself included: one more list entry is free)
+  uint32_t *list = reinterpret_cast<uint32_t *>(L.blk);  // DCT scratch, free during the search
   int nsurv = 0;
 #pragma unroll
   for (int d = 0; d < 15; d++) nsurv += __popcll(__ballot(acc[d] <= T));
@@ -458,46 +601,16 @@ __device__ __forceinline__ void me_full(MbLds &L, const uint8_t *cur_blk, int w,
 
   unsigned bk = 0xFFFFFFFFu;
   if (nsurv > ME_LIST_MAX) {  // little pruned: finish every candidate densely
-    full_rows<MP, 16, MP, 30>(wrow, sh, cs, acc);
+    full_rows_chunked<MP, 16>(wrow, sh, cur_blk, w, cs, acc);
 #pragma unroll
     for (int d = 0; d < 15; d++) bk = min(bk, (acc[d] << 11) + base + d);
   } else {
-    // compact the survivors' partial keys into LDS (the DCT scratch is free
-    // during the search), then finish them 64 at a time, one per lane
-    uint32_t *list = reinterpret_cast<uint32_t *>(L.blk);
-    int pos = 0;
-#pragma unroll
-    for (int d = 0; d < 15; d++) {
-      const bool sv = acc[d] <= T;
-      const uint64_t bl = __ballot(sv);
-      if (bl) {
-        const int idx = pos + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bl >> 32),
-                                                             __builtin_amdgcn_mbcnt_lo((uint32_t)bl, 0u));
-        if (sv) list[idx] = (acc[d] << 11) + base + d;
-        pos += __popcll(bl);
-      }
-    }
+    compact_keys(acc, T, base, lane, list);
     __syncthreads();
-    for (int c0 = 0; c0 < nsurv; c0 += 64) {
-      if (c0 + lane < nsurv) {
-        const unsigned pk_i = list[c0 + lane];
-        const int ord = (int)(pk_i & 2047u) - 1;
-        const int cdx = ord / 30 - 15, cdy = ord % 30 - 15;
-        const int cb = WIN_OX + cdx, csh = cb & 3;
-        const uint32_t *p0 = L.win + (WIN_OY + cdy + MP) * WIN_WORDS + (cb >> 2);
-        uint32_t a = 0;
-#pragma unroll
-        for (int r = MP; r < 16; r++) {
-          const uint32_t *p = p0 + (r - MP) * WIN_WORDS;
-          const uint32_t a0 = p[0], a1 = p[1], a2 = p[2], a3 = p[3], a4 = p[4];
-          a = sad4(align4(a1, a0, csh), cs[4 * r + 0], a);
-          a = sad4(align4(a2, a1, csh), cs[4 * r + 1], a);
-          a = sad4(align4(a3, a2, csh), cs[4 * r + 2], a);
-          a = sad4(align4(a4, a3, csh), cs[4 * r + 3], a);
-        }
-        bk = min(bk, pk_i + (a << 11));
-      }
-    }
+    if (nsurv <= 16)
+      bk = finish_16<MP>(L, list, nsurv, lane);  // the common case on textured content
+    else
+      list_rows<MP, 16>(L, list, nsurv, T, lane, bk);
   }
 
   // 4. winner
@@ -626,15 +739,11 @@ __device__ __forceinline__ void unpack8(uint32_t lo, uint32_t hi, int v[8]) {
     v[4 + k] = (hi >> (8 * k)) & 255;
   }
 }
-// Values are taken through an empty asm first: on ROCm 7.2 hipcc fuses
+// Values are taken through an empty asm (opaque) first: on ROCm 7.2 hipcc fuses
 // "(x >> 4) clamped to 0..255, packed" into gfx950's v_ashr_pk_u8_i32 and then
 // ORs the packed pair into a dword whose upper half it assumes is zero, which
 // corrupted byte 3 on the hardware (tools/repro_ashr_pk.hip); the barrier keeps
 // the clamp and the pack as separate instructions.
-__device__ __forceinline__ int opaque(int v) {
-  asm volatile("" : "+v"(v));
-  return v;
-}
 __device__ __forceinline__ uint2 pack8(const int in[8]) {
   int v[8];
 #pragma unroll
@@ -865,24 +974,38 @@ __device__ __forceinline__ CbpOut cbp_decide(const int lev[6]) {
 // zigzag -> CBP -> IQ -> IDCT -> reconstruction, one wave per macroblock.
 // MODE: 0 intra picture, 1 TSS, 2 FULL.
 
+// per-macroblock inputs, all loads in flight before the first use
+struct MbFetch {
+  LumaFetch luma;  // MODE != 0: search window and current luma
+  uint2 crow;      // the lane's row of its block in the current picture
+};
 template <int MODE>
-__global__ __launch_bounds__(64) void k_encode(p64gpu_encode_args a, const int32_t *mb_list) {
-  __shared__ MbLds L;
-  const int lane = threadIdx.x;
+__device__ __forceinline__ MbFetch fetch_mb(const p64gpu_encode_args &a, const uint8_t *cur_all,
+                                            unsigned gid, int lane) {
   const int w = a.width, h = a.height, mbw = w >> 4, nmb = mbw * (h >> 4);
-  int fi, mb;
-  if (mb_list) {  // one picture, listed macroblocks only (p64gpu_encode_mb_list)
-    fi = 0;
-    mb = mb_list[blockIdx.x];
-    if (mb < 0 || mb >= nmb) return;  // whole workgroup
-  } else {
-    const unsigned gid = xcd_remap(blockIdx.x, gridDim.x);
-    fi = (int)(gid / (unsigned)nmb);
-    mb = (int)(gid - (unsigned)fi * nmb);
-  }
+  const int fi = (int)(gid / (unsigned)nmb), mb = (int)(gid - (unsigned)fi * nmb);
+  const int mbx = mb % mbw, mby = mb / mbw;
+  const Picture cur = picture_at(cur_all + (size_t)fi * a.frame_stride, w, h);
+  const int b = min(lane >> 3, 5), r = lane & 7;
+  const BlockGeom g = block_geom(b, mbx, mby);
+  const int pw = g.plane ? w >> 1 : w;
+  const uint8_t *cplane = g.plane == 0 ? cur.y : (g.plane == 1 ? cur.u : cur.v);
+  MbFetch f;
+  f.crow = *reinterpret_cast<const uint2 *>(cplane + (g.y + r) * pw + g.x);
+  if (MODE != 0)
+    f.luma = fetch_luma(a.ref + (size_t)fi * a.frame_stride, cur.y, w, h, 16 * mbx, 16 * mby, lane);
+  return f;
+}
+
+// one macroblock, its luma already in L (MODE != 0)
+template <int MODE>
+__device__ __forceinline__ void encode_mb(const p64gpu_encode_args &a, const uint8_t *cur_all,
+                                          MbLds &L, int lane, unsigned gid, uint2 crow) {
+  const int w = a.width, h = a.height, mbw = w >> 4, nmb = mbw * (h >> 4);
+  const int fi = (int)(gid / (unsigned)nmb), mb = (int)(gid - (unsigned)fi * nmb);
   const int mbx = mb % mbw, mby = mb / mbw, x0 = 16 * mbx, y0 = 16 * mby;
   const size_t gmb = (size_t)fi * nmb + mb;
-  const Picture cur = picture_at(a.cur + (size_t)fi * a.frame_stride, w, h);
+  const Picture cur = picture_at(cur_all + (size_t)fi * a.frame_stride, w, h);
   const Picture ref = picture_at(a.ref + (size_t)fi * a.frame_stride, w, h);
   uint8_t *rec = a.recon + (size_t)fi * a.frame_stride;
 
@@ -891,12 +1014,9 @@ __global__ __launch_bounds__(64) void k_encode(p64gpu_encode_args a, const int32
   const bool act = lane < 48;
   const BlockGeom g = block_geom(b, mbx, mby);
   const int pw = g.plane ? w >> 1 : w;
-  const uint8_t *cplane = g.plane == 0 ? cur.y : (g.plane == 1 ? cur.u : cur.v);
-  const uint2 crow = *reinterpret_cast<const uint2 *>(cplane + (g.y + r) * pw + g.x);
 
   int mt = 0, mvx = 0, mvy = 0;
   if (MODE != 0) {
-    stage_luma(L, ref.y, cur.y, w, h, x0, y0, lane);
     __syncthreads();
     const MeOut me = motion_estimate<MODE>(L, cur.y, w, h, x0, y0, a.search_limit, lane);
     if (a.me && lane == 0) {
@@ -1001,9 +1121,29 @@ __global__ __launch_bounds__(64) void k_encode(p64gpu_encode_args a, const int32
   }
 }
 
+#ifndef ENCODE_WAVES_PER_SIMD
+#define ENCODE_WAVES_PER_SIMD 1
+#endif
+template <int MODE>
+__global__ __launch_bounds__(64, ENCODE_WAVES_PER_SIMD) void k_encode(p64gpu_encode_args a, const int32_t *mb_list) {
+  __shared__ MbLds L;
+  const int lane = threadIdx.x;
+  unsigned gid;
+  if (mb_list) {  // one picture, listed macroblocks only (p64gpu_encode_mb_list)
+    const int mb = mb_list[blockIdx.x];
+    if (mb < 0 || mb >= (a.width >> 4) * (a.height >> 4)) return;  // whole workgroup
+    gid = (unsigned)mb;
+  } else {
+    gid = xcd_remap(blockIdx.x, gridDim.x);
+  }
+  const MbFetch f = fetch_mb<MODE>(a, a.cur, gid, lane);
+  if (MODE != 0) put_luma(L, f.luma, lane);
+  encode_mb<MODE>(a, a.cur, L, lane, gid, f.crow);
+}
+
 // ME only (MotionEstimation me.c:340-363 over a batch of luma planes)
 template <int MODE>
-__global__ __launch_bounds__(64) void k_motion(int w, int h, int64_t stride, const uint8_t *ref_y,
+__global__ __launch_bounds__(64, ENCODE_WAVES_PER_SIMD) void k_motion(int w, int h, int64_t stride, const uint8_t *ref_y,
                                                const uint8_t *cur_y, int sl, p64_me_rec *out) {
   __shared__ MbLds L;
   const int lane = threadIdx.x;
@@ -1011,7 +1151,8 @@ __global__ __launch_bounds__(64) void k_motion(int w, int h, int64_t stride, con
   const unsigned gid = xcd_remap(blockIdx.x, gridDim.x);
   const int fi = (int)(gid / (unsigned)nmb), mb = (int)(gid - (unsigned)fi * nmb);
   const int x0 = 16 * (mb % mbw), y0 = 16 * (mb / mbw);
-  stage_luma(L, ref_y + (size_t)fi * stride, cur_y + (size_t)fi * stride, w, h, x0, y0, lane);
+  put_luma(L, fetch_luma(ref_y + (size_t)fi * stride, cur_y + (size_t)fi * stride, w, h, x0, y0, lane),
+           lane);
   __syncthreads();
   const MeOut me = motion_estimate<MODE>(L, cur_y + (size_t)fi * stride, w, h, x0, y0, sl, lane);
   if (lane == 0) {
@@ -1023,7 +1164,7 @@ __global__ __launch_bounds__(64) void k_motion(int w, int h, int64_t stride, con
     o.var = me.var;
     o.varor = me.varor;
     o.mwor = me.mwor;
-    out[(size_t)fi * nmb + mb] = o;
+    out[gid] = o;
   }
 }
 
