@@ -170,35 +170,27 @@ __device__ __forceinline__ int clampi(int v, int lo, int hi) { return min(max(v,
 // ---------------------------------------------------------------------------
 // quantisers (transform.c:271-451, non-VERSION_1_0)
 
-// Truncating c / d for d = 2q.  In the fused kernels |c| <= 2048 (BoundDctMatrix
-// plus the +-1 of even q), where the 20-bit reciprocal is exact for every
-// d <= 62 (tests/test_quant_magic.py checks it exhaustively); the block-op path
+// Truncating c / 2q.  In the fused kernels |c| <= 2048 (BoundDctMatrix plus
+// the +-1 of even q): there (int)(c * r) in binary32, r = 1/(2q) rounded and
+// then raised one ulp, equals C's c / (2q) for every q = 1..31 (|c| <= 4096:
+// tests/test_quant_recip.py checks it exhaustively); the block-op path
 // handles arbitrary int32 with a true division.
-// a * m for a, m < 2^24 on the full-rate 24-bit multiplier.  The backend only
-// selects v_mul_u32_u24 when it can prove the operand widths itself and
-// otherwise falls back to the quarter-rate v_mul_lo_u32.
-__device__ __forceinline__ unsigned mul_u24_s(unsigned a, unsigned m_uniform) {
-  unsigned r;
-  asm("v_mul_u32_u24 %0, %1, %2" : "=v"(r) : "s"(m_uniform), "v"(a));
-  return r;
+struct QuantRecip {
+  float r[32];
+};
+constexpr QuantRecip make_quant_recip() {
+  QuantRecip t{};
+  for (int q = 1; q < 32; q++)
+    t.r[q] = __builtin_bit_cast(float, __builtin_bit_cast(uint32_t, 1.0f / (float)(2 * q)) + 1u);
+  return t;
 }
-
-template <bool BOUNDED>
-__device__ __forceinline__ int div_trunc(int c, int d, unsigned magic) {
-  if (BOUNDED) {
-    const unsigned a = (unsigned)abs(c);
-    const int qq = (int)(mul_u24_s(a, magic) >> 20);
-    return c < 0 ? -qq : qq;
-  }
-  return c / d;
-}
+__constant__ QuantRecip c_qrecip = make_quant_recip();
 
 // H.261 level: odd q -> c/(2q); even q -> (c + sign(c))/(2q), sign(0) = -1
 // (transform.c:283-306, 339-347)
-template <bool BOUNDED>
-__device__ __forceinline__ int qlevel(int c, int q, unsigned magic) {
+__device__ __forceinline__ int qlevel(int c, int q) {
   if (!(q & 1)) c += c > 0 ? 1 : -1;
-  return div_trunc<BOUNDED>(c, 2 * q, magic);
+  return c / (2 * q);
 }
 // intra DC (transform.c:321-325): (DC +- dcq/2) / dcq, sign by DC > 0
 __device__ __forceinline__ int qdc_intra(int c, int dcq) {
@@ -214,7 +206,6 @@ __device__ __forceinline__ int rlevel(int l, int q) {
   return v;
 }
 
-__host__ __device__ constexpr unsigned quant_magic(int q) { return (1u << 20) / (2u * (unsigned)q) + 1u; }
 
 // ---------------------------------------------------------------------------
 // wave helpers
@@ -715,15 +706,20 @@ __device__ __forceinline__ MeOut motion_estimate(MbLds &L, const uint8_t *cur_y,
   return o;
 }
 
-// MTYPE decision (p64.c:734-756) in binary64, as written.
+// MTYPE decision (p64.c:734-756).  xv = sad0/256 and yv = sad/256 are exact
+// in binary64, so xv < 1, xv < 3 and yv > xv*0.5 are integer tests; yv >
+// xv/1.1 is 11 sad > 10 sad0 unless the two are equal (the double quotient's
+// error, < 2e-11, cannot cross a gap of 1/11 otherwise), and on equality the
+// rounded quotient decides, computed as written.
 __device__ __forceinline__ int decide_mtype(const MeOut &m) {
-  double xv = (double)m.sad0, yv = (double)m.sad;
-  xv = xv / 256;
-  yv = yv / 256;
   if (m.var < 64 || m.varor > m.var) {
-    if (xv < 1.0 || (xv < 3.0 && yv > xv * 0.5) || yv > xv / 1.1) return 2;
-    if (m.var < 6.0) return 5;
-    return 8;
+    bool inter = m.sad0 < 256 || (m.sad0 < 768 && 2 * m.sad > m.sad0);
+    if (!inter) {
+      const int t = 11 * m.sad - 10 * m.sad0;
+      inter = t != 0 ? t > 0 : (double)m.sad / 256 > ((double)m.sad0 / 256) / 1.1;
+    }
+    if (inter) return 2;
+    return m.var < 6 ? 5 : 8;  // VAR < D_FILTERTHRESHOLD (6.0)
   }
   return 0;
 }
@@ -924,14 +920,11 @@ __device__ __forceinline__ void blk_put(MbLds &L, int k, int e, int v) {
 // coefficient (transform.c:271-350, 460-537), branch-free.  dc: lane holds the
 // DC coefficient; INTRA selects the flat DC quantiser.
 template <bool INTRA>
-__device__ __forceinline__ int quantise(int raw, bool dc, bool qeven, unsigned magic) {
+__device__ __forceinline__ int quantise(int raw, bool dc, bool qeven, float rq) {
   int v = dct_final(raw);
   v = clampi(v, dc ? -0x7fffffff : -1023, dc ? 2047 : 1023);
   const int c = qeven ? v + (v > 0 ? 1 : -1) : v;  // sign(0) = -1 (transform.c:285)
-  // trunc(c / 2q) = floor(c * magic / 2^20) for c >= 0 and the ceiling for
-  // c < 0: one signed 24-bit multiply, the ceiling as + (2^20 - 1) on negatives
-  const int t = __mul24(c, (int)magic);
-  int l = (t + (int)((unsigned)(c >> 31) >> 12)) >> 20;
+  int l = (int)((float)c * rq);                     // trunc(c / 2q), see c_qrecip
   l = clampi(l, -127, 127);
   if (INTRA) l = dc ? clampi(dct_final(v), 1, 254) : l;  // (DC +- 4) / 8, transform.c:321-325
   return l;
@@ -1042,7 +1035,7 @@ __device__ __forceinline__ void encode_mb(const p64gpu_encode_args &a, const uin
   if (li > 131) mt = 0;  // SEQUENCE_INTRA_THRESHOLD (p64.c:159, 772)
   mt = uni(mt);
   const int q = uni(a.quant_mb ? a.quant_mb[gmb] : a.quant);
-  const unsigned magic = quant_magic(q);
+  const float rq = c_qrecip.r[q];
   const bool qeven = !(q & 1);
 
   int pred[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -1064,10 +1057,10 @@ __device__ __forceinline__ void encode_mb(const p64gpu_encode_args &a, const uin
     forward_2d(L, act, b, r, res);
     if (mt_intra(mt)) {
 #pragma unroll
-      for (int k = 0; k < 6; k++) lev[k] = quantise<true>(blk_at(L, k, e), dc, qeven, magic);
+      for (int k = 0; k < 6; k++) lev[k] = quantise<true>(blk_at(L, k, e), dc, qeven, rq);
     } else {
 #pragma unroll
-      for (int k = 0; k < 6; k++) lev[k] = quantise<false>(blk_at(L, k, e), dc, qeven, magic);
+      for (int k = 0; k < 6; k++) lev[k] = quantise<false>(blk_at(L, k, e), dc, qeven, rq);
     }
   }
   int cbp = 0x3f;
@@ -1256,11 +1249,11 @@ __global__ void k_block_op(int op, const int32_t *in, int32_t *out, int64_t nblo
     }
     case P64GPU_OP_QUANT_INTRA:
       m[0] = qdc_intra(m[0], dcq);
-      for (int n = 1; n < 64; n++) m[n] = qlevel<false>(m[n], acq, 0);
+      for (int n = 1; n < 64; n++) m[n] = qlevel(m[n], acq);
       break;
     case P64GPU_OP_QUANT_INTER:
-      m[0] = qlevel<false>(m[0], dcq, 0);
-      for (int n = 1; n < 64; n++) m[n] = qlevel<false>(m[n], acq, 0);
+      m[0] = qlevel(m[0], dcq);
+      for (int n = 1; n < 64; n++) m[n] = qlevel(m[n], acq);
       break;
     case P64GPU_OP_IQUANT_INTRA:
       m[0] = m[0] * dcq;
