@@ -166,6 +166,15 @@ __device__ __forceinline__ void inv8(const int x[8], int o[8]) {
 __device__ __forceinline__ int dct_final(int v) { return (v + 4 + (v >> 31)) >> 3; }   // chendct.c:204
 __device__ __forceinline__ int idct_final(int v) { return (v + 8 + (v >> 31)) >> 4; }  // chendct.c:373
 __device__ __forceinline__ int clampi(int v, int lo, int hi) { return min(max(v, lo), hi); }
+// Per-lane row offsets on the 24-bit multiplier: both factors are below 2^23
+// (pictures are at most 4096 x 4096, check_geometry) and the product below
+// 2^25; a plain int product of two vector values is the quarter-rate v_mul_lo.
+__device__ __forceinline__ int mul24(int a, int b) { return __mul24(a, b); }
+// byte offset of plane 0/1/2 in a 4:2:0 picture (selects of uniform values)
+__device__ __forceinline__ int plane_offset(int plane, int w, int h) {
+  const int wh = w * h;
+  return plane == 0 ? 0 : (plane == 1 ? wh : wh + (wh >> 2));
+}
 
 // ---------------------------------------------------------------------------
 // quantisers (transform.c:271-451, non-VERSION_1_0)
@@ -317,9 +326,9 @@ __device__ __forceinline__ LumaFetch fetch_luma(const uint8_t *ref_y, const uint
     const int gy = y0 - WIN_OY + row, gx = x0 - WIN_OX + seg * 16;
     f.v[i] = make_uint4(0, 0, 0, 0);
     if (t < WIN_SEGS && (inside || (gy >= 0 && gy < h && gx >= 0 && gx < w)))
-      f.v[i] = *reinterpret_cast<const uint4 *>(ref_y + gy * w + gx);
+      f.v[i] = *reinterpret_cast<const uint4 *>(ref_y + (uint32_t)(mul24(gy, w) + gx));
   }
-  f.c = *reinterpret_cast<const uint32_t *>(cur_y + (y0 + (lane >> 2)) * w + x0 + 4 * (lane & 3));
+  f.c = *reinterpret_cast<const uint32_t *>(cur_y + (uint32_t)(mul24(y0 + (lane >> 2), w) + x0 + 4 * (lane & 3)));
   return f;
 }
 __device__ __forceinline__ void put_luma(MbLds &L, const LumaFetch &f, int lane) {
@@ -803,7 +812,7 @@ __device__ __forceinline__ void stage_chroma(MbLds &L, const Picture &ref, int w
   const bool mf = mt_mf(mt);
   const int ox = 8 * mbx + (mf ? mvx / 2 : 0), oy = 8 * mby + (mf ? mvy / 2 : 0);
   const int pl = lane >> 5, row = (lane >> 2) & 7, c2 = (lane & 3) * 2;
-  const uint8_t *src = (pl ? ref.v : ref.u) + (oy + row) * cw + ox + c2;
+  const uint8_t *src = (pl ? ref.v : ref.u) + (uint32_t)(mul24(oy + row, cw) + ox + c2);
   const uint32_t v = (uint32_t)src[0] | ((uint32_t)src[1] << 8);
   reinterpret_cast<uint16_t *>(L.cpred)[pl * 32 + row * 4 + (c2 >> 1)] = (uint16_t)v;
 }
@@ -837,7 +846,7 @@ __device__ __forceinline__ void predict_row_glb(const Picture &ref, int w, int b
   const int pw = g.plane ? w / 2 : w;
   const uint8_t *pl = g.plane == 0 ? ref.y : (g.plane == 1 ? ref.u : ref.v);
   const int dx = mf ? (g.plane ? mvx / 2 : mvx) : 0, dy = mf ? (g.plane ? mvy / 2 : mvy) : 0;
-  const uint8_t *src = pl + (g.y + dy + r) * pw + g.x + dx;
+  const uint8_t *src = pl + mul24(g.y + dy + r, pw) + g.x + dx;
   uint32_t lo = 0, hi = 0;
 #pragma unroll
   for (int k = 0; k < 4; k++) {
@@ -984,7 +993,7 @@ __device__ __forceinline__ MbFetch fetch_mb(const p64gpu_encode_args &a, const u
   const int pw = g.plane ? w >> 1 : w;
   const uint8_t *cplane = g.plane == 0 ? cur.y : (g.plane == 1 ? cur.u : cur.v);
   MbFetch f;
-  f.crow = *reinterpret_cast<const uint2 *>(cplane + (g.y + r) * pw + g.x);
+  f.crow = *reinterpret_cast<const uint2 *>(cplane + (uint32_t)(mul24(g.y + r, pw) + g.x));
   if (MODE != 0)
     f.luma = fetch_luma(a.ref + (size_t)fi * a.frame_stride, cur.y, w, h, 16 * mbx, 16 * mby, lane);
   return f;
@@ -1100,8 +1109,8 @@ __device__ __forceinline__ void encode_mb(const p64gpu_encode_args &a, const uin
   if (act) {
 #pragma unroll
     for (int k = 0; k < 8; k++) res[k] = clampi(res[k] + pred[k], 0, 255);  // pred = 0 if intra
-    uint8_t *pl = rec + (g.plane == 0 ? 0 : w * h + (g.plane - 1) * (w >> 1) * (h >> 1));
-    *reinterpret_cast<uint2 *>(pl + (g.y + r) * pw + g.x) = pack8(res);
+    *reinterpret_cast<uint2 *>(rec + (uint32_t)(plane_offset(g.plane, w, h) + mul24(g.y + r, pw) + g.x)) =
+        pack8(res);
   }
   if (lane == 0) {
     p64_mb_rec o;
@@ -1203,8 +1212,8 @@ __global__ __launch_bounds__(64) void k_decode_recon(int w, int h, int64_t strid
   if (act) {
 #pragma unroll
     for (int k = 0; k < 8; k++) res[k] = clampi(res[k] + pred[k], 0, 255);
-    uint8_t *pl = rec + (g.plane == 0 ? 0 : w * h + (g.plane - 1) * (w / 2) * (h / 2));
-    *reinterpret_cast<uint2 *>(pl + (g.y + r) * pw + g.x) = pack8(res);
+    *reinterpret_cast<uint2 *>(rec + (uint32_t)(plane_offset(g.plane, w, h) + mul24(g.y + r, pw) + g.x)) =
+        pack8(res);
   }
 }
 
