@@ -261,11 +261,13 @@ __device__ __forceinline__ uint32_t align4(uint32_t hi, uint32_t lo, int shift) 
   return __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)shift);
 }
 // value of lane-1 / lane+1 inside the 16-lane DPP row (row_shr:1 / row_shl:1)
+// (bound_ctrl: a lane without a source reads 0, so `x + from_prev_lane(v)`
+// fuses into one v_add_u32_dpp)
 __device__ __forceinline__ int from_prev_lane(int v) {
-  return __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, false);
+  return __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, true);
 }
 __device__ __forceinline__ int from_next_lane(int v) {
-  return __builtin_amdgcn_update_dpp(0, v, 0x101, 0xf, 0xf, false);
+  return __builtin_amdgcn_update_dpp(0, v, 0x101, 0xf, 0xf, true);
 }
 
 // workgroup id -> macroblock id, bijective, so that ids sharing an XCD
@@ -770,17 +772,25 @@ __device__ __forceinline__ void pred_from_row(uint32_t lo, uint32_t hi, bool fil
     for (int k = 0; k < 8; k++) p[k] = s[k];
     return;
   }
-  int hz[8];
+  // hz[k] = s[k-1] + 2 s[k] + s[k+1] as sums of neighbour pairs (two-source
+  // adds issue at twice the rate of the three-source forms)
+  int a[7], hz[8];
+#pragma unroll
+  for (int k = 0; k < 7; k++) a[k] = opaque(s[k] + s[k + 1]);
   hz[0] = s[0] << 2;
 #pragma unroll
-  for (int k = 1; k < 7; k++) hz[k] = s[k - 1] + 2 * s[k] + s[k + 1];
+  for (int k = 1; k < 7; k++) hz[k] = a[k - 1] + a[k];
   hz[7] = s[7] << 2;
   const bool edge = r == 0 || r == 7;  // rows 0 and 7 are not filtered vertically
 #pragma unroll
   for (int k = 0; k < 8; k++) {
-    const int up = from_prev_lane(hz[k]), dn = from_next_lane(hz[k]);
-    const int v = edge ? hz[k] : (up + 2 * hz[k] + dn) >> 2;
-    p[k] = (v + 2) >> 2;  // == (v & 2) ? (v >> 2) + 1 : v >> 2 for v >= 0
+    // reference: v = (up + 2hz + dn) >> 2 (edge rows: v = hz), then
+    // (v & 2) ? (v >> 2) + 1 : v >> 2 == (v + 2) >> 2 for v >= 0; and
+    // ((t >> 2) + 2) >> 2 == (t + 8) >> 4 for t >= 0 (t mod 4 never borrows)
+    // (opaque: two DPP-fused adds instead of two DPP moves and a v_add3)
+    const int h2 = opaque(hz[k] << 1);
+    const int t = opaque(h2 + from_prev_lane(hz[k])) + from_next_lane(hz[k]);
+    p[k] = ((edge ? h2 << 1 : t) + 8) >> 4;
   }
 }
 

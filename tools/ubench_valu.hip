@@ -29,6 +29,22 @@ __global__ __launch_bounds__(256) void k(uint32_t seed, int iters, uint32_t* out
         if (OP == 7) a[j] = __mul24((int)x, (int)a[j]) ;
         if (OP == 8) a[j] = x ^ a[j];
         if (OP == 9) a[j] = __builtin_amdgcn_qsad_pk_u16_u8(((uint64_t)x << 32) | y, y, a[j]);
+        if (OP == 10) asm("v_pk_add_u16 %0, %1, %2" : "=v"(a[j]) : "v"(x), "v"(a[j]));
+        if (OP == 11) asm("v_pk_mad_u16 %0, %1, %2, %3" : "=v"(a[j]) : "v"(x), "v"(y), "v"(a[j]));
+        if (OP == 12) asm("v_add_u32_e64 %0, %1, %2" : "=v"(a[j]) : "v"(x), "v"(a[j]));
+        if (OP == 13) asm("v_med3_i32 %0, %1, %2, %3" : "=v"(a[j]) : "v"(x), "v"(y), "v"(a[j]));
+        if (OP == 14) asm("v_add_u32_dpp %0, %1, %2 row_shr:1 row_mask:0xf bank_mask:0xf" : "=v"(a[j]) : "v"(x), "v"(a[j]));
+        if (OP == 15) asm("v_cvt_f32_i32_e32 %0, %1" : "=v"(a[j]) : "v"(a[j] ^ x));
+        if (OP == 16) asm("v_mul_f32_e32 %0, %1, %2" : "=v"(a[j]) : "v"(x), "v"(a[j]));
+        if (OP == 17) asm("v_lshl_add_u32 %0, %1, 1, %2" : "=v"(a[j]) : "v"(x), "v"(a[j]));
+        if (OP == 18) asm("v_pk_lshrrev_b16 %0, 1, %1" : "=v"(a[j]) : "v"(a[j]));
+        if (OP == 19) asm("v_bfe_u32 %0, %1, 3, 7" : "=v"(a[j]) : "v"(a[j]));
+        if (OP == 20) asm("v_mul_u32_u24_e32 %0, %1, %2" : "=v"(a[j]) : "v"(x), "v"(a[j]));
+        if (OP == 21) asm("v_ashrrev_i32_e32 %0, 3, %1" : "=v"(a[j]) : "v"(a[j]));
+        if (OP == 22) asm("v_ashrrev_i32_e64 %0, 3, %1" : "=v"(a[j]) : "v"(a[j]));
+        if (OP == 23) asm("v_cndmask_b32_e64 %0, %1, %2, s[0:1]" : "=v"(a[j]) : "v"(x), "v"(a[j]));
+        if (OP == 24) asm("v_mad_i32_i24 %0, %1, %2, %3" : "=v"(a[j]) : "v"(x), "v"(y), "v"(a[j]));
+        if (OP == 25) asm("v_mov_b32_dpp %0, %1 row_shr:1 row_mask:0xf bank_mask:0xf" : "=v"(a[j]) : "v"(a[j]));
       }
     asm volatile("" : "+v"(r[0]), "+v"(r[3]));
   }
@@ -76,5 +92,21 @@ int main() {
   run<7, false>("v_mul_i32_i24", d);
   run<8, false>("v_xor_b32", d);
   run<9, true>("v_qsad_pk_u16_u8", d);
+  run<10, false>("v_pk_add_u16", d);
+  run<11, false>("v_pk_mad_u16", d);
+  run<12, false>("v_add_u32_e64", d);
+  run<13, false>("v_med3_i32", d);
+  run<14, false>("v_add_u32_dpp", d);
+  run<15, false>("v_cvt_f32_i32+xor", d);
+  run<16, false>("v_mul_f32", d);
+  run<17, false>("v_lshl_add_u32", d);
+  run<18, false>("v_pk_lshrrev_b16", d);
+  run<19, false>("v_bfe_u32", d);
+  run<20, false>("v_mul_u32_u24_e32", d);
+  run<21, false>("v_ashrrev_i32_e32", d);
+  run<22, false>("v_ashrrev_i32_e64", d);
+  run<23, false>("v_cndmask_b32_e64", d);
+  run<24, false>("v_mad_i32_i24", d);
+  run<25, false>("v_mov_b32_dpp", d);
   return 0;
 }
