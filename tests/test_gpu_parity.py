@@ -293,3 +293,59 @@ def test_device_synth_matches_host(p64, torch_dev):
         for t in range(2):
             for s in range(3):
                 np.testing.assert_array_equal(d[t, s], p64.synth_frame(5 + s, 10 + t, w, h))
+
+
+# ---------------------------------------------------------------------------
+# the bench's full size: 256 CIF sequences per launch, FULL SL=31, q=8
+
+def test_bench_scale_properties(p64, oracle_mod, torch_dev):
+    """At BASELINE's full size (one launch over 256 CIF pictures = 101,376 MBs,
+    device-generated as in bench.py): the decoder reconstruction of the coded
+    output equals the encoder's closed-loop reconstruction for every sequence,
+    a relaunch is bit-identical, the levels obey the H.261 bounds, and two
+    sampled sequences equal the oracle exactly."""
+    torch = torch_dev
+    w, h, S, nfr, q = 352, 288, 256, 3, 8
+    nmb, pic = (w // 16) * (h // 16), w * h * 3 // 2
+    fr = p64.synth_frames_device(w, h, 1, S, 0, nfr)  # [t][s] = synth_frame(1 + s, t)
+    li = torch.zeros(S * nmb, dtype=torch.uint8, device="cuda")
+    recs = [torch.zeros(S * pic, dtype=torch.uint8, device="cuda") for _ in range(nfr)]
+    outs = []
+    for t in range(nfr):
+        o = p64.encode_frames(fr[t].reshape(-1), recs[t - 1] if t else None, recs[t], li, width=w,
+                              height=h, intra=(t == 0), quant=q, me_mode=p64.ME_FULL,
+                              search_limit=31)
+        outs.append((o.coef.clone(), o.mb.clone(), o.me.clone()))
+    qmb = torch.full((S * nmb,), q, dtype=torch.uint8, device="cuda")
+    mask = torch.ones_like(qmb)
+    prev = torch.zeros(S * pic, dtype=torch.uint8, device="cuda")
+    for t in range(nfr):
+        d = torch.zeros_like(prev)
+        p64.decode_recon(prev, d, outs[t][0], outs[t][1], qmb, mask, width=w, height=h)
+        assert torch.equal(d, recs[t]), f"decoder recon != encoder recon at picture {t}"
+        prev = d
+        coef = outs[t][0].view(S, nmb, 6, 64)
+        assert int(coef.abs().max()) <= 254 and int(coef[:, :, :, 1:].abs().max()) <= 127
+    # relaunch of the last picture: identical levels, records and reconstruction
+    li2 = li.clone()
+    li2.zero_()
+    rec_again = torch.zeros_like(recs[-1])
+    o = p64.encode_frames(fr[nfr - 1].reshape(-1), recs[nfr - 2], rec_again, li2, width=w, height=h,
+                          intra=False, quant=q, me_mode=p64.ME_FULL, search_limit=31)
+    # (LastIntra differs only through the counters, which are all < 131 here)
+    assert torch.equal(o.coef, outs[-1][0]) and torch.equal(o.mb, outs[-1][1])
+    assert torch.equal(rec_again, recs[-1])
+    # two sampled sequences against the oracle
+    frames_h = fr.cpu().numpy()
+    for s in (0, S - 1):
+        li_o = np.zeros(nmb, np.uint8)
+        ref = None
+        for t in range(nfr):
+            coef, mb, me, recon = oracle_mod.encode_frame(w, h, frames_h[t][s], ref, li_o,
+                                                          intra=(t == 0), quant=q, me_mode=1,
+                                                          search_limit=31)
+            ref = recon
+            np.testing.assert_array_equal(host(outs[t][0]).reshape(S, nmb, 6, 64)[s], coef,
+                                          err_msg=f"coef s{s} t{t}")
+            np.testing.assert_array_equal(host(recs[t]).reshape(S, pic)[s], recon,
+                                          err_msg=f"recon s{s} t{t}")
