@@ -33,6 +33,14 @@
 
 namespace {
 
+// development aid: -DP64_SECTIONS marks kernel phases in the ISA listing
+// (tools/section_census.py counts instructions per phase)
+#ifdef P64_SECTIONS
+#define SECTION(name) asm volatile(";## " name)
+#else
+#define SECTION(name)
+#endif
+
 // ---------------------------------------------------------------------------
 // error reporting
 
@@ -288,12 +296,23 @@ constexpr int WIN_WORDS = WIN_BYTES / 4;
 constexpr int WIN_OY = 15, WIN_OX = 16;  // window coordinates of (x0, y0)
 constexpr int BLK_STRIDE = 72, ROW_STRIDE = 9;  // padded DCT scratch
 
+constexpr int LB_MAP_WORDS = 4 * 42 * 12 / 4;  // FULL search lower-bound map (me_full)
+constexpr int SURV_LIST_MAX = 256;             // FULL search survivor list (me_full)
+
+// (the union comes first: LDS offset 0 keeps the map's row offsets within the
+// 8-bit dword offsets of ds_read2_b32)
 struct __align__(16) MbLds {
+  union {  // the transform scratch is free while the FULL search runs
+    struct {
+      int blk[6 * BLK_STRIDE];  // row/column exchange for DCT/IDCT
+      int16_t zz[6 * 64];       // zigzagged levels for the store
+    };
+    uint32_t map[LB_MAP_WORDS];   // lower-bound map (phase planes)
+    uint32_t list[SURV_LIST_MAX];  // survivor list (after the map is dead)
+  };
   uint32_t win[WIN_ROWS * WIN_WORDS];  // previous reconstruction, luma
   uint32_t cur[64];                    // current 16x16 luma
   uint32_t cpred[2 * 16];              // chroma prediction sources, 2 x 8x8 bytes
-  int blk[6 * BLK_STRIDE];             // row/column exchange for DCT/IDCT
-  int16_t zz[6 * 64];                  // zigzagged levels for the store
 };
 
 struct Picture {  // one planar 4:2:0 picture
@@ -352,34 +371,43 @@ __device__ __forceinline__ int sad_zero(const MbLds &L, int lane) {
   return wave_sum((int)sad4(r, L.cur[lane], 0));
 }
 
-// FastBME (me.c:187-227) over [-sl/2, sl/2)^2, exact, with a partial-distortion
-// pre-pass (the GPU form of ComputeError's early exit, me.c:122-170).
+// FastBME (me.c:187-227) over [-sl/2, sl/2)^2, exact, pruned by a lower bound
+// on the SAD built from 4x4 sub-block averages (the GPU form of ComputeError's
+// early exit, me.c:122-170: work on candidates that cannot win is skipped, the
+// answer is unchanged).
 //
-// Lane layout: lane = (dy half, dx index); each lane owns the 15 candidates
-// dy = -15 + 15*half + d, d = 0..14, of its column dx = dxi - 15.  The window
-// row i of the lane's half meets current row r at candidate d = i - r, so a
-// row of window bytes, aligned once, feeds up to 15 candidates.
-//
-//  1. rows 0..MP-1 of every candidate (MP = 6: 3/8 of the SAD work)
-//  2. c* = the valid candidate with the least partial sum (first in scan order);
-//     its full SAD, and SAD(0,0), bound the answer: T = min(SAD(c*), SAD(0,0))
-//  3. a candidate whose partial sum already exceeds T can neither win nor tie
-//     (its SAD only grows), so rows MP..15 are summed only for the survivors:
-//     compacted into an LDS list and finished 16 lanes per candidate when at
-//     most 16 survive, one per lane up to ME_LIST_MAX, densely beyond (flat
-//     content, where little prunes).  A second pruning after row 11 was
-//     measured and bought nothing: this phase is not VALU-bound.
+//  1. m(x, y) = nested floor average of the 4x4 pixels at (x, y), four levels of
+//     v_lerp_u8 (bytewise (a+b)>>1): m = sum/16 - e with e in [0, 2] (each level
+//     adds at most 1/2).  For a candidate and the current block, per 4x4
+//     sub-block |sum_c - sum_r| >= 16 |m_c - m_r| - 32, so
+//         SAD >= LB = 16 S - 512,  S = sum over the 16 sub-blocks |m_c - m_r|
+//     (S: four v_sad_u8 per candidate against the current block's 16 averages).
+//  2. c* = the valid candidate with the least S (first in scan order); its full
+//     SAD and SAD(0,0) bound the answer: T = min(SAD(c*), SAD(0,0)).
+//  3. a candidate with LB > T, i.e. S > (T + 512) / 16, can neither win nor tie;
+//     the survivors (a handful on natural content) get their full SAD: 4, 8 or
+//     16 lanes per candidate for up to 32 of them, one per lane up to
+//     ME_LIST_MAX, every candidate densely beyond (flat content, where nothing
+//     prunes).
 //  4. the winner is the least (SAD, scan order) key among c*, the survivors and
 //     (0,0), which wins ties because FastBME evaluates it first (me.c:203, 220).
 // The result is identical to the exhaustive search for every input.
-#ifndef ME_PARTIAL_ROWS
-#define ME_PARTIAL_ROWS 6
-#endif
+//
+// Lane layout of the bound: lane = (dy half, dx index), 15 candidates
+// dy = -15 + 15*half + d, d = 0..14, of the column dx = dxi - 15.  Keys are
+// SUM << 10 | ord, ord = 1 + (dx+15)*32 + (dy+15): FastBME's dx-major scan order
+// (ord 0 is reserved for the zero vector).
 #ifndef ME_LIST_MAX
 #define ME_LIST_MAX 256
 #endif
-constexpr int MP = ME_PARTIAL_ROWS;  // rows of every candidate in the pre-pass
-static_assert(ME_LIST_MAX <= 6 * BLK_STRIDE, "survivor list lives in the DCT scratch");
+static_assert(ME_LIST_MAX <= SURV_LIST_MAX, "survivor list size");
+constexpr uint32_t ME_INVALID = 1u << 19;  // above any real SAD (<= 65280) or S
+constexpr int KEY_SHIFT = 10;
+constexpr unsigned KEY_ORD = (1u << KEY_SHIFT) - 1;
+// lower-bound map: 4 phase planes (x mod 4) x MAP_ROWS rows x MAP_ROW_BYTES
+// bytes; plane p, row y, byte k holds m(4k + p, y) in window coordinates
+constexpr int MAP_ROWS = 42, MAP_ROW_BYTES = 12, MAP_PLANE_BYTES = MAP_ROWS * MAP_ROW_BYTES;
+static_assert(4 * MAP_PLANE_BYTES == 4 * LB_MAP_WORDS, "map size");
 
 // rows [R0, R1) of the current block against window rows [I0, I1) of the lane
 template <int R0, int R1, int I0, int I1>
@@ -423,61 +451,114 @@ __device__ __forceinline__ void load_cur_rows(const uint8_t *cur_blk, int w, uin
   }
 }
 
-// survivors' keys (partial << 11 | 1 + scan order) of the dense sums into the
-// LDS list, in lane-major order
-__device__ __forceinline__ void compact_keys(const uint32_t acc[15], unsigned T, unsigned base,
-                                             int lane, uint32_t *list) {
-  int pos = 0;
+__device__ __forceinline__ uint32_t lerp4(uint32_t a, uint32_t b) {  // bytewise (a+b)>>1
+  return __builtin_amdgcn_lerp(a, b, 0u);
+}
+// value of lane+1 across the whole wave (DPP wave_shl:1; lane 63 reads 0)
+__device__ __forceinline__ uint32_t from_next_lane_wave(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x130, 0xf, 0xf, true);
+}
+
+// 1. the map over the window (rows 0..41, x 1..42 used) into L.map.  Lane =
+// (chunk c of 9 map rows, natural dword n = x/4); vertical levels on the window
+// dwords, horizontal levels with the neighbour dword from lane + 1, the four
+// bytes of a natural dword scattered to the four phase planes.
+__device__ __forceinline__ void build_lb_map(MbLds &L, int lane) {
+  const int c = lane / 12, n = lane - 12 * c;
+  const bool act = lane < 60;
+  const int y0 = 9 * min(c, 4);
+  uint32_t v1[11];
 #pragma unroll
-  for (int d = 0; d < 15; d++) {
-    const bool sv = acc[d] <= T;
-    const uint64_t bl = __ballot(sv);
-    if (bl) {
-      const int idx = pos + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bl >> 32),
-                                                           __builtin_amdgcn_mbcnt_lo((uint32_t)bl, 0u));
-      if (sv) list[idx] = (acc[d] << 11) + base + d;
-      pos += __popcll(bl);
+  for (int t = 0; t < 11; t++) {
+    const int ya = min(y0 + t, WIN_ROWS - 1), yb = min(y0 + t + 1, WIN_ROWS - 1);
+    v1[t] = lerp4(L.win[ya * WIN_WORDS + n], L.win[yb * WIN_WORDS + n]);
+  }
+  uint8_t *mp = reinterpret_cast<uint8_t *>(L.map) + n;
+#pragma unroll
+  for (int t = 0; t < 9; t++) {
+    const uint32_t v = lerp4(v1[t], v1[t + 2]);  // rows y..y+3
+    const uint32_t h1 = lerp4(v, align4(from_next_lane_wave(v), v, 1));
+    const uint32_t h2 = lerp4(h1, align4(from_next_lane_wave(h1), h1, 2));
+    const int y = y0 + t;
+    if (act && y < MAP_ROWS) {
+      uint8_t *q = mp + y * MAP_ROW_BYTES;
+      q[0] = (uint8_t)h2;
+      q[MAP_PLANE_BYTES] = (uint8_t)(h2 >> 8);
+      q[2 * MAP_PLANE_BYTES] = (uint8_t)(h2 >> 16);
+      q[3 * MAP_PLANE_BYTES] = (uint8_t)(h2 >> 24);
     }
   }
 }
 
-// dense rows [R0, R1) in two chunks, each with its current rows in scalar
-// registers only while it runs (the window rows are aligned twice)
-template <int R0, int R1>
-__device__ __forceinline__ void full_rows_chunked(const uint32_t *wrow, int sh, const uint8_t *cur_blk,
-                                                  int w, uint32_t *cs, uint32_t *acc) {
-  constexpr int RH = (R0 + R1) / 2;
-  load_cur_rows<R0, RH - R0>(cur_blk, w, cs);
-  full_rows<R0, RH, R0, RH + 14>(wrow, sh, cs, acc);
-  load_cur_rows<RH, R1 - RH>(cur_blk, w, cs);
-  full_rows<RH, R1, RH, R1 + 14>(wrow, sh, cs, acc);
+// the current block's 16 sub-block averages (same nesting as the map), row j
+// of sub-blocks as one wave-uniform dword cm[j] (byte i = sub-block (i, j))
+__device__ __forceinline__ void cur_lb_map(MbLds &L, int lane, uint32_t cm[4]) {
+  if (lane < 16) {
+    const int i = lane & 3, j = lane >> 2;
+    const uint32_t *r = L.cur + 16 * j + i;
+    const uint32_t v = lerp4(lerp4(r[0], r[4]), lerp4(r[8], r[12]));
+    const uint32_t h1 = lerp4(v, v >> 8);
+    const uint32_t h2 = lerp4(h1, h1 >> 16);
+    reinterpret_cast<uint8_t *>(L.cpred)[lane] = (uint8_t)h2;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < 4; j++) cm[j] = (uint32_t)uni((int)L.cpred[j]);
 }
 
-__device__ __forceinline__ void key_pos(unsigned key, int &cdx, int &cdy) {
-  const int ord = (int)(key & 2047u) - 1;
-  cdx = ord / 30 - 15;
-  cdy = ord % 30 - 15;
+__device__ __forceinline__ void ord_pos(unsigned ord, int &cdx, int &cdy) {  // ord >= 1
+  cdx = (int)((ord - 1) >> 5) - 15;
+  cdy = (int)((ord - 1) & 31) - 15;
 }
 
-// rows [R0, R1) of the n listed candidates, one per lane.  R1 == 16: the
-// keys are complete and folded into bk; otherwise the candidates still <= T
-// are compacted in place (a chunk's reads precede its writes) and counted.
-template <int R0, int R1>
-__device__ __forceinline__ int list_rows(const MbLds &L, uint32_t *list, int n, unsigned T, int lane,
-                                         unsigned &bk) {
-  int pos = 0;
+// full SADs of the n <= 32 listed candidates (ords in L.list), 4*RG lanes per
+// candidate: lane (slot, rg, d) sums dword d of rows rg, rg+RG, ...; returns the
+// least key
+template <int RG>
+__device__ __forceinline__ unsigned finish_groups(const MbLds &L, int n, int lane) {
+  constexpr int G = 4 * RG, PER = 64 / G, NR = 16 / RG;
+  const int d = lane & 3, rg = (lane >> 2) & (RG - 1), slot = lane / G;
+  uint32_t cw[NR];
+#pragma unroll
+  for (int t = 0; t < NR; t++) cw[t] = L.cur[4 * (rg + RG * t) + d];
+  unsigned bk = 0xFFFFFFFFu;
+  for (int c0 = 0; c0 < n; c0 += PER) {
+    const int j = c0 + slot;
+    const unsigned ord = j < n ? L.list[j] : 1u;
+    int cdx, cdy;
+    ord_pos(ord, cdx, cdy);
+    const int cb = WIN_OX + cdx, csh = cb & 3;
+    const uint32_t *p0 = L.win + (WIN_OY + cdy + rg) * WIN_WORDS + (cb >> 2) + d;
+    uint32_t a = 0;
+#pragma unroll
+    for (int t = 0; t < NR; t++) {
+      const uint32_t *p = p0 + RG * t * WIN_WORDS;
+      a = sad4(align4(p[1], p[0], csh), cw[t], a);
+    }
+    a += dpp<0xB1>(a);  // the group's lanes: quad, then 8, then 16
+    a += dpp<0x4E>(a);
+    if (RG >= 2) a += dpp<0x141>(a);
+    if (RG >= 4) a += dpp<0x140>(a);
+    if (j < n) bk = min(bk, (a << KEY_SHIFT) | ord);
+  }
+  return wave_min(bk);
+}
+
+// full SADs of the listed candidates (keys with the ord in the low bits), one
+// per lane; returns the least key
+__device__ __forceinline__ unsigned finish_list(const MbLds &L, int n, int lane) {
+  unsigned bk = 0xFFFFFFFFu;
   for (int c0 = 0; c0 < n; c0 += 64) {
-    const bool live = c0 + lane < n;
-    unsigned key = live ? list[c0 + lane] : 0xFFFFFFFFu;
-    if (live) {
+    if (c0 + lane < n) {
+      const unsigned ord = L.list[c0 + lane] & KEY_ORD;
       int cdx, cdy;
-      key_pos(key, cdx, cdy);
+      ord_pos(ord, cdx, cdy);
       const int cb = WIN_OX + cdx, csh = cb & 3;
-      const uint32_t *p0 = L.win + (WIN_OY + cdy + R0) * WIN_WORDS + (cb >> 2);
+      const uint32_t *p0 = L.win + (WIN_OY + cdy) * WIN_WORDS + (cb >> 2);
       uint32_t a = 0;
 #pragma unroll
-      for (int r = R0; r < R1; r++) {
-        const uint32_t *p = p0 + (r - R0) * WIN_WORDS;
+      for (int r = 0; r < 16; r++) {
+        const uint32_t *p = p0 + r * WIN_WORDS;
         const uint32_t a0 = p[0], a1 = p[1], a2 = p[2], a3 = p[3], a4 = p[4];
         // LDS broadcast, re-read per chunk (opaque index: not hoisted out of
         // the loop into live registers)
@@ -487,59 +568,23 @@ __device__ __forceinline__ int list_rows(const MbLds &L, uint32_t *list, int n, 
         a = sad4(align4(a3, a2, csh), c.z, a);
         a = sad4(align4(a4, a3, csh), c.w, a);
       }
-      key += a << 11;
+      bk = min(bk, (a << KEY_SHIFT) | ord);
     }
-    if (R1 == 16) {
-      bk = min(bk, key);
-    } else {
-      const bool sv = live && (key >> 11) <= T;
-      const uint64_t bl = __ballot(sv);
-      const int idx = pos + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bl >> 32),
-                                                           __builtin_amdgcn_mbcnt_lo((uint32_t)bl, 0u));
-      if (sv) list[idx] = key;
-      pos += __popcll(bl);
-    }
-  }
-  if (R1 != 16) __syncthreads();
-  return uni(pos);
-}
-
-// rows [R0, 16) of n <= 16 listed candidates, four at a time, 16 lanes each:
-// lane (d, rg) sums dword d of rows R0+rg, R0+rg+4, ...; returns the least key
-template <int R0>
-__device__ __forceinline__ unsigned finish_16(const MbLds &L, const uint32_t *list, int n, int lane) {
-  constexpr int NT = (16 - R0 + 3) / 4;
-  const int d = lane & 3, rg = (lane >> 2) & 3;
-  uint32_t cw[NT];
-#pragma unroll
-  for (int t = 0; t < NT; t++) {
-    const int r = R0 + rg + 4 * t;
-    cw[t] = r < 16 ? L.cur[4 * r + d] : 0u;
-  }
-  unsigned bk = 0xFFFFFFFFu;
-  for (int c0 = 0; c0 < n; c0 += 4) {
-    const int j = c0 + (lane >> 4);
-    const unsigned key = j < n ? list[j] : 0xFFFFFFFFu;
-    int cdx, cdy;
-    key_pos(key, cdx, cdy);
-    const int cb = WIN_OX + cdx, csh = cb & 3;
-    const uint32_t *p0 = L.win + (WIN_OY + cdy + R0 + rg) * WIN_WORDS + (cb >> 2) + d;
-    uint32_t a = 0;
-#pragma unroll
-    for (int t = 0; t < NT; t++) {
-      if (R0 + rg + 4 * t < 16) {
-        const uint32_t *p = p0 + 4 * t * WIN_WORDS;
-        a = sad4(align4(p[1], p[0], csh), cw[t], a);
-      }
-    }
-    a += dpp<0xB1>(a);
-    a += dpp<0x4E>(a);
-    a += dpp<0x141>(a);
-    a += dpp<0x140>(a);
-    if (j < n) bk = min(bk, key + (a << 11));
   }
   return wave_min(bk);
 }
+
+#ifdef P64_ME_STATS
+// development aid (tools/me_paths.py): which survivor path each macroblock took
+__device__ unsigned long long g_me_stats[8];
+__device__ __forceinline__ void me_stats_count(int lane, int nsurv) {
+  if (lane == 0) {
+    atomicAdd(&g_me_stats[0], 1ull);
+    atomicAdd(&g_me_stats[1], (unsigned long long)nsurv);
+    atomicAdd(&g_me_stats[nsurv <= 4 ? 2 : nsurv <= 8 ? 3 : nsurv <= 32 ? 4 : nsurv <= ME_LIST_MAX ? 5 : 6], 1ull);
+  }
+}
+#endif
 
 __device__ __forceinline__ void me_full(MbLds &L, const uint8_t *cur_blk, int w, int h, int x0,
                                         int y0, int sl, int lane, int sad0, int &mx, int &my,
@@ -547,83 +592,145 @@ __device__ __forceinline__ void me_full(MbLds &L, const uint8_t *cur_blk, int w,
   const int half = lane >> 5, dxi = lane & 31;
   const bool lane_ok = dxi < 30;
   const int colb = (lane_ok ? dxi : 29) + 1;  // window byte column of dx = dxi-15
-  const int w0 = colb >> 2, sh = colb & 3;
-  const uint32_t *wrow = L.win + (15 * half) * WIN_WORDS + w0;
 
   // Validity (me.c:206-212: range and `< W-16`) is folded into the sums: an
-  // invalid candidate starts at INVALID, above any real SAD (<= 65280), so it
-  // never survives and never wins, and needs no per-candidate test later.
-  constexpr uint32_t INVALID = 1u << 19;
+  // invalid candidate starts at ME_INVALID, so it never survives and never wins.
   const int hl = sl >> 1;
   const int dx = dxi - 15, px = x0 + dx;
   const bool col_ok = lane_ok && dx >= -hl && dx < hl && px >= 0 && px < w - 16;
   // valid dy: [max(-hl, -y0), min(hl, h-16-y0)), i.e. d in [dlo, dhi) for this half
   const int dlo = max(-hl, -y0) + 15 - 15 * half, dhi = min(hl, h - 16 - y0) + 15 - 15 * half;
   const bool all_rows = dlo <= 0 && dhi >= 15;
+  const bool interior = uni(__all(!lane_ok || (col_ok && all_rows)));
+  auto init = [&](uint32_t *a) {
+    if (interior) {  // one select for all
+      const uint32_t v = lane_ok ? 0u : ME_INVALID;
+#pragma unroll
+      for (int d = 0; d < 15; d++) a[d] = v;
+    } else {
+#pragma unroll
+      for (int d = 0; d < 15; d++) a[d] = (col_ok && d >= dlo && d < dhi) ? 0u : ME_INVALID;
+    }
+  };
+  const unsigned base = ((unsigned)dxi << 5) + (unsigned)(15 * half) + 1u;  // ord of d = 0
+
+  // 1. lower bounds S
+  SECTION("lb_map");
+  build_lb_map(L, lane);
+  SECTION("cur_map");
+  uint32_t cm[4];
+  cur_lb_map(L, lane, cm);  // (its barrier also orders the map stores)
+  SECTION("lb_pass");
   uint32_t acc[15];
-  if (uni(__all(!lane_ok || (col_ok && all_rows)))) {  // interior: one select for all
-    const uint32_t init = lane_ok ? 0u : INVALID;
+  init(acc);
+  {
+    const int xq = colb >> 2;
+    const uint32_t *mrow = L.map + ((colb & 3) * MAP_PLANE_BYTES + 15 * half * MAP_ROW_BYTES) / 4 + (xq >> 2);
+    const int msh = xq & 3;
 #pragma unroll
-    for (int d = 0; d < 15; d++) acc[d] = init;
-  } else {
+    for (int i = 0; i < 27; i++) {
+      const uint32_t *q = mrow + i * (MAP_ROW_BYTES / 4);
+      const uint32_t m4 = align4(q[1], q[0], msh);
 #pragma unroll
-    for (int d = 0; d < 15; d++) acc[d] = (col_ok && d >= dlo && d < dhi) ? 0u : INVALID;
+      for (int j = 0; j < 4; j++) {
+        const int d = i - 4 * j;
+        if (d >= 0 && d < 15) acc[d] = sad4(m4, cm[j], acc[d]);
+      }
+    }
   }
 
-  uint32_t cs[64];
-  load_cur_rows<0, MP>(cur_blk, w, cs);
-  // 1. rows 0..MP-1
-  full_rows<0, MP, 0, MP + 14>(wrow, sh, cs, acc);
-
-  // key = SUM<<11 | (1 + scan order); scan order (dx+15)*30+(dy+15)
-  const unsigned base = (unsigned)(dxi * 30 + 15 * half + 1);
   // 2. c* and its full SAD
+  SECTION("cstar");
   unsigned pk = 0xFFFFFFFFu;
 #pragma unroll
-  for (int d = 0; d < 15; d++) pk = min(pk, (acc[d] << 11) + base + d);
+  for (int d = 0; d < 15; d++) pk = min(pk, (acc[d] << KEY_SHIFT) + base + d);
   pk = uni((int)wave_min(pk));
   unsigned ckey = 0xFFFFFFFFu;  // full key of c* (none if nothing is valid)
-  if ((pk >> 11) < INVALID) {
-    const int ord = (int)(pk & 2047u) - 1;
-    const int cdx = ord / 30 - 15, cdy = ord % 30 - 15;
+  if ((pk >> KEY_SHIFT) < ME_INVALID) {
+    int cdx, cdy;
+    ord_pos(pk & KEY_ORD, cdx, cdy);
     const int cb = WIN_OX + cdx + 4 * (lane & 3);
-    const uint32_t *p = L.win + (WIN_OY + cdy + MP + (lane >> 2)) * WIN_WORDS + (cb >> 2);
-    const uint32_t s =
-        lane < 4 * (16 - MP) ? sad4(align4(p[1], p[0], cb & 3), L.cur[4 * MP + lane], 0u) : 0u;
-    ckey = pk + ((unsigned)uni(wave_sum((int)s)) << 11);
+    const uint32_t *p = L.win + (WIN_OY + cdy + (lane >> 2)) * WIN_WORDS + (cb >> 2);
+    const uint32_t s = sad4(align4(p[1], p[0], cb & 3), L.cur[lane], 0u);
+    ckey = (pk & KEY_ORD) | ((unsigned)uni(wave_sum((int)s)) << KEY_SHIFT);
   }
-  const unsigned T = min(ckey >> 11, (unsigned)sad0);
+  const unsigned T = min(ckey >> KEY_SHIFT, (unsigned)sad0);
+  const unsigned Ts = (T + 512u) >> 4;  // survivors: S <= Ts
 
-  // 3. survivors: partial <= T (c* itself included: one more list entry is free)
-  uint32_t *list = reinterpret_cast<uint32_t *>(L.blk);  // DCT scratch, free during the search
+  SECTION("survivors");
+  // 3. survivors.  Up to 32 of them are listed by walking the ballots in
+  // scalar registers (lane 0 stores the ords); the count decides the path.
+  uint32_t *list = L.list;  // aliases the map, which is dead now
   int nsurv = 0;
 #pragma unroll
-  for (int d = 0; d < 15; d++) nsurv += __popcll(__ballot(acc[d] <= T));
+  for (int d = 0; d < 15; d++) {
+    uint64_t m = __ballot(acc[d] <= Ts);
+    const int c = __popcll(m);
+    if (nsurv + c <= 32) {
+      int idx = nsurv;
+      while (m) {
+        const int l = __builtin_ctzll(m);
+        m &= m - 1;
+        const unsigned ord = ((unsigned)(l & 31) << 5) + (unsigned)(15 * (l >> 5) + d) + 1u;
+        if (lane == 0) list[idx] = ord;
+        idx++;
+      }
+    }
+    nsurv += c;
+  }
   nsurv = uni(nsurv);
+#ifdef P64_ME_STATS
+  me_stats_count(lane, nsurv);
+#endif
 
+  SECTION("finish");
   unsigned bk = 0xFFFFFFFFu;
-  if (nsurv > ME_LIST_MAX) {  // little pruned: finish every candidate densely
-    full_rows_chunked<MP, 16>(wrow, sh, cur_blk, w, cs, acc);
-#pragma unroll
-    for (int d = 0; d < 15; d++) bk = min(bk, (acc[d] << 11) + base + d);
-  } else {
-    compact_keys(acc, T, base, lane, list);
+  if (nsurv <= 32) {
     __syncthreads();
-    if (nsurv <= 16)
-      bk = finish_16<MP>(L, list, nsurv, lane);  // the common case on textured content
+    if (nsurv <= 4)
+      bk = finish_groups<4>(L, nsurv, lane);
+    else if (nsurv <= 8)
+      bk = finish_groups<2>(L, nsurv, lane);
     else
-      list_rows<MP, 16>(L, list, nsurv, T, lane, bk);
+      bk = finish_groups<1>(L, nsurv, lane);
+  } else if (nsurv <= ME_LIST_MAX) {
+    int pos = 0;
+#pragma unroll
+    for (int d = 0; d < 15; d++) {
+      const bool sv = acc[d] <= Ts;
+      const uint64_t bl = __ballot(sv);
+      if (bl) {
+        const int idx = pos + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bl >> 32),
+                                                             __builtin_amdgcn_mbcnt_lo((uint32_t)bl, 0u));
+        if (sv) list[idx] = base + d;
+        pos += __popcll(bl);
+      }
+    }
+    __syncthreads();
+    bk = finish_list(L, nsurv, lane);
+  } else {  // little pruned: every candidate densely, rows in two chunks
+    const uint32_t *wrow = L.win + (15 * half) * WIN_WORDS + (colb >> 2);
+    const int sh = colb & 3;
+    uint32_t cs[64];
+    init(acc);
+    load_cur_rows<0, 8>(cur_blk, w, cs);
+    full_rows<0, 8, 0, 22>(wrow, sh, cs, acc);
+    load_cur_rows<8, 8>(cur_blk, w, cs);
+    full_rows<8, 16, 8, 30>(wrow, sh, cs, acc);
+#pragma unroll
+    for (int d = 0; d < 15; d++) bk = min(bk, (acc[d] << KEY_SHIFT) + base + d);
+    bk = wave_min(bk);
   }
 
   // 4. winner
-  bk = min(min(wave_min(bk), ckey), (unsigned)sad0 << 11);
-  const int ord = (int)(bk & 2047u);
-  best = (int)(bk >> 11);
+  SECTION("winner");
+  bk = min(min(bk, ckey), (unsigned)sad0 << KEY_SHIFT);
+  const unsigned ord = bk & KEY_ORD;
+  best = (int)(bk >> KEY_SHIFT);
   if (ord == 0) {
     mx = my = 0;
   } else {
-    mx = (ord - 1) / 30 - 15;
-    my = (ord - 1) % 30 - 15;
+    ord_pos(ord, mx, my);
   }
 }
 
@@ -1030,6 +1137,7 @@ __device__ __forceinline__ void encode_mb(const p64gpu_encode_args &a, const uin
   int mt = 0, mvx = 0, mvy = 0;
   if (MODE != 0) {
     __syncthreads();
+    SECTION("e_me");
     const MeOut me = motion_estimate<MODE>(L, cur.y, w, h, x0, y0, a.search_limit, lane);
     if (a.me && lane == 0) {
       p64_me_rec o;
@@ -1042,6 +1150,7 @@ __device__ __forceinline__ void encode_mb(const p64gpu_encode_args &a, const uin
       o.mwor = me.mwor;
       a.me[gmb] = o;
     }
+    SECTION("e_decide");
     mt = decide_mtype(me);
     if (a.mtype_override) {
       const int ov = a.mtype_override[gmb];
@@ -1057,6 +1166,7 @@ __device__ __forceinline__ void encode_mb(const p64gpu_encode_args &a, const uin
   const float rq = c_qrecip.r[q];
   const bool qeven = !(q & 1);
 
+  SECTION("e_predict");
   int pred[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   if (!mt_intra(mt)) {
     stage_chroma(L, ref, w, mbx, mby, mt, mvx, mvy, lane);
@@ -1064,6 +1174,7 @@ __device__ __forceinline__ void encode_mb(const p64gpu_encode_args &a, const uin
     predict_row(L, b, r, mt, mvx, mvy, pred);
   }
 
+  SECTION("e_fwd_dct");
   // ReadCompressMDU (p64.c:830-912): levels in element layout
   const int e = lane;
   const bool dc = e == 0;
@@ -1074,6 +1185,7 @@ __device__ __forceinline__ void encode_mb(const p64gpu_encode_args &a, const uin
 #pragma unroll
     for (int k = 0; k < 8; k++) res[k] -= pred[k];
     forward_2d(L, act, b, r, res);
+    SECTION("e_quant");
     if (mt_intra(mt)) {
 #pragma unroll
       for (int k = 0; k < 6; k++) lev[k] = quantise<true>(blk_at(L, k, e), dc, qeven, rq);
@@ -1082,6 +1194,7 @@ __device__ __forceinline__ void encode_mb(const p64gpu_encode_args &a, const uin
       for (int k = 0; k < 6; k++) lev[k] = quantise<false>(blk_at(L, k, e), dc, qeven, rq);
     }
   }
+  SECTION("e_cbp");
   int cbp = 0x3f;
   if (mt_cbp(mt)) {
     const CbpOut c = cbp_decide(lev);
@@ -1098,6 +1211,7 @@ __device__ __forceinline__ void encode_mb(const p64gpu_encode_args &a, const uin
       }
     }
   }
+  SECTION("e_zz_dequant");
   const int zpos = c_zz.pos[e];
   __syncthreads();  // element reads of blk are complete before it is rewritten
   const int coded = mt_tcoeff(mt) ? cbp : 0;  // block c coded <=> bit 5-c
@@ -1113,6 +1227,7 @@ __device__ __forceinline__ void encode_mb(const p64gpu_encode_args &a, const uin
   if (lane < 48)
     reinterpret_cast<uint4 *>(a.coef + gmb * 384)[lane] = reinterpret_cast<const uint4 *>(L.zz)[lane];
 
+  SECTION("e_inverse");
   // reconstruction (p64.c:945-959, 971-1013)
   int res[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   if (coded) inverse_2d(L, act, b, r, res);
@@ -1122,6 +1237,7 @@ __device__ __forceinline__ void encode_mb(const p64gpu_encode_args &a, const uin
     *reinterpret_cast<uint2 *>(rec + (uint32_t)(plane_offset(g.plane, w, h) + mul24(g.y + r, pw) + g.x)) =
         pack8(res);
   }
+  SECTION("e_mbrec");
   if (lane == 0) {
     p64_mb_rec o;
     o.mtype = (int8_t)mt;
@@ -1651,5 +1767,17 @@ int p64gpu_encoder_frame(p64gpu_encoder *e, const uint8_t *picture, int intra, i
 }
 
 void p64gpu_encoder_close(p64gpu_encoder *e) { enc_free(e); }
+
+#ifdef P64_ME_STATS
+int p64gpu_dbg_stats(unsigned long long *out, int reset) {
+  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_me_stats), sizeof(g_me_stats)));
+  if (reset) {
+    static const unsigned long long z[8] = {};
+    HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_me_stats), z, sizeof(z)));
+  }
+  return 0;
+}
+#endif
 
 }  // extern "C"
