@@ -262,6 +262,10 @@ __device__ __forceinline__ int opaque(int v) {
 // wave-uniform by construction (results of wave reductions); saying so lets
 // hipcc use scalar registers and scalar branches for everything that follows
 __device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
+// LDS pointer in the LDS address space: stores through it cannot alias global
+// memory, so later uniform global loads stay scalar (s_load)
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+__device__ __forceinline__ lds_u32 *as_lds(uint32_t *p) { return (lds_u32 *)p; }
 __device__ __forceinline__ uint32_t sad4(uint32_t a, uint32_t b, uint32_t acc) {
   return __builtin_amdgcn_sad_u8(a, b, acc);
 }
@@ -401,7 +405,10 @@ __device__ __forceinline__ int sad_zero(const MbLds &L, int lane) {
 #define ME_LIST_MAX 256
 #endif
 static_assert(ME_LIST_MAX <= SURV_LIST_MAX, "survivor list size");
-constexpr uint32_t ME_INVALID = 1u << 19;  // above any real SAD (<= 65280) or S
+constexpr uint32_t ME_INVALID = 1u << 19;
+#ifndef ME_LOW_CONTRAST
+#define ME_LOW_CONTRAST 12
+#endif  // above any real SAD (<= 65280) or S
 constexpr int KEY_SHIFT = 10;
 constexpr unsigned KEY_ORD = (1u << KEY_SHIFT) - 1;
 // lower-bound map: 4 phase planes (x mod 4) x MAP_ROWS rows x MAP_ROW_BYTES
@@ -437,17 +444,37 @@ __device__ __forceinline__ void full_rows(const uint32_t *wrow, int sh, const ui
   }
 }
 
-// current-block rows r0..r0+n-1 as wave-uniform dwords, read straight from
-// global memory into SGPRs (scalar loads: no vector instructions spent)
-template <int R0, int N>
-__device__ __forceinline__ void load_cur_rows(const uint8_t *cur_blk, int w, uint32_t *cs) {
+// current-block rows R0..R0+7 as wave-uniform dwords, read straight from
+// global memory into SGPRs with scalar loads (no vector instructions, no
+// VGPRs).  Inline asm: the compiler turns these loads into vector loads when it
+// cannot prove that no store of the kernel clobbers them (the current picture
+// is never written by this kernel).  The wait is inside the same statement, so
+// no use can be scheduled ahead of it.
+typedef unsigned su4 __attribute__((ext_vector_type(4)));
+template <int R0>
+__device__ __forceinline__ void load_cur_rows8(const uint8_t *cur_blk, int w, uint32_t *cs) {
+  su4 v0, v1, v2, v3, v4, v5, v6, v7;
+  const int o = R0 * w;
+  asm volatile(
+      "s_load_dwordx4 %0, %8, %9\n"
+      "s_load_dwordx4 %1, %8, %10\n"
+      "s_load_dwordx4 %2, %8, %11\n"
+      "s_load_dwordx4 %3, %8, %12\n"
+      "s_load_dwordx4 %4, %8, %13\n"
+      "s_load_dwordx4 %5, %8, %14\n"
+      "s_load_dwordx4 %6, %8, %15\n"
+      "s_load_dwordx4 %7, %8, %16\n"
+      "s_waitcnt lgkmcnt(0)"
+      : "=&s"(v0), "=&s"(v1), "=&s"(v2), "=&s"(v3), "=&s"(v4), "=&s"(v5), "=&s"(v6), "=&s"(v7)
+      : "s"(cur_blk), "s"(o), "s"(o + w), "s"(o + 2 * w), "s"(o + 3 * w), "s"(o + 4 * w),
+        "s"(o + 5 * w), "s"(o + 6 * w), "s"(o + 7 * w));
+  const su4 v[8] = {v0, v1, v2, v3, v4, v5, v6, v7};
 #pragma unroll
-  for (int r = R0; r < R0 + N; r++) {
-    const uint4 v = *reinterpret_cast<const uint4 *>(cur_blk + (size_t)r * w);
-    cs[4 * r + 0] = v.x;
-    cs[4 * r + 1] = v.y;
-    cs[4 * r + 2] = v.z;
-    cs[4 * r + 3] = v.w;
+  for (int r = 0; r < 8; r++) {
+    cs[4 * (R0 + r) + 0] = v[r].x;
+    cs[4 * (R0 + r) + 1] = v[r].y;
+    cs[4 * (R0 + r) + 2] = v[r].z;
+    cs[4 * (R0 + r) + 3] = v[r].w;
   }
 }
 
@@ -491,8 +518,10 @@ __device__ __forceinline__ void build_lb_map(MbLds &L, int lane) {
 }
 
 // the current block's 16 sub-block averages (same nesting as the map), row j
-// of sub-blocks as one wave-uniform dword cm[j] (byte i = sub-block (i, j))
-__device__ __forceinline__ void cur_lb_map(MbLds &L, int lane, uint32_t cm[4]) {
+// of sub-blocks as one wave-uniform dword cm[j] (byte i = sub-block (i, j));
+// returns their range (max - min)
+__device__ __forceinline__ int cur_lb_map(MbLds &L, int lane, uint32_t cm[4]) {
+  unsigned lo = 255, hi = 0;
   if (lane < 16) {
     const int i = lane & 3, j = lane >> 2;
     const uint32_t *r = L.cur + 16 * j + i;
@@ -500,10 +529,22 @@ __device__ __forceinline__ void cur_lb_map(MbLds &L, int lane, uint32_t cm[4]) {
     const uint32_t h1 = lerp4(v, v >> 8);
     const uint32_t h2 = lerp4(h1, h1 >> 16);
     reinterpret_cast<uint8_t *>(L.cpred)[lane] = (uint8_t)h2;
+    lo = hi = h2 & 255u;
   }
+  // min and max over DPP row 0 (lanes 0..15)
+  lo = min(lo, dpp<0xB1>(lo));
+  hi = max(hi, dpp<0xB1>(hi));
+  lo = min(lo, dpp<0x4E>(lo));
+  hi = max(hi, dpp<0x4E>(hi));
+  lo = min(lo, dpp<0x141>(lo));
+  hi = max(hi, dpp<0x141>(hi));
+  lo = min(lo, dpp<0x140>(lo));
+  hi = max(hi, dpp<0x140>(hi));
+  const int range = __builtin_amdgcn_readlane((int)(hi - lo), 0);
   __syncthreads();
 #pragma unroll
   for (int j = 0; j < 4; j++) cm[j] = (uint32_t)uni((int)L.cpred[j]);
+  return range;
 }
 
 __device__ __forceinline__ void ord_pos(unsigned ord, int &cdx, int &cdy) {  // ord >= 1
@@ -576,9 +617,12 @@ __device__ __forceinline__ unsigned finish_list(const MbLds &L, int n, int lane)
 
 #ifdef P64_ME_STATS
 // development aid (tools/me_paths.py): which survivor path each macroblock took
-__device__ unsigned long long g_me_stats[8];
-__device__ __forceinline__ void me_stats_count(int lane, int nsurv) {
+__device__ unsigned long long g_me_stats[48];
+__device__ __forceinline__ void me_stats_count(int lane, int nsurv, int range) {
+  // range of the current block's 16 sub-block averages, against the path
+  const int bucket = min(range >> 2, 15);
   if (lane == 0) {
+    atomicAdd(&g_me_stats[8 + 2 * bucket + (nsurv > ME_LIST_MAX ? 1 : 0)], 1ull);
     atomicAdd(&g_me_stats[0], 1ull);
     atomicAdd(&g_me_stats[1], (unsigned long long)nsurv);
     atomicAdd(&g_me_stats[nsurv <= 4 ? 2 : nsurv <= 8 ? 3 : nsurv <= 32 ? 4 : nsurv <= ME_LIST_MAX ? 5 : 6], 1ull);
@@ -614,77 +658,84 @@ __device__ __forceinline__ void me_full(MbLds &L, const uint8_t *cur_blk, int w,
   };
   const unsigned base = ((unsigned)dxi << 5) + (unsigned)(15 * half) + 1u;  // ord of d = 0
 
-  // 1. lower bounds S
-  SECTION("lb_map");
-  build_lb_map(L, lane);
   SECTION("cur_map");
   uint32_t cm[4];
-  cur_lb_map(L, lane, cm);  // (its barrier also orders the map stores)
-  SECTION("lb_pass");
+  const int range = uni(cur_lb_map(L, lane, cm));
+  unsigned bk = 0xFFFFFFFFu, ckey = 0xFFFFFFFFu, Ts = 0;
   uint32_t acc[15];
-  init(acc);
-  {
-    const int xq = colb >> 2;
-    const uint32_t *mrow = L.map + ((colb & 3) * MAP_PLANE_BYTES + 15 * half * MAP_ROW_BYTES) / 4 + (xq >> 2);
-    const int msh = xq & 3;
+  lds_u32 *list = as_lds(L.list);  // aliases the map once the map is dead
+  int nsurv = 1000;
+  // Low-contrast blocks (sub-block averages within a few levels) prune almost
+  // nothing: they go to the dense search straight away (speed only, the result
+  // is the same; tools/me_paths.py measured 98% dense below 12, none above 15).
+  if (range >= ME_LOW_CONTRAST) {
+    // 1. lower bounds S
+    SECTION("lb_map");
+    build_lb_map(L, lane);
+    __syncthreads();
+    SECTION("lb_pass");
+    init(acc);
+    {
+      const int xq = colb >> 2;
+      const uint32_t *mrow =
+          L.map + ((colb & 3) * MAP_PLANE_BYTES + 15 * half * MAP_ROW_BYTES) / 4 + (xq >> 2);
+      const int msh = xq & 3;
 #pragma unroll
-    for (int i = 0; i < 27; i++) {
-      const uint32_t *q = mrow + i * (MAP_ROW_BYTES / 4);
-      const uint32_t m4 = align4(q[1], q[0], msh);
+      for (int i = 0; i < 27; i++) {
+        const uint32_t *q = mrow + i * (MAP_ROW_BYTES / 4);
+        const uint32_t m4 = align4(q[1], q[0], msh);
 #pragma unroll
-      for (int j = 0; j < 4; j++) {
-        const int d = i - 4 * j;
-        if (d >= 0 && d < 15) acc[d] = sad4(m4, cm[j], acc[d]);
+        for (int j = 0; j < 4; j++) {
+          const int d = i - 4 * j;
+          if (d >= 0 && d < 15) acc[d] = sad4(m4, cm[j], acc[d]);
+        }
       }
     }
-  }
 
-  // 2. c* and its full SAD
-  SECTION("cstar");
-  unsigned pk = 0xFFFFFFFFu;
+    // 2. c* and its full SAD
+    SECTION("cstar");
+    unsigned pk = 0xFFFFFFFFu;
 #pragma unroll
-  for (int d = 0; d < 15; d++) pk = min(pk, (acc[d] << KEY_SHIFT) + base + d);
-  pk = uni((int)wave_min(pk));
-  unsigned ckey = 0xFFFFFFFFu;  // full key of c* (none if nothing is valid)
-  if ((pk >> KEY_SHIFT) < ME_INVALID) {
-    int cdx, cdy;
-    ord_pos(pk & KEY_ORD, cdx, cdy);
-    const int cb = WIN_OX + cdx + 4 * (lane & 3);
-    const uint32_t *p = L.win + (WIN_OY + cdy + (lane >> 2)) * WIN_WORDS + (cb >> 2);
-    const uint32_t s = sad4(align4(p[1], p[0], cb & 3), L.cur[lane], 0u);
-    ckey = (pk & KEY_ORD) | ((unsigned)uni(wave_sum((int)s)) << KEY_SHIFT);
-  }
-  const unsigned T = min(ckey >> KEY_SHIFT, (unsigned)sad0);
-  const unsigned Ts = (T + 512u) >> 4;  // survivors: S <= Ts
-
-  SECTION("survivors");
-  // 3. survivors.  Up to 32 of them are listed by walking the ballots in
-  // scalar registers (lane 0 stores the ords); the count decides the path.
-  uint32_t *list = L.list;  // aliases the map, which is dead now
-  int nsurv = 0;
-#pragma unroll
-  for (int d = 0; d < 15; d++) {
-    uint64_t m = __ballot(acc[d] <= Ts);
-    const int c = __popcll(m);
-    if (nsurv + c <= 32) {
-      int idx = nsurv;
-      while (m) {
-        const int l = __builtin_ctzll(m);
-        m &= m - 1;
-        const unsigned ord = ((unsigned)(l & 31) << 5) + (unsigned)(15 * (l >> 5) + d) + 1u;
-        if (lane == 0) list[idx] = ord;
-        idx++;
-      }
+    for (int d = 0; d < 15; d++) pk = min(pk, (acc[d] << KEY_SHIFT) + base + d);
+    pk = uni((int)wave_min(pk));
+    if ((pk >> KEY_SHIFT) < ME_INVALID) {  // else nothing is valid
+      int cdx, cdy;
+      ord_pos(pk & KEY_ORD, cdx, cdy);
+      const int cb = WIN_OX + cdx + 4 * (lane & 3);
+      const uint32_t *p = L.win + (WIN_OY + cdy + (lane >> 2)) * WIN_WORDS + (cb >> 2);
+      const uint32_t s = sad4(align4(p[1], p[0], cb & 3), L.cur[lane], 0u);
+      ckey = (pk & KEY_ORD) | ((unsigned)uni(wave_sum((int)s)) << KEY_SHIFT);
     }
-    nsurv += c;
+    const unsigned T = min(ckey >> KEY_SHIFT, (unsigned)sad0);
+    Ts = (T + 512u) >> 4;  // survivors: S <= Ts
+
+    SECTION("survivors");
+    // 3. survivors.  Up to 32 of them are listed by walking the ballots in
+    // scalar registers (lane 0 stores the ords); the count decides the path.
+    nsurv = 0;
+#pragma unroll
+    for (int d = 0; d < 15; d++) {
+      uint64_t m = __ballot(acc[d] <= Ts);
+      const int c = __popcll(m);
+      if (nsurv + c <= 32) {
+        int idx = nsurv;
+        while (m) {
+          const int l = __builtin_ctzll(m);
+          m &= m - 1;
+          const unsigned ord = ((unsigned)(l & 31) << 5) + (unsigned)(15 * (l >> 5) + d) + 1u;
+          if (lane == 0) list[idx] = ord;
+          idx++;
+        }
+      }
+      nsurv += c;
+    }
+    nsurv = uni(nsurv);
   }
-  nsurv = uni(nsurv);
 #ifdef P64_ME_STATS
-  me_stats_count(lane, nsurv);
+  me_stats_count(lane, nsurv, range);
 #endif
 
   SECTION("finish");
-  unsigned bk = 0xFFFFFFFFu;
   if (nsurv <= 32) {
     __syncthreads();
     if (nsurv <= 4)
@@ -713,9 +764,9 @@ __device__ __forceinline__ void me_full(MbLds &L, const uint8_t *cur_blk, int w,
     const int sh = colb & 3;
     uint32_t cs[64];
     init(acc);
-    load_cur_rows<0, 8>(cur_blk, w, cs);
+    load_cur_rows8<0>(cur_blk, w, cs);
     full_rows<0, 8, 0, 22>(wrow, sh, cs, acc);
-    load_cur_rows<8, 8>(cur_blk, w, cs);
+    load_cur_rows8<8>(cur_blk, w, cs);
     full_rows<8, 16, 8, 30>(wrow, sh, cs, acc);
 #pragma unroll
     for (int d = 0; d < 15; d++) bk = min(bk, (acc[d] << KEY_SHIFT) + base + d);
@@ -1572,12 +1623,11 @@ int p64gpu_motion_estimation(int w, int h, int nframes, int64_t stride, const ui
   if (mode != P64GPU_ME_TSS && mode != P64GPU_ME_FULL) return fail(P64GPU_E_INVALID, "me mode %d", mode);
   if (sl < 1 || sl > 31) return fail(P64GPU_E_INVALID, "search_limit %d not in 1..31", sl);
   const unsigned grid = (unsigned)((int64_t)nframes * (w / 16) * (h / 16));
+  hipStream_t st = (hipStream_t)stream;
   if (mode == P64GPU_ME_FULL)
-    hipLaunchKernelGGL(k_motion<2>, dim3(grid), dim3(64), 0, (hipStream_t)stream, w, h, stride,
-                       ref_y, cur_y, sl, out);
+    hipLaunchKernelGGL(k_motion<2>, dim3(grid), dim3(64), 0, st, w, h, stride, ref_y, cur_y, sl, out);
   else
-    hipLaunchKernelGGL(k_motion<1>, dim3(grid), dim3(64), 0, (hipStream_t)stream, w, h, stride,
-                       ref_y, cur_y, sl, out);
+    hipLaunchKernelGGL(k_motion<1>, dim3(grid), dim3(64), 0, st, w, h, stride, ref_y, cur_y, sl, out);
   HIP_TRY(hipGetLastError());
   return P64GPU_OK;
 }
@@ -1769,11 +1819,11 @@ int p64gpu_encoder_frame(p64gpu_encoder *e, const uint8_t *picture, int intra, i
 void p64gpu_encoder_close(p64gpu_encoder *e) { enc_free(e); }
 
 #ifdef P64_ME_STATS
-int p64gpu_dbg_stats(unsigned long long *out, int reset) {
+int p64gpu_dbg_stats(unsigned long long *out, int reset) {  // out[48]
   HIP_TRY(hipDeviceSynchronize());
   HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_me_stats), sizeof(g_me_stats)));
   if (reset) {
-    static const unsigned long long z[8] = {};
+    static const unsigned long long z[48] = {};
     HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_me_stats), z, sizeof(z)));
   }
   return 0;

@@ -22,7 +22,7 @@ out = p64_amd.FrameBatchOut(coef=torch.empty((S, nmb, 6, 64), dtype=torch.int16,
 p64_amd.encode_frames(fr[0].reshape(-1), None, r0, li, width=w, height=h, intra=True, out=out)
 torch.cuda.synchronize()
 lib = p64_amd.lib()
-st = (ctypes.c_ulonglong * 8)()
+st = (ctypes.c_ulonglong * 48)()
 lib.p64gpu_dbg_stats(st, 1)
 for t in range(1, 6):
     p64_amd.encode_frames(fr[t].reshape(-1), r0, r1, li, width=w, height=h, intra=False,
@@ -33,3 +33,8 @@ for t in range(1, 6):
     n = st[0]
     print(f"picture {t}: MBs {n}  mean survivors {st[1]/n:.1f}  <=4 {st[2]/n:.3f}  <=8 {st[3]/n:.3f}  "
           f"<=32 {st[4]/n:.3f}  list {st[5]/n:.3f}  dense {st[6]/n:.4f}")
+    if t == 5:  # sub-block-average range of the current block vs the dense path
+        for b in range(16):
+            a, d = st[8 + 2 * b], st[9 + 2 * b]
+            if a + d:
+                print(f"  range {4*b:3d}-{4*b+3:3d}{'+' if b == 15 else ' '}: MBs {a+d:7d}  dense {d/(a+d):.3f}")

@@ -45,6 +45,18 @@ __global__ __launch_bounds__(256) void k(uint32_t seed, int iters, uint32_t* out
         if (OP == 23) asm("v_cndmask_b32_e64 %0, %1, %2, s[0:1]" : "=v"(a[j]) : "v"(x), "v"(a[j]));
         if (OP == 24) asm("v_mad_i32_i24 %0, %1, %2, %3" : "=v"(a[j]) : "v"(x), "v"(y), "v"(a[j]));
         if (OP == 25) asm("v_mov_b32_dpp %0, %1 row_shr:1 row_mask:0xf bank_mask:0xf" : "=v"(a[j]) : "v"(a[j]));
+        if (OP == 26) a[j] = __builtin_amdgcn_lerp(x, a[j], 0u);
+        if (OP == 27) asm("v_perm_b32 %0, %1, %2, %3" : "=v"(a[j]) : "v"(x), "v"(a[j]), "v"(y));
+        if (OP == 28) asm("v_cndmask_b32_e32 %0, %1, %2, vcc" : "=v"(a[j]) : "v"(x), "v"(a[j]));
+        if (OP == 29) asm("v_add_u32_e32 %0, %1, %2" : "=v"(a[j]) : "v"(x), "v"(a[j]));
+        if (OP == 30) asm("v_fma_f32 %0, %1, %2, %3" : "=v"(a[j]) : "v"(x), "v"(y), "v"(a[j]));
+        if (OP == 31) asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(a[j]) : "v"(x), "v"(y), "v"(a[j]));
+        if (OP == 32) asm("v_min_u32_e32 %0, %1, %2" : "=v"(a[j]) : "v"(x), "v"(a[j]));
+        if (OP == 33) asm("v_cmp_gt_i32_e64 s[2:3], %1, %2\n v_cndmask_b32_e64 %0, %1, %2, s[2:3]" : "=v"(a[j]) : "v"(x), "v"(a[j]) : "s2", "s3");
+        if (OP == 34) asm("v_cvt_i32_f32_e32 %0, %1" : "=v"(a[j]) : "v"(a[j] ^ x));
+        if (OP == 35) asm("v_pk_fma_f32 %0, %1, %2, %3" : "=v"(*(uint64_t*)&a[j & 6]) : "v"(((uint64_t)x << 32) | y), "v"(((uint64_t)y << 32) | x), "v"(*(uint64_t*)&a[j & 6]));
+        if (OP == 36) asm("v_lshrrev_b32_e32 %0, 8, %1" : "=v"(a[j]) : "v"(a[j]));
+        if (OP == 37) asm("v_sad_u8 %0, %1, %2, %3" : "=v"(a[j]) : "v"(x), "v"(r[(u + j + 3) & 7]), "v"(a[j]));
       }
     asm volatile("" : "+v"(r[0]), "+v"(r[3]));
   }
@@ -108,5 +120,17 @@ int main() {
   run<23, false>("v_cndmask_b32_e64", d);
   run<24, false>("v_mad_i32_i24", d);
   run<25, false>("v_mov_b32_dpp", d);
+  run<26, false>("v_lerp_u8", d);
+  run<27, false>("v_perm_b32", d);
+  run<28, false>("v_cndmask_b32_e32", d);
+  run<29, false>("v_add_u32_e32", d);
+  run<30, false>("v_fma_f32", d);
+  run<31, false>("v_bfi_b32", d);
+  run<32, false>("v_min_u32_e32", d);
+  run<33, false>("cmp_e64+cndmask_e64", d);
+  run<34, false>("v_cvt_i32_f32+xor", d);
+  run<35, false>("v_pk_fma_f32", d);
+  run<36, false>("v_lshrrev_b32_e32", d);
+  run<37, false>("v_sad_u8 (3 vgpr)", d);
   return 0;
 }
