@@ -61,7 +61,8 @@ def parse():
     p.add_argument("--streams", type=int, default=256, help="sequences per GPU")
     p.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     p.add_argument("--cpu-procs", type=int, default=8)
-    p.add_argument("--cpu-frames", type=int, default=120)
+    p.add_argument("--cpu-frames", type=int, default=300,
+                   help="pictures per CPU process (8 x 300 CIF pictures: ~15 s of CPU work)")
     p.add_argument("--no-verify", action="store_true")
     p.add_argument("--no-vlc", action="store_true", help="skip the encode+entropy-coding measurement")
     p.add_argument("--feed", choices=("local", "root"), default="local",
