@@ -1094,26 +1094,31 @@ __device__ __forceinline__ void blk_put(MbLds &L, int k, int e, int v) {
 }
 
 // BoundDctMatrix + CCITT(Flat)Quantize + (Flat)BoundQuantizeMatrix of one raw
-// coefficient (transform.c:271-350, 460-537), branch-free.  dc: lane holds the
-// DC coefficient; INTRA selects the flat DC quantiser.
+// coefficient (transform.c:271-350, 460-537), branch-free.  lo/hi: the lane's
+// BoundDct range (DC: no lower bound, <= 2047; AC: +-1023).  The even-q step
+// c + sign(c) (sign(0) = -1, transform.c:285) is folded into one fma: with
+// s = copysign(rqe, c), rqe = rq for even q and 0 for odd q, fma(c, rq, s) is
+// the one rounding of the exact (c + sign c) * rq that the reference division
+// truncates (c_qrecip: trunc of that product == C's c / 2q; for c = 0 both
+// give 0).  INTRA selects the flat DC quantiser (dc: lane holds the DC).
 template <bool INTRA>
-__device__ __forceinline__ int quantise(int raw, bool dc, bool qeven, float rq) {
-  int v = dct_final(raw);
-  v = clampi(v, dc ? -0x7fffffff : -1023, dc ? 2047 : 1023);
-  const int c = qeven ? v + (v > 0 ? 1 : -1) : v;  // sign(0) = -1 (transform.c:285)
-  int l = (int)((float)c * rq);                     // trunc(c / 2q), see c_qrecip
+__device__ __forceinline__ int quantise(int raw, int lo, int hi, bool dc, float rq, float rqe) {
+  int v;  // clamp to [lo, hi] (per-lane bounds: one v_med3 instead of max + min)
+  asm("v_med3_i32 %0, %1, %2, %3" : "=v"(v) : "v"(dct_final(raw)), "v"(lo), "v"(hi));
+  const float x = (float)v;
+  int l = (int)__builtin_fmaf(x, rq, __builtin_copysignf(rqe, x));
   l = clampi(l, -127, 127);
   if (INTRA) l = dc ? clampi(dct_final(v), 1, 254) : l;  // (DC +- 4) / 8, transform.c:321-325
   return l;
 }
 // ICCITT(Flat)Quantize of one level (transform.c:359-451), branch-free: with
-// sg = sign(l) (0 for l = 0) the reconstruction is (2l + sg) q, minus sg for
-// even q, and 0 stays 0.
+// sg = sign(l) (0 for l = 0) the reconstruction (2l + sg) q, minus sg for even
+// q, is l * q2 + sg * qq with q2 = 2q and qq = q - [q even]; 0 stays 0.  An
+// uncoded block passes q2 = qq = 0 (uniform per block).  Intra DC: DC * 8.
 template <bool INTRA>
-__device__ __forceinline__ int dequantise(int l, bool dc, int q, bool qeven) {
+__device__ __forceinline__ int dequantise(int l, bool dc, int q2, int qq) {
   const int sg = clampi(l, -1, 1);
-  int v = __mul24(2 * l + sg, q);
-  if (qeven) v -= sg;
+  int v = __mul24(l, q2) + __mul24(sg, qq);
   if (INTRA) v = dc ? l * 8 : v;
   return v;
 }
@@ -1216,6 +1221,7 @@ __device__ __forceinline__ void encode_mb(const p64gpu_encode_args &a, const uin
   const int q = uni(a.quant_mb ? a.quant_mb[gmb] : a.quant);
   const float rq = c_qrecip.r[q];
   const bool qeven = !(q & 1);
+  const float rqe = qeven ? rq : 0.0f;
 
   SECTION("e_predict");
   int pred[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -1229,6 +1235,7 @@ __device__ __forceinline__ void encode_mb(const p64gpu_encode_args &a, const uin
   // ReadCompressMDU (p64.c:830-912): levels in element layout
   const int e = lane;
   const bool dc = e == 0;
+  const int qlo = dc ? -0x7fffffff : -1023, qhi = dc ? 2047 : 1023;  // BoundDctMatrix
   int lev[6] = {0, 0, 0, 0, 0, 0};
   if (mt_tcoeff(mt)) {
     int res[8];
@@ -1239,10 +1246,10 @@ __device__ __forceinline__ void encode_mb(const p64gpu_encode_args &a, const uin
     SECTION("e_quant");
     if (mt_intra(mt)) {
 #pragma unroll
-      for (int k = 0; k < 6; k++) lev[k] = quantise<true>(blk_at(L, k, e), dc, qeven, rq);
+      for (int k = 0; k < 6; k++) lev[k] = quantise<true>(blk_at(L, k, e), qlo, qhi, dc, rq, rqe);
     } else {
 #pragma unroll
-      for (int k = 0; k < 6; k++) lev[k] = quantise<false>(blk_at(L, k, e), dc, qeven, rq);
+      for (int k = 0; k < 6; k++) lev[k] = quantise<false>(blk_at(L, k, e), qlo, qhi, dc, rq, rqe);
     }
   }
   SECTION("e_cbp");
@@ -1270,9 +1277,9 @@ __device__ __forceinline__ void encode_mb(const p64gpu_encode_args &a, const uin
 #pragma unroll
   for (int k = 0; k < 6; k++) {
     L.zz[k * 64 + zpos] = (int16_t)lev[k];
-    const int dq = intra ? dequantise<true>(lev[k], dc, q, qeven)
-                         : dequantise<false>(lev[k], dc, q, qeven);
-    blk_put(L, k, e, ((coded >> (5 - k)) & 1) ? dq : 0);
+    const bool ck = (coded >> (5 - k)) & 1;
+    const int q2 = ck ? 2 * q : 0, qq = ck ? q - (int)qeven : 0;
+    blk_put(L, k, e, intra ? dequantise<true>(lev[k], dc, q2, qq) : dequantise<false>(lev[k], dc, q2, qq));
   }
   __syncthreads();
   if (lane < 48)
@@ -1378,8 +1385,8 @@ __global__ __launch_bounds__(64) void k_decode_recon(int w, int h, int64_t strid
   for (int k = 0; k < 6; k++) {
     const bool ck = (coded >> (5 - k)) & 1;
     const int lev = ck ? coef[gmb * 384 + k * 64 + zpos] : 0;  // IZigzagMatrix
-    const int dq = intra ? dequantise<true>(lev, dc, q, qeven) : dequantise<false>(lev, dc, q, qeven);
-    blk_put(L, k, e, ck ? dq : 0);
+    const int q2 = ck ? 2 * q : 0, qq = ck ? q - (int)qeven : 0;
+    blk_put(L, k, e, intra ? dequantise<true>(lev, dc, q2, qq) : dequantise<false>(lev, dc, q2, qq));
   }
   int pred[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   if (!mt_intra(mt)) predict_row_glb(ref, w, b, mbx, mby, r, mt, m.mvx, m.mvy, pred);
