@@ -5,10 +5,13 @@
 // Execution model: one 64-lane wavefront (one workgroup) per macroblock.
 //   * the 16x16 current luma block and a 46x48-byte window of the previous
 //     reconstruction around it are staged in LDS with 16-byte loads;
-//   * FULL search: lane = (dx, dy-half); each lane slides its column of the
-//     window past the 16 current rows (held in SGPRs) with v_sad_u8, keeping 15
-//     SAD accumulators; the argmin is one wave-wide min over packed
-//     (SAD, scan-order) keys, reproducing FastBME's first-minimum rule;
+//   * FULL search: lane = (dx, dy-half), 15 candidates per lane; a lower bound
+//     on every candidate's SAD from 4x4 sub-block averages (v_lerp_u8 map, four
+//     v_sad_u8 per candidate) prunes all but a handful, which get full SADs;
+//     low-contrast blocks, where nothing prunes, take the dense exhaustive pass
+//     (window rows slid past current rows held in SGPRs).  The argmin is one
+//     wave-wide min over packed (SAD, scan-order) keys, reproducing FastBME's
+//     first-minimum rule;
 //   * TSS: lane = (candidate, row pair); four dependent steps of 8 candidates;
 //   * encode: "row" layout lane = (block, row) for the prediction, the loop
 //     filter (vertical taps exchanged with DPP) and the Chen row/column passes;

@@ -57,6 +57,20 @@ __global__ __launch_bounds__(256) void k(uint32_t seed, int iters, uint32_t* out
         if (OP == 35) asm("v_pk_fma_f32 %0, %1, %2, %3" : "=v"(*(uint64_t*)&a[j & 6]) : "v"(((uint64_t)x << 32) | y), "v"(((uint64_t)y << 32) | x), "v"(*(uint64_t*)&a[j & 6]));
         if (OP == 36) asm("v_lshrrev_b32_e32 %0, 8, %1" : "=v"(a[j]) : "v"(a[j]));
         if (OP == 37) asm("v_sad_u8 %0, %1, %2, %3" : "=v"(a[j]) : "v"(x), "v"(r[(u + j + 3) & 7]), "v"(a[j]));
+        if (OP == 38) asm("v_floor_f32_e32 %0, %1" : "=v"(a[j]) : "v"(a[j]));
+        if (OP == 39) asm("v_trunc_f32_e32 %0, %1" : "=v"(a[j]) : "v"(a[j]));
+        if (OP == 40) asm("v_cvt_f32_ubyte1_e32 %0, %1" : "=v"(a[j]) : "v"(a[j]));
+        if (OP == 41) asm("v_cvt_pk_u8_f32 %0, %1, 1, %2" : "=v"(a[j]) : "v"(x), "v"(a[j]));
+        if (OP == 42) asm("v_med3_f32 %0, %1, %2, %3" : "=v"(a[j]) : "v"(x), "v"(y), "v"(a[j]));
+        if (OP == 43) asm("v_max_f32_e32 %0, %1, %2" : "=v"(a[j]) : "v"(x), "v"(a[j]));
+        if (OP == 44) asm("v_add_f32_e32 %0, %1, %2" : "=v"(a[j]) : "v"(x), "v"(a[j]));
+        if (OP == 45) asm("v_sub_f32_e32 %0, %1, %2" : "=v"(a[j]) : "v"(x), "v"(a[j]));
+        if (OP == 46) asm("v_rndne_f32_e32 %0, %1" : "=v"(a[j]) : "v"(a[j]));
+        if (OP == 47) asm("v_cvt_i32_f32_e32 %0, %1" : "=v"(a[j]) : "v"(a[j]));
+        if (OP == 48) asm("v_cvt_f32_i32_e32 %0, %1" : "=v"(a[j]) : "v"(a[j]));
+        if (OP == 49) asm("v_and_b32_e32 %0, %1, %2" : "=v"(a[j]) : "v"(x), "v"(a[j]));
+        if (OP == 50) asm("v_or_b32_e32 %0, %1, %2" : "=v"(a[j]) : "v"(x), "v"(a[j]));
+        if (OP == 51) asm("v_max_i32_e32 %0, %1, %2" : "=v"(a[j]) : "v"(x), "v"(a[j]));
       }
     asm volatile("" : "+v"(r[0]), "+v"(r[3]));
   }
@@ -132,5 +146,19 @@ int main() {
   run<35, false>("v_pk_fma_f32", d);
   run<36, false>("v_lshrrev_b32_e32", d);
   run<37, false>("v_sad_u8 (3 vgpr)", d);
+  run<38, false>("v_floor_f32", d);
+  run<39, false>("v_trunc_f32", d);
+  run<40, false>("v_cvt_f32_ubyte1", d);
+  run<41, false>("v_cvt_pk_u8_f32", d);
+  run<42, false>("v_med3_f32", d);
+  run<43, false>("v_max_f32", d);
+  run<44, false>("v_add_f32", d);
+  run<45, false>("v_sub_f32", d);
+  run<46, false>("v_rndne_f32", d);
+  run<47, false>("v_cvt_i32_f32", d);
+  run<48, false>("v_cvt_f32_i32", d);
+  run<49, false>("v_and_b32", d);
+  run<50, false>("v_or_b32", d);
+  run<51, false>("v_max_i32", d);
   return 0;
 }
