@@ -96,6 +96,57 @@ def test_motion_estimation_random_cif_vs_oracle(p64, oracle_mod, torch_dev):
             np.testing.assert_array_equal(got[i], exp, err_msg=f"mode {mode} frame {i}")
 
 
+def _adversarial_pictures(w, h):
+    """Luma planes that stress the pruned full search (me_full): ties, flat and
+    low-contrast blocks on both sides of the dense-path threshold, periodic
+    patterns, ramps, saturated blocks, plain noise."""
+    rng = np.random.default_rng(2026)
+    y, x = np.mgrid[0:h, 0:w]
+    out = []
+    tex = rng.integers(0, 256, (h, w)).astype(np.int32)
+    # periodic in x and y (exact ties at every multiple of the period)
+    for px, py in ((4, 4), (8, 2), (3, 5)):
+        base = rng.integers(0, 256, (py, px))
+        out.append(base[y % py, x % px])
+    # low contrast around the dense-path threshold (sub-block ranges ~4..24)
+    for amp in (3, 6, 10, 16):
+        out.append(128 + (tex * amp) // 255 - amp // 2)
+    out.append((x * 255) // (w - 1))                  # ramp
+    out.append(np.where((x // 16 + y // 16) % 2 == 0, 0, 255))  # saturated checkerboard
+    out.append(tex)                                   # noise
+    mixed = tex.copy()
+    mixed[:, : w // 2] = 77
+    out.append(mixed)                                 # half flat, half noise
+    return [np.clip(p, 0, 255).astype(np.uint8).reshape(-1) for p in out]
+
+
+@pytest.mark.parametrize("w,h", [(352, 288), (176, 144)])
+def test_full_search_adversarial_vs_oracle(p64, oracle_mod, torch_dev, w, h):
+    """The lower-bound pruning must never change FastBME's answer (me.c:187-246):
+    each picture against a shifted-and-noised copy of itself and against an
+    unrelated picture, every search limit class."""
+    torch = torch_dev
+    rng = np.random.default_rng(7)
+    pics = _adversarial_pictures(w, h)
+    refs, curs = [], []
+    for p in pics:
+        img = p.reshape(h, w).astype(np.int32)
+        dy, dx = rng.integers(-9, 10, 2)
+        shifted = np.roll(np.roll(img, dy, 0), dx, 1) + rng.integers(-2, 3, img.shape)
+        refs.append(np.clip(shifted, 0, 255).astype(np.uint8).reshape(-1))
+        curs.append(p)
+    refs.append(pics[0])
+    curs.append(pics[-1])
+    cur = dev(torch, np.stack(curs))
+    ref = dev(torch, np.stack(refs))
+    for sl in (31, 15, 7, 2):
+        got = host(p64.MotionEstimation(ref, cur, w, h, mode=1, search_limit=sl, frame_stride=w * h))
+        for i in range(len(curs)):
+            exp = oracle_mod.motion_estimation(refs[i], curs[i], w, h, 1, sl)
+            exp = np.stack([exp[f] for f in exp.dtype.names], axis=1)
+            np.testing.assert_array_equal(got[i], exp, err_msg=f"sl {sl} picture {i}")
+
+
 # ---------------------------------------------------------------------------
 # whole-encoder fixtures, through the batched device API and the host context
 
