@@ -38,10 +38,35 @@ namespace {
 
 // development aid: -DP64_SECTIONS marks kernel phases in the ISA listing
 // (tools/section_census.py counts instructions per phase)
-#ifdef P64_SECTIONS
+#if defined(P64_TIMING)
+// -DP64_TIMING: each SECTION() stores the wave's s_memtime offset from its
+// start into a per-wave slot of g_phase_buf (tools/phase_times.py)
+__device__ uint32_t *g_phase_buf;
+__shared__ uint64_t g_tm_t0;
+__shared__ uint32_t g_tm_gid;
+__device__ __forceinline__ void p64_stamp(int k) {
+  const uint64_t now = __builtin_amdgcn_s_memtime();
+  if (threadIdx.x == 0 && g_phase_buf && g_tm_gid < gridDim.x)  // (kernels without TIMING_BEGIN)
+    g_phase_buf[(size_t)g_tm_gid * 32 + k] = (uint32_t)(now - g_tm_t0);
+}
+#define SECTION(name) p64_stamp(__COUNTER__)
+#define TIMING_BEGIN(gid)                                      \
+  do {                                                         \
+    if (threadIdx.x == 0) {                                    \
+      g_tm_t0 = __builtin_amdgcn_s_memtime();                  \
+      g_tm_gid = (gid);                                        \
+    }                                                          \
+    __syncthreads();                                           \
+  } while (0)
+#define TIMING_END() p64_stamp(31)
+#elif defined(P64_SECTIONS)
 #define SECTION(name) asm volatile(";## " name)
 #else
 #define SECTION(name)
+#endif
+#ifndef TIMING_BEGIN
+#define TIMING_BEGIN(gid)
+#define TIMING_END()
 #endif
 
 // ---------------------------------------------------------------------------
@@ -713,55 +738,42 @@ __device__ __forceinline__ void me_full(MbLds &L, const uint8_t *cur_blk, int w,
     Ts = (T + 512u) >> 4;  // survivors: S <= Ts
 
     SECTION("survivors");
-    // 3. survivors.  Up to 32 of them are listed by walking the ballots in
-    // scalar registers (lane 0 stores the ords); the count decides the path.
+    // 3. survivors: counted with ballots, then (if at most ME_LIST_MAX) their
+    // ords compacted into L.list with mbcnt (no per-survivor scalar loop)
     nsurv = 0;
 #pragma unroll
-    for (int d = 0; d < 15; d++) {
-      uint64_t m = __ballot(acc[d] <= Ts);
-      const int c = __popcll(m);
-      if (nsurv + c <= 32) {
-        int idx = nsurv;
-        while (m) {
-          const int l = __builtin_ctzll(m);
-          m &= m - 1;
-          const unsigned ord = ((unsigned)(l & 31) << 5) + (unsigned)(15 * (l >> 5) + d) + 1u;
-          if (lane == 0) list[idx] = ord;
-          idx++;
+    for (int d = 0; d < 15; d++) nsurv += __popcll(__ballot(acc[d] <= Ts));
+    nsurv = uni(nsurv);
+    if (nsurv <= ME_LIST_MAX) {
+      int pos = 0;
+#pragma unroll
+      for (int d = 0; d < 15; d++) {
+        const bool sv = acc[d] <= Ts;
+        const uint64_t bl = __ballot(sv);
+        if (bl) {
+          const int idx = pos + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bl >> 32),
+                                                               __builtin_amdgcn_mbcnt_lo((uint32_t)bl, 0u));
+          if (sv) list[idx] = base + d;
+          pos += __popcll(bl);
         }
       }
-      nsurv += c;
     }
-    nsurv = uni(nsurv);
   }
 #ifdef P64_ME_STATS
   me_stats_count(lane, nsurv, range);
 #endif
 
   SECTION("finish");
-  if (nsurv <= 32) {
+  if (nsurv <= ME_LIST_MAX) {
     __syncthreads();
     if (nsurv <= 4)
       bk = finish_groups<4>(L, nsurv, lane);
     else if (nsurv <= 8)
       bk = finish_groups<2>(L, nsurv, lane);
-    else
+    else if (nsurv <= 32)
       bk = finish_groups<1>(L, nsurv, lane);
-  } else if (nsurv <= ME_LIST_MAX) {
-    int pos = 0;
-#pragma unroll
-    for (int d = 0; d < 15; d++) {
-      const bool sv = acc[d] <= Ts;
-      const uint64_t bl = __ballot(sv);
-      if (bl) {
-        const int idx = pos + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bl >> 32),
-                                                             __builtin_amdgcn_mbcnt_lo((uint32_t)bl, 0u));
-        if (sv) list[idx] = base + d;
-        pos += __popcll(bl);
-      }
-    }
-    __syncthreads();
-    bk = finish_list(L, nsurv, lane);
+    else
+      bk = finish_list(L, nsurv, lane);
   } else {  // little pruned: every candidate densely, rows in two chunks
     const uint32_t *wrow = L.win + (15 * half) * WIN_WORDS + (colb >> 2);
     const int sh = colb & 3;
@@ -1325,9 +1337,12 @@ __global__ __launch_bounds__(64, ENCODE_WAVES_PER_SIMD) void k_encode(p64gpu_enc
   } else {
     gid = xcd_remap(blockIdx.x, gridDim.x);
   }
+  TIMING_BEGIN(gid);
   const MbFetch f = fetch_mb<MODE>(a, a.cur, gid, lane);
   if (MODE != 0) put_luma(L, f.luma, lane);
+  SECTION("fetched");
   encode_mb<MODE>(a, a.cur, L, lane, gid, f.crow);
+  TIMING_END();
 }
 
 // ME only (MotionEstimation me.c:340-363 over a batch of luma planes)
@@ -1828,6 +1843,12 @@ int p64gpu_encoder_frame(p64gpu_encoder *e, const uint8_t *picture, int intra, i
 
 void p64gpu_encoder_close(p64gpu_encoder *e) { enc_free(e); }
 
+#ifdef P64_TIMING
+int p64gpu_dbg_phase_buffer(uint32_t *dev_buf) {  // [grid][32] uint32, zeroed by the caller
+  HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_phase_buf), &dev_buf, sizeof dev_buf));
+  return 0;
+}
+#endif
 #ifdef P64_ME_STATS
 int p64gpu_dbg_stats(unsigned long long *out, int reset) {  // out[48]
   HIP_TRY(hipDeviceSynchronize());
