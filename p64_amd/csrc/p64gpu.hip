@@ -689,7 +689,7 @@ __device__ __forceinline__ void me_full(MbLds &L, const uint8_t *cur_blk, int w,
   SECTION("cur_map");
   uint32_t cm[4];
   const int range = uni(cur_lb_map(L, lane, cm));
-  unsigned bk = 0xFFFFFFFFu, ckey = 0xFFFFFFFFu, Ts = 0;
+  unsigned bk = 0xFFFFFFFFu, ckey = 0xFFFFFFFFu, Ts = 0, pk = 0;
   uint32_t acc[15];
   lds_u32 *list = as_lds(L.list);  // aliases the map once the map is dead
   int nsurv = 1000;
@@ -722,7 +722,7 @@ __device__ __forceinline__ void me_full(MbLds &L, const uint8_t *cur_blk, int w,
 
     // 2. c* and its full SAD
     SECTION("cstar");
-    unsigned pk = 0xFFFFFFFFu;
+    pk = 0xFFFFFFFFu;
 #pragma unroll
     for (int d = 0; d < 15; d++) pk = min(pk, (acc[d] << KEY_SHIFT) + base + d);
     pk = uni((int)wave_min(pk));
@@ -766,7 +766,10 @@ __device__ __forceinline__ void me_full(MbLds &L, const uint8_t *cur_blk, int w,
   SECTION("finish");
   if (nsurv <= ME_LIST_MAX) {
     __syncthreads();
-    if (nsurv <= 4)
+    // nothing to finish when c* (whose key is known) is the only survivor
+    if (nsurv == 0 || (nsurv == 1 && (unsigned)uni((int)list[0]) == (pk & KEY_ORD)))
+      ;
+    else if (nsurv <= 4)
       bk = finish_groups<4>(L, nsurv, lane);
     else if (nsurv <= 8)
       bk = finish_groups<2>(L, nsurv, lane);
@@ -1168,6 +1171,7 @@ __device__ __forceinline__ CbpOut cbp_decide(const int lev[6]) {
 struct MbFetch {
   LumaFetch luma;  // MODE != 0: search window and current luma
   uint2 crow;      // the lane's row of its block in the current picture
+  int li, q, ov;   // LastIntra, UseQuant and the -o MTYPE override of the MB
 };
 template <int MODE>
 __device__ __forceinline__ MbFetch fetch_mb(const p64gpu_encode_args &a, const uint8_t *cur_all,
@@ -1182,6 +1186,10 @@ __device__ __forceinline__ MbFetch fetch_mb(const p64gpu_encode_args &a, const u
   const uint8_t *cplane = g.plane == 0 ? cur.y : (g.plane == 1 ? cur.u : cur.v);
   MbFetch f;
   f.crow = *reinterpret_cast<const uint2 *>(cplane + (uint32_t)(mul24(g.y + r, pw) + g.x));
+  const size_t gmb = (size_t)fi * nmb + mb;
+  f.li = a.last_intra[gmb];
+  f.q = a.quant_mb ? a.quant_mb[gmb] : a.quant;
+  f.ov = a.mtype_override ? a.mtype_override[gmb] : -1;
   if (MODE != 0)
     f.luma = fetch_luma(a.ref + (size_t)fi * a.frame_stride, cur.y, w, h, 16 * mbx, 16 * mby, lane);
   return f;
@@ -1190,7 +1198,8 @@ __device__ __forceinline__ MbFetch fetch_mb(const p64gpu_encode_args &a, const u
 // one macroblock, its luma already in L (MODE != 0)
 template <int MODE>
 __device__ __forceinline__ void encode_mb(const p64gpu_encode_args &a, const uint8_t *cur_all,
-                                          MbLds &L, int lane, unsigned gid, uint2 crow) {
+                                          MbLds &L, int lane, unsigned gid, const MbFetch &f) {
+  const uint2 crow = f.crow;
   const int w = a.width, h = a.height, mbw = w >> 4, nmb = mbw * (h >> 4);
   const int fi = (int)(gid / (unsigned)nmb), mb = (int)(gid - (unsigned)fi * nmb);
   const int mbx = mb % mbw, mby = mb / mbw, x0 = 16 * mbx, y0 = 16 * mby;
@@ -1223,17 +1232,15 @@ __device__ __forceinline__ void encode_mb(const p64gpu_encode_args &a, const uin
     }
     SECTION("e_decide");
     mt = decide_mtype(me);
-    if (a.mtype_override) {
-      const int ov = a.mtype_override[gmb];
-      if (ov >= 0) mt = ov;
-    }
+    const int ov = uni(f.ov);
+    if (ov >= 0) mt = ov;
     mvx = me.mx;
     mvy = me.my;
   }
-  const uint8_t li = a.last_intra[gmb];
+  const int li = uni(f.li);
   if (li > 131) mt = 0;  // SEQUENCE_INTRA_THRESHOLD (p64.c:159, 772)
   mt = uni(mt);
-  const int q = uni(a.quant_mb ? a.quant_mb[gmb] : a.quant);
+  const int q = uni(f.q);
   const float rq = c_qrecip.r[q];
   const bool qeven = !(q & 1);
   const float rqe = qeven ? rq : 0.0f;
@@ -1341,7 +1348,7 @@ __global__ __launch_bounds__(64, ENCODE_WAVES_PER_SIMD) void k_encode(p64gpu_enc
   const MbFetch f = fetch_mb<MODE>(a, a.cur, gid, lane);
   if (MODE != 0) put_luma(L, f.luma, lane);
   SECTION("fetched");
-  encode_mb<MODE>(a, a.cur, L, lane, gid, f.crow);
+  encode_mb<MODE>(a, a.cur, L, lane, gid, f);
   TIMING_END();
 }
 
