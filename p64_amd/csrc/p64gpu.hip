@@ -319,6 +319,37 @@ __device__ __forceinline__ unsigned xcd_remap(unsigned bid, unsigned n) {
   return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + k;
 }
 
+// macroblock index -> (picture, MB, MB column, MB row) without integer
+// division (a runtime divide is ~25 scalar instructions): q = umulhi(n, m) >> s
+// with s = floor(log2 d) - 1 and m = floor(2^(32+s)/d) + 1 < 2^32 is exact for
+// n < 2^30 and 2 <= d <= 65536, since the excess n (m - 2^(32+s)/d) / 2^(32+s)
+// stays below 1/d.  check_geometry keeps n < 2^30.
+struct MbDiv {
+  uint32_t mn, sn, mw, sw;  // magic and shift for nmb and for mbw
+};
+static inline MbDiv mb_div(int w, int h) {
+  auto magic = [](uint32_t d, uint32_t &m, uint32_t &s) {
+    s = 31 - (uint32_t)__builtin_clz(d);
+    s = s ? s - 1 : 0;
+    m = (uint32_t)((((uint64_t)1) << (32 + s)) / d + 1);
+  };
+  MbDiv k;
+  magic((uint32_t)((w >> 4) * (h >> 4)), k.mn, k.sn);
+  magic((uint32_t)(w >> 4), k.mw, k.sw);
+  return k;
+}
+struct MbPos {
+  int fi, mb, mbx, mby;
+};
+__device__ __forceinline__ MbPos mb_pos(unsigned gid, int nmb, int mbw, const MbDiv &k) {
+  MbPos p;
+  p.fi = (int)(__umulhi(gid, k.mn) >> k.sn);
+  p.mb = (int)(gid - (unsigned)p.fi * (unsigned)nmb);
+  p.mby = (int)(__umulhi((unsigned)p.mb, k.mw) >> k.sw);
+  p.mbx = p.mb - p.mby * mbw;
+  return p;
+}
+
 // ---------------------------------------------------------------------------
 // per-macroblock LDS image
 
@@ -1175,10 +1206,10 @@ struct MbFetch {
 };
 template <int MODE>
 __device__ __forceinline__ MbFetch fetch_mb(const p64gpu_encode_args &a, const uint8_t *cur_all,
-                                            unsigned gid, int lane) {
+                                            unsigned gid, const MbDiv &kd, int lane) {
   const int w = a.width, h = a.height, mbw = w >> 4, nmb = mbw * (h >> 4);
-  const int fi = (int)(gid / (unsigned)nmb), mb = (int)(gid - (unsigned)fi * nmb);
-  const int mbx = mb % mbw, mby = mb / mbw;
+  const MbPos ps = mb_pos(gid, nmb, mbw, kd);
+  const int fi = ps.fi, mb = ps.mb, mbx = ps.mbx, mby = ps.mby;
   const Picture cur = picture_at(cur_all + (size_t)fi * a.frame_stride, w, h);
   const int b = min(lane >> 3, 5), r = lane & 7;
   const BlockGeom g = block_geom(b, mbx, mby);
@@ -1198,11 +1229,12 @@ __device__ __forceinline__ MbFetch fetch_mb(const p64gpu_encode_args &a, const u
 // one macroblock, its luma already in L (MODE != 0)
 template <int MODE>
 __device__ __forceinline__ void encode_mb(const p64gpu_encode_args &a, const uint8_t *cur_all,
-                                          MbLds &L, int lane, unsigned gid, const MbFetch &f) {
+                                          MbLds &L, int lane, unsigned gid, const MbDiv &kd,
+                                          const MbFetch &f) {
   const uint2 crow = f.crow;
   const int w = a.width, h = a.height, mbw = w >> 4, nmb = mbw * (h >> 4);
-  const int fi = (int)(gid / (unsigned)nmb), mb = (int)(gid - (unsigned)fi * nmb);
-  const int mbx = mb % mbw, mby = mb / mbw, x0 = 16 * mbx, y0 = 16 * mby;
+  const MbPos ps = mb_pos(gid, nmb, mbw, kd);
+  const int fi = ps.fi, mb = ps.mb, mbx = ps.mbx, mby = ps.mby, x0 = 16 * mbx, y0 = 16 * mby;
   const size_t gmb = (size_t)fi * nmb + mb;
   const Picture cur = picture_at(cur_all + (size_t)fi * a.frame_stride, w, h);
   const Picture ref = picture_at(a.ref + (size_t)fi * a.frame_stride, w, h);
@@ -1333,7 +1365,8 @@ __device__ __forceinline__ void encode_mb(const p64gpu_encode_args &a, const uin
 #define ENCODE_WAVES_PER_SIMD 1
 #endif
 template <int MODE>
-__global__ __launch_bounds__(64, ENCODE_WAVES_PER_SIMD) void k_encode(p64gpu_encode_args a, const int32_t *mb_list) {
+__global__ __launch_bounds__(64, ENCODE_WAVES_PER_SIMD) void k_encode(p64gpu_encode_args a, const int32_t *mb_list,
+                                                                      MbDiv kd) {
   __shared__ MbLds L;
   const int lane = threadIdx.x;
   unsigned gid;
@@ -1345,23 +1378,24 @@ __global__ __launch_bounds__(64, ENCODE_WAVES_PER_SIMD) void k_encode(p64gpu_enc
     gid = xcd_remap(blockIdx.x, gridDim.x);
   }
   TIMING_BEGIN(gid);
-  const MbFetch f = fetch_mb<MODE>(a, a.cur, gid, lane);
+  const MbFetch f = fetch_mb<MODE>(a, a.cur, gid, kd, lane);
   if (MODE != 0) put_luma(L, f.luma, lane);
   SECTION("fetched");
-  encode_mb<MODE>(a, a.cur, L, lane, gid, f);
+  encode_mb<MODE>(a, a.cur, L, lane, gid, kd, f);
   TIMING_END();
 }
 
 // ME only (MotionEstimation me.c:340-363 over a batch of luma planes)
 template <int MODE>
 __global__ __launch_bounds__(64, ENCODE_WAVES_PER_SIMD) void k_motion(int w, int h, int64_t stride, const uint8_t *ref_y,
-                                               const uint8_t *cur_y, int sl, p64_me_rec *out) {
+                                               const uint8_t *cur_y, int sl, p64_me_rec *out,
+                                               MbDiv kd) {
   __shared__ MbLds L;
   const int lane = threadIdx.x;
   const int mbw = w >> 4, nmb = mbw * (h >> 4);
   const unsigned gid = xcd_remap(blockIdx.x, gridDim.x);
-  const int fi = (int)(gid / (unsigned)nmb), mb = (int)(gid - (unsigned)fi * nmb);
-  const int x0 = 16 * (mb % mbw), y0 = 16 * (mb / mbw);
+  const MbPos ps = mb_pos(gid, nmb, mbw, kd);
+  const int fi = ps.fi, x0 = 16 * ps.mbx, y0 = 16 * ps.mby;
   put_luma(L, fetch_luma(ref_y + (size_t)fi * stride, cur_y + (size_t)fi * stride, w, h, x0, y0, lane),
            lane);
   __syncthreads();
@@ -1385,15 +1419,15 @@ __global__ __launch_bounds__(64) void k_decode_recon(int w, int h, int64_t strid
                                                      const uint8_t *refp, uint8_t *recp,
                                                      const int16_t *coef, const p64_mb_rec *mbr,
                                                      const uint8_t *quant_mb,
-                                                     const uint8_t *coded_mask) {
+                                                     const uint8_t *coded_mask, MbDiv kd) {
   __shared__ MbLds L;
   const int lane = threadIdx.x;
   const int mbw = w >> 4, nmb = mbw * (h >> 4);
   const unsigned gid = xcd_remap(blockIdx.x, gridDim.x);
-  const int fi = (int)(gid / (unsigned)nmb), mb = (int)(gid - (unsigned)fi * nmb);
+  const MbPos ps = mb_pos(gid, nmb, mbw, kd);
+  const int fi = ps.fi, mb = ps.mb, mbx = ps.mbx, mby = ps.mby;
   const size_t gmb = (size_t)fi * nmb + mb;
   if (!coded_mask[gmb]) return;  // whole workgroup exits together
-  const int mbx = mb % mbw, mby = mb / mbw;
   const Picture ref = picture_at(refp + (size_t)fi * stride, w, h);
   uint8_t *rec = recp + (size_t)fi * stride;
   const p64_mb_rec m = mbr[gmb];
@@ -1542,7 +1576,7 @@ int check_geometry(int w, int h, int nframes, int64_t stride, bool luma_only = f
     return fail(P64GPU_E_INVALID, "frame_stride %lld: need >= %lld and a multiple of 16",
                 (long long)stride, (long long)need);
   const int64_t blocks = (int64_t)nframes * (w / 16) * (h / 16);
-  if (blocks > 0x7fffffffLL) return fail(P64GPU_E_INVALID, "too many macroblocks in one call");
+  if (blocks >= (1LL << 30)) return fail(P64GPU_E_INVALID, "too many macroblocks in one call");
   return P64GPU_OK;
 }
 
@@ -1657,9 +1691,11 @@ int p64gpu_motion_estimation(int w, int h, int nframes, int64_t stride, const ui
   const unsigned grid = (unsigned)((int64_t)nframes * (w / 16) * (h / 16));
   hipStream_t st = (hipStream_t)stream;
   if (mode == P64GPU_ME_FULL)
-    hipLaunchKernelGGL(k_motion<2>, dim3(grid), dim3(64), 0, st, w, h, stride, ref_y, cur_y, sl, out);
+    hipLaunchKernelGGL(k_motion<2>, dim3(grid), dim3(64), 0, st, w, h, stride, ref_y, cur_y, sl, out,
+                       mb_div(w, h));
   else
-    hipLaunchKernelGGL(k_motion<1>, dim3(grid), dim3(64), 0, st, w, h, stride, ref_y, cur_y, sl, out);
+    hipLaunchKernelGGL(k_motion<1>, dim3(grid), dim3(64), 0, st, w, h, stride, ref_y, cur_y, sl, out,
+                       mb_div(w, h));
   HIP_TRY(hipGetLastError());
   return P64GPU_OK;
 }
@@ -1701,12 +1737,13 @@ static int encode_launch(const p64gpu_encode_args *a, const int32_t *mb_list, in
   const unsigned grid =
       mb_list ? (unsigned)count : (unsigned)((int64_t)a->nframes * (a->width / 16) * (a->height / 16));
   hipStream_t st = (hipStream_t)stream;
+  const MbDiv kd = mb_div(a->width, a->height);
   if (a->intra)
-    hipLaunchKernelGGL(k_encode<0>, dim3(grid), dim3(64), 0, st, *a, mb_list);
+    hipLaunchKernelGGL(k_encode<0>, dim3(grid), dim3(64), 0, st, *a, mb_list, kd);
   else if (a->me_mode == P64GPU_ME_FULL)
-    hipLaunchKernelGGL(k_encode<2>, dim3(grid), dim3(64), 0, st, *a, mb_list);
+    hipLaunchKernelGGL(k_encode<2>, dim3(grid), dim3(64), 0, st, *a, mb_list, kd);
   else
-    hipLaunchKernelGGL(k_encode<1>, dim3(grid), dim3(64), 0, st, *a, mb_list);
+    hipLaunchKernelGGL(k_encode<1>, dim3(grid), dim3(64), 0, st, *a, mb_list, kd);
   HIP_TRY(hipGetLastError());
   return P64GPU_OK;
 }
@@ -1720,7 +1757,7 @@ int p64gpu_decode_recon(int w, int h, int nframes, int64_t stride, const uint8_t
     return fail(P64GPU_E_INVALID, "NULL buffer");
   const unsigned grid = (unsigned)((int64_t)nframes * (w / 16) * (h / 16));
   hipLaunchKernelGGL(k_decode_recon, dim3(grid), dim3(64), 0, (hipStream_t)stream, w, h, stride,
-                     ref, recon, coef, mb, quant_mb, coded_mask);
+                     ref, recon, coef, mb, quant_mb, coded_mask, mb_div(w, h));
   HIP_TRY(hipGetLastError());
   return P64GPU_OK;
 }
