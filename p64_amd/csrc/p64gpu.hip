@@ -566,12 +566,13 @@ __device__ __forceinline__ void build_lb_map(MbLds &L, int lane) {
     const uint32_t h1 = lerp4(v, align4(from_next_lane_wave(v), v, 1));
     const uint32_t h2 = lerp4(h1, align4(from_next_lane_wave(h1), h1, 2));
     const int y = y0 + t;
-    if (act && y < MAP_ROWS) {
+    if (act && y < MAP_ROWS) {  // bytes 0/2 and, after one shift, 1/3 (ds_write_b8[_d16_hi])
       uint8_t *q = mp + y * MAP_ROW_BYTES;
+      const uint32_t h2s = h2 >> 8;
       q[0] = (uint8_t)h2;
-      q[MAP_PLANE_BYTES] = (uint8_t)(h2 >> 8);
       q[2 * MAP_PLANE_BYTES] = (uint8_t)(h2 >> 16);
-      q[3 * MAP_PLANE_BYTES] = (uint8_t)(h2 >> 24);
+      q[MAP_PLANE_BYTES] = (uint8_t)h2s;
+      q[3 * MAP_PLANE_BYTES] = (uint8_t)(h2s >> 16);
     }
   }
 }
@@ -753,9 +754,12 @@ __device__ __forceinline__ void me_full(MbLds &L, const uint8_t *cur_blk, int w,
 
     // 2. c* and its full SAD
     SECTION("cstar");
-    pk = 0xFFFFFFFFu;
+    {  // least (S, d) of the lane as S << 4 | d, then its key S << 10 | ord
+      unsigned m = 0xFFFFFFFFu;
 #pragma unroll
-    for (int d = 0; d < 15; d++) pk = min(pk, (acc[d] << KEY_SHIFT) + base + d);
+      for (int d = 0; d < 15; d++) m = min(m, (acc[d] << 4) | (unsigned)d);
+      pk = m == 0xFFFFFFFFu ? m : ((m >> 4) << KEY_SHIFT) + base + (m & 15u);
+    }
     pk = uni((int)wave_min(pk));
     if ((pk >> KEY_SHIFT) < ME_INVALID) {  // else nothing is valid
       int cdx, cdy;
@@ -769,26 +773,21 @@ __device__ __forceinline__ void me_full(MbLds &L, const uint8_t *cur_blk, int w,
     Ts = (T + 512u) >> 4;  // survivors: S <= Ts
 
     SECTION("survivors");
-    // 3. survivors: counted with ballots, then (if at most ME_LIST_MAX) their
-    // ords compacted into L.list with mbcnt (no per-survivor scalar loop)
+    // 3. survivors: their ords compacted into L.list with ballot + mbcnt (the
+    // first ME_LIST_MAX of them), counted on the way
     nsurv = 0;
 #pragma unroll
-    for (int d = 0; d < 15; d++) nsurv += __popcll(__ballot(acc[d] <= Ts));
-    nsurv = uni(nsurv);
-    if (nsurv <= ME_LIST_MAX) {
-      int pos = 0;
-#pragma unroll
-      for (int d = 0; d < 15; d++) {
-        const bool sv = acc[d] <= Ts;
-        const uint64_t bl = __ballot(sv);
-        if (bl) {
-          const int idx = pos + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bl >> 32),
+    for (int d = 0; d < 15; d++) {
+      const bool sv = acc[d] <= Ts;
+      const uint64_t bl = __ballot(sv);
+      if (bl) {
+        const int idx = nsurv + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bl >> 32),
                                                                __builtin_amdgcn_mbcnt_lo((uint32_t)bl, 0u));
-          if (sv) list[idx] = base + d;
-          pos += __popcll(bl);
-        }
+        if (sv && idx < ME_LIST_MAX) list[idx] = base + d;
+        nsurv += __popcll(bl);
       }
     }
+    nsurv = uni(nsurv);
   }
 #ifdef P64_ME_STATS
   me_stats_count(lane, nsurv, range);
