@@ -262,16 +262,21 @@ template <int CTRL>
 __device__ __forceinline__ unsigned dpp(unsigned v) {
   return (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xf, 0xf, false);
 }
+// after the row folds every lane of a row holds the row's result; row_bcast:15
+// (rows 1 and 3 take lane 15 of rows 0 and 2) and row_bcast:31 (rows 2 and 3
+// take lane 31) finish the wave in lane 63 -- one v_readlane instead of four
+template <int CTRL, int ROWS>
+__device__ __forceinline__ unsigned dpp_rows(unsigned old, unsigned v) {
+  return (unsigned)__builtin_amdgcn_update_dpp((int)old, (int)v, CTRL, ROWS, 0xf, false);
+}
 __device__ __forceinline__ unsigned wave_min(unsigned v) {
   v = min(v, dpp<0xB1>(v));
   v = min(v, dpp<0x4E>(v));
   v = min(v, dpp<0x141>(v));
   v = min(v, dpp<0x140>(v));
-  const unsigned a = (unsigned)__builtin_amdgcn_readlane((int)v, 0);
-  const unsigned b = (unsigned)__builtin_amdgcn_readlane((int)v, 16);
-  const unsigned c = (unsigned)__builtin_amdgcn_readlane((int)v, 32);
-  const unsigned d = (unsigned)__builtin_amdgcn_readlane((int)v, 48);
-  return min(min(a, b), min(c, d));
+  v = min(v, dpp_rows<0x142, 0xa>(0xFFFFFFFFu, v));
+  v = min(v, dpp_rows<0x143, 0xc>(0xFFFFFFFFu, v));
+  return (unsigned)__builtin_amdgcn_readlane((int)v, 63);
 }
 __device__ __forceinline__ int wave_sum(int v) {
   unsigned u = (unsigned)v;
@@ -279,8 +284,9 @@ __device__ __forceinline__ int wave_sum(int v) {
   u += dpp<0x4E>(u);
   u += dpp<0x141>(u);
   u += dpp<0x140>(u);
-  return __builtin_amdgcn_readlane((int)u, 0) + __builtin_amdgcn_readlane((int)u, 16) +
-         __builtin_amdgcn_readlane((int)u, 32) + __builtin_amdgcn_readlane((int)u, 48);
+  u += dpp_rows<0x142, 0xa>(0u, u);
+  u += dpp_rows<0x143, 0xc>(0u, u);
+  return __builtin_amdgcn_readlane((int)u, 63);
 }
 // a value the compiler cannot see through (nor hoist out of a loop)
 __device__ __forceinline__ int opaque(int v) {
