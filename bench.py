@@ -376,8 +376,8 @@ def main():
                          "peak": round(SAD_PEAK / 1e12, 3), "unit": "T byte-absdiff/s",
                          "frac": round(sad_rate / SAD_PEAK, 4), "candidates_per_mb": cand,
                          "note": "exhaustive-search equivalent: candidates x 256 byte-absdiffs "
-                                 "per MB; the FULL kernel executes fewer (exact partial-"
-                                 "distortion pruning, DESIGN.md)"},
+                                 "per MB; the FULL kernel executes far fewer (exact pruning by a "
+                                 "4x4-average lower bound, DESIGN.md section 5)"},
         "cpu_baseline": cpu,
         "with_vlc": with_vlc,
         "verified_vs_oracle": verified,
