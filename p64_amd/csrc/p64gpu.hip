@@ -875,11 +875,9 @@ __device__ __forceinline__ void me_tss(const MbLds &L, int w, int h, int x0, int
     s += dpp<0x4E>(s);
     s += dpp<0x141>(s);
     // the first least SAD in neighbour order: min of (SAD << 3 | k) over the
-    // eight group leaders, in scalar registers
+    // wave (every lane of a group holds its group's key)
     const unsigned key = ok ? (s << 3) | (unsigned)k : 0xFFFFFFFFu;
-    unsigned m = 0xFFFFFFFFu;
-#pragma unroll
-    for (int j = 0; j < 8; j++) m = min(m, (unsigned)__builtin_amdgcn_readlane((int)key, 8 * j));
+    const unsigned m = wave_min(key);
     if ((m >> 3) < bsad) {
       bsad = m >> 3;
       const int j = (int)(m & 7u), jj = j < 4 ? j : j + 1;
