@@ -63,6 +63,11 @@ def main():
                           me_mode=p64_amd.ME_FULL, search_limit=31, out=out)
     res["decode_recon"] = timed(lambda: p64_amd.decode_recon(r0, d1, out.coef, out.mb, qmb, mask,
                                                              width=w, height=h), a.reps)
+    # entropy coding of that picture batch (count, scan, emit + the bits copy)
+    from p64_amd import stream as p64s
+    gq = torch.full((S, nmb // 33), 8, dtype=torch.uint8, device="cuda")
+    trs = torch.full((S,), 1, dtype=torch.int32, device="cuda")
+    res["vlc"] = timed(lambda: p64s.vlc_pictures(out.mb, out.coef, gq, trs, width=w, height=h), a.reps)
     for k, (med, mn) in res.items():
         print(f"{k:16s} median {med:9.1f} us  min {mn:9.1f} us  {S * nmb / med * 1e6 / 1e6:8.1f} M MB/s")
 
