@@ -345,6 +345,10 @@ def encode_frames(cur, ref, recon, last_intra, *, width: int, height: int, intra
     _dev_check(last_intra, torch.uint8, "last_intra")
     if not intra:
         _dev_check(ref, torch.uint8, "ref")
+    if quant_mb is not None:
+        _dev_check(quant_mb, torch.uint8, "quant_mb")
+    if mtype_override is not None:
+        _dev_check(mtype_override, torch.int8, "mtype_override")
     need = nframes * stride
     nmb_all = nframes * nmb
     if nframes < 1 or recon.numel() < need or last_intra.numel() < nmb_all or \
@@ -357,6 +361,15 @@ def encode_frames(cur, ref, recon, last_intra, *, width: int, height: int, intra
             coef=torch.empty((nframes, nmb, 6, 64), dtype=torch.int16, device=dev),
             mb=torch.empty((nframes, nmb, 4), dtype=torch.int8, device=dev),
             me=torch.empty((nframes, nmb, 7), dtype=torch.int32, device=dev) if want_me else None)
+    else:  # caller-supplied outputs: the kernels write nmb_all records into them
+        _dev_check(out.coef, torch.int16, "out.coef")
+        _dev_check(out.mb, torch.int8, "out.mb")
+        if out.coef.numel() < nmb_all * 384 or out.mb.numel() < nmb_all * 4:
+            raise P64GpuError("out.coef / out.mb smaller than nframes x nmb records")
+        if out.me is not None:
+            _dev_check(out.me, torch.int32, "out.me")
+            if out.me.numel() < nmb_all * 7:
+                raise P64GpuError("out.me smaller than nframes x nmb records")
     a = EncodeArgs(width=width, height=height, nframes=nframes, intra=int(bool(intra)),
                    quant=quant, me_mode=me_mode, search_limit=search_limit, reserved=0,
                    frame_stride=stride, cur=cur.data_ptr(),
@@ -373,6 +386,10 @@ def encode_frames(cur, ref, recon, last_intra, *, width: int, height: int, intra
 def decode_recon(ref, recon, coef, mb, quant_mb, coded_mask, *, width: int, height: int):
     """Decoder reconstruction (p64.c:1179-1237 + 971-1013) of coded MBs into recon."""
     torch = _torch()
+    for t, dt, name in ((ref, torch.uint8, "ref"), (recon, torch.uint8, "recon"),
+                        (coef, torch.int16, "coef"), (mb, torch.int8, "mb"),
+                        (quant_mb, torch.uint8, "quant_mb"), (coded_mask, torch.uint8, "coded_mask")):
+        _dev_check(t, dt, name)
     stride = picture_bytes(width, height)
     nframes = recon.numel() // stride
     nmb_all = nframes * (width // 16) * (height // 16)

@@ -102,7 +102,8 @@ __host__ __device__ constexpr bool mt_tcoeff(int m) { return m != 4 && m != 7; }
 
 // zigzag scan position of natural index n (transform.c:67-75), generated
 struct ZigZag {
-  uint8_t pos[64];
+  uint8_t pos[64];  // natural index -> scan position
+  uint8_t inv[64];  // scan position -> natural index
 };
 constexpr ZigZag make_zigzag() {
   ZigZag z{};
@@ -114,6 +115,7 @@ constexpr ZigZag make_zigzag() {
     else
       for (int r = hi; r >= lo; r--) z.pos[8 * r + s - r] = (uint8_t)k++;
   }
+  for (int n = 0; n < 64; n++) z.inv[z.pos[n]] = (uint8_t)n;
   return z;
 }
 __constant__ ZigZag c_zz = make_zigzag();
@@ -1463,6 +1465,326 @@ __global__ __launch_bounds__(64) void k_decode_recon(int w, int h, int64_t strid
   }
 }
 
+// ---------------------------------------------------------------------------
+// Block layout: one LANE per 8x8 block, the whole block in 64 VGPRs.  For the
+// two HBM-bound paths (intra pictures, decoder reconstruction) this removes
+// every lane exchange: the Chen column and row passes, the zigzag (a register
+// renaming) and the quantisers run in registers, with no LDS and no barrier,
+// and no lane idles (the row layout of k_encode leaves 16 of 64 lanes idle).
+// Thread t of a launch maps to picture t / (6 nmb) and, inside the picture,
+// first the luma blocks in raster order of the 8x8 block grid, then the U and
+// the V blocks in raster order: a wave's 64 lanes read and write 64 adjacent
+// 8-byte row segments (512 contiguous bytes per row instruction), and each
+// lane writes its block's 128 bytes of levels as whole cache lines.
+
+constexpr ZigZag k_zz = make_zigzag();  // compile-time copy for register renaming
+
+// keeps the machine scheduler from interleaving the 8 lines of a pass (it
+// would trade registers for ILP the block layout does not need: other waves
+// hide latency; -DNO_SCHED_FENCE to compare)
+#ifdef NO_SCHED_FENCE
+#define SCHED_FENCE()
+#else
+#define SCHED_FENCE() __builtin_amdgcn_sched_barrier(0)
+#endif
+
+// occupancy hint for the block-layout kernels (-DBLK_WAVES=n: at least n waves
+// per SIMD, i.e. at most 512/n VGPRs)
+#if defined(BLK_WAVES) && BLK_WAVES > 0
+#define BLK_OCC __attribute__((amdgpu_waves_per_eu(BLK_WAVES)))
+#else
+#define BLK_OCC
+#endif
+
+struct BlkDiv {
+  uint32_t mp, sp;  // picture: 6 nmb blocks
+  uint32_t mb, sb;  // luma block row: w/8 blocks
+  uint32_t mw, sw;  // MB row: w/16 MBs
+};
+static inline void magic_div(uint32_t d, uint32_t &m, uint32_t &s) {
+  s = 31 - (uint32_t)__builtin_clz(d);
+  s = s ? s - 1 : 0;
+  m = (uint32_t)((((uint64_t)1) << (32 + s)) / d + 1);
+}
+static inline BlkDiv blk_div(int w, int h) {
+  BlkDiv k;
+  magic_div((uint32_t)(6 * (w >> 4) * (h >> 4)), k.mp, k.sp);
+  magic_div((uint32_t)(w >> 3), k.mb, k.sb);
+  magic_div((uint32_t)(w >> 4), k.mw, k.sw);
+  return k;
+}
+__device__ __forceinline__ unsigned mdiv(unsigned n, uint32_t m, uint32_t s) { return __umulhi(n, m) >> s; }
+
+struct BlkPos {
+  int fi;     // picture in the launch
+  int mb;     // raster macroblock
+  int b;      // block c = 0..5 of the MB (p64.c:77-79)
+  int plane;  // 0 Y, 1 U, 2 V
+  int x, y;   // block origin in its plane
+};
+__device__ __forceinline__ BlkPos blk_pos(unsigned t, int w, int h, const BlkDiv &k) {
+  const int mbw = w >> 4, nmb = mbw * (h >> 4), bw = w >> 3;
+  BlkPos p;
+  p.fi = (int)mdiv(t, k.mp, k.sp);
+  int i = (int)(t - (unsigned)p.fi * (unsigned)(6 * nmb));
+  if (i < 4 * nmb) {  // luma block (bx, by)
+    const int by = (int)mdiv((unsigned)i, k.mb, k.sb), bx = i - by * bw;
+    p.plane = 0;
+    p.x = 8 * bx;
+    p.y = 8 * by;
+    p.mb = (by >> 1) * mbw + (bx >> 1);
+    p.b = ((by & 1) << 1) | (bx & 1);
+  } else {
+    i -= 4 * nmb;
+    const int pl = i >= nmb;
+    i -= pl ? nmb : 0;
+    const int mby = (int)mdiv((unsigned)i, k.mw, k.sw), mbx = i - mby * mbw;
+    p.plane = 1 + pl;
+    p.x = 8 * mbx;
+    p.y = 8 * mby;
+    p.mb = i;
+    p.b = 4 + pl;
+  }
+  return p;
+}
+
+// 64 reconstructed values (already in 0..255) -> 8 row stores
+__device__ __forceinline__ void store_block(uint8_t *dst, int pw, const int v[64]) {
+#pragma unroll
+  for (int k = 0; k < 8; k++) *reinterpret_cast<uint2 *>(dst + (uint32_t)mul24(k, pw)) = pack8(v + 8 * k);
+}
+
+// ChenDct (chendct.c:97-206) on a register block given as its 8 packed pixel
+// rows: column pass (pixels unpacked per column, so the packed rows and the
+// unpacked block are never live together), then row pass; leaves the raw
+// (pre-/8) coefficients in v
+__device__ __forceinline__ void fdct_block(const uint2 rows[8], int v[64]) {
+#pragma unroll
+  for (int c = 0; c < 8; c++) {
+    int x[8], o[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) x[k] = (int)(((c < 4 ? rows[k].x : rows[k].y) >> (8 * (c & 3))) & 255);
+    fwd_col<true>(x, o);
+#pragma unroll
+    for (int k = 0; k < 8; k++) v[8 * k + c] = o[k];
+    SCHED_FENCE();
+  }
+#pragma unroll
+  for (int r = 0; r < 8; r++) {
+    int o[8];
+    fwd_row<true>(v + 8 * r, o);
+#pragma unroll
+    for (int k = 0; k < 8; k++) v[8 * r + k] = o[k];
+    SCHED_FENCE();
+  }
+}
+// ChenIDct (chendct.c:217-375) on a register block: column pass (inputs <<2,
+// folded into the constants), row pass, final rounding
+__device__ __forceinline__ void idct_block(int v[64]) {
+#pragma unroll
+  for (int c = 0; c < 8; c++) {
+    int x[8], o[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) x[k] = v[8 * k + c];
+    inv8<true, 4>(x, o);
+#pragma unroll
+    for (int k = 0; k < 8; k++) v[8 * k + c] = o[k];
+    SCHED_FENCE();
+  }
+#pragma unroll
+  for (int r = 0; r < 8; r++) {
+    int o[8];
+    inv8<true>(v + 8 * r, o);
+#pragma unroll
+    for (int k = 0; k < 8; k++) v[8 * r + k] = idct_final(o[k]);
+    SCHED_FENCE();
+  }
+}
+
+// intra picture (p64.c:635, 770-771: every MB is MTYPE 0, CBP 0x3f), block
+// layout: load -> ChenDct -> BoundDct + CCITTFlatQuantize + FlatBound ->
+// zigzag store -> ICCITTFlatQuantize -> ChenIDct -> BoundIDct -> recon
+__global__ __launch_bounds__(256) BLK_OCC void k_intra_blk(p64gpu_encode_args a, BlkDiv kd, unsigned total) {
+  const unsigned t = blockIdx.x * 256u + threadIdx.x;
+  if (t >= total) return;
+  const int w = a.width, h = a.height, nmb = (w >> 4) * (h >> 4);
+  const BlkPos p = blk_pos(t, w, h, kd);
+  const size_t gmb = (size_t)p.fi * nmb + p.mb;
+  const int pw = p.plane ? w >> 1 : w;
+  const uint32_t off = (uint32_t)(plane_offset(p.plane, w, h) + mul24(p.y, pw) + p.x);
+  const uint8_t *src = a.cur + (size_t)p.fi * a.frame_stride + off;
+  uint2 rows[8];
+#pragma unroll
+  for (int k = 0; k < 8; k++) rows[k] = *reinterpret_cast<const uint2 *>(src + (uint32_t)mul24(k, pw));
+  const int q = a.quant_mb ? a.quant_mb[gmb] : a.quant;
+  const float rq = c_qrecip.r[q];
+  const float rqe = (q & 1) ? 0.0f : rq;
+  const int q2 = 2 * q, qq = q - (int)!(q & 1);
+  int v[64];
+  fdct_block(rows, v);
+  // in scan order: quantise (BoundDct + CCITTFlatQuantize + FlatBound), pack
+  // the level pair, dequantise (ICCITTFlatQuantize) in place; one 16-byte
+  // store per 8 levels, so at most 4 packed words are live
+  uint4 *dst = reinterpret_cast<uint4 *>(a.coef + gmb * 384 + p.b * 64);
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    uint32_t pk[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      int l2[2];
+#pragma unroll
+      for (int i = 0; i < 2; i++) {
+        const int e = k_zz.inv[8 * k + 2 * j + i];
+        const bool dc = e == 0;
+        l2[i] = quantise<true>(v[e], dc ? -0x7fffffff : -1023, dc ? 2047 : 1023, dc, rq, rqe);
+        v[e] = dequantise<true>(l2[i], dc, q2, qq);
+      }
+      pk[j] = (uint32_t)(l2[0] & 0xffff) | ((uint32_t)l2[1] << 16);
+    }
+    dst[k] = make_uint4(pk[0], pk[1], pk[2], pk[3]);
+    SCHED_FENCE();
+  }
+  idct_block(v);
+#pragma unroll
+  for (int e = 0; e < 64; e++) v[e] = clampi(v[e], 0, 255);  // BoundIDctMatrix
+  store_block(a.recon + (size_t)p.fi * a.frame_stride + off, pw, v);
+  if (p.b == 0) {
+    p64_mb_rec o;
+    o.mtype = 0;
+    o.cbp = 0x3f;
+    o.mvx = 0;
+    o.mvy = 0;
+    a.mb[gmb] = o;
+    a.last_intra[gmb] = 0;  // p64.c:909-910
+  }
+}
+
+// The source of an 8x8 prediction at (x, y) of a plane (any byte alignment):
+// three aligned dwords per row; the third is read only when the row is
+// misaligned, so no byte past the row's end is touched
+struct PredSrc {
+  uint32_t d[8][3];
+  int sh;
+};
+__device__ __forceinline__ PredSrc load_pred(const uint8_t *plane, int pw, int x, int y) {
+  const uint8_t *row0 = plane + (uint32_t)(mul24(y, pw) + (x & ~3));
+  PredSrc p;
+  p.sh = x & 3;
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    const uint32_t *s = reinterpret_cast<const uint32_t *>(row0 + (uint32_t)mul24(k, pw));
+    p.d[k][0] = s[0];
+    p.d[k][1] = s[1];
+    p.d[k][2] = p.sh ? s[2] : 0u;
+  }
+  return p;
+}
+__device__ __forceinline__ void pred_row(const PredSrc &p, int r, int s[8]) {
+  unpack8(align4(p.d[r][1], p.d[r][0], p.sh), align4(p.d[r][2], p.d[r][1], p.sh), s);
+}
+// horizontal taps of the H.261 loop filter: [1 2 1], edge columns x4
+__device__ __forceinline__ void hz_row(const PredSrc &p, int r, int hz[8]) {
+  int s[8];
+  pred_row(p, r, s);
+  hz[0] = s[0] << 2;
+#pragma unroll
+  for (int k = 1; k < 7; k++) hz[k] = s[k - 1] + 2 * s[k] + s[k + 1];
+  hz[7] = s[7] << 2;
+}
+// v += prediction, row by row (the loop filter LoadFilterMatrix io.c:323-372
+// when `filter`: separable [1 2 1], rows 0/7 not filtered vertically, one
+// rounding (t + 8) >> 4 as in pred_from_row); three rows of taps live at once
+__device__ __forceinline__ void add_pred(const PredSrc &p, bool filter, int v[64]) {
+  if (filter) {
+    int hp[8], hc[8], hn[8];
+    hz_row(p, 0, hc);
+    hz_row(p, 1, hn);
+#pragma unroll
+    for (int r = 0; r < 8; r++) {
+#pragma unroll
+      for (int k = 0; k < 8; k++)
+        v[8 * r + k] += (r == 0 || r == 7) ? ((hc[k] << 2) + 8) >> 4 : (hp[k] + 2 * hc[k] + hn[k] + 8) >> 4;
+#pragma unroll
+      for (int k = 0; k < 8; k++) {
+        hp[k] = hc[k];
+        hc[k] = hn[k];
+      }
+      if (r + 2 < 8) hz_row(p, r + 2, hn);
+    }
+  } else {
+#pragma unroll
+    for (int r = 0; r < 8; r++) {
+      int s8[8];
+      pred_row(p, r, s8);
+#pragma unroll
+      for (int k = 0; k < 8; k++) v[8 * r + k] += s8[k];
+    }
+  }
+}
+
+// decoder reconstruction (DecompressMDU p64.c:1179-1237 + DecodeSaveMDU
+// p64.c:971-1013), block layout.  MBs whose coded_mask is 0 are left alone.
+// Motion vectors are clamped so that a block's source stays inside its plane:
+// a conforming stream never needs it (H.261 vectors point inside the
+// picture) and a corrupt one cannot make the kernel read outside the buffer.
+__global__ __launch_bounds__(256) BLK_OCC void k_recon_blk(int w, int h, int64_t stride, const uint8_t *refp,
+                                                   uint8_t *recp, const int16_t *coef,
+                                                   const p64_mb_rec *mbr, const uint8_t *quant_mb,
+                                                   const uint8_t *coded_mask, BlkDiv kd, unsigned total) {
+  const unsigned t = blockIdx.x * 256u + threadIdx.x;
+  if (t >= total) return;
+  const int nmb = (w >> 4) * (h >> 4);
+  const BlkPos p = blk_pos(t, w, h, kd);
+  const size_t gmb = (size_t)p.fi * nmb + p.mb;
+  if (!coded_mask[gmb]) return;
+  const uint32_t m = *reinterpret_cast<const uint32_t *>(mbr + gmb);
+  const int mt = (int)(int8_t)(m & 0xff);
+  const int cbp = mt_cbp(mt) ? (int)((m >> 8) & 0x3f) : 0x3f;  // p64.c:1200
+  const bool ck = mt_tcoeff(mt) && ((cbp >> (5 - p.b)) & 1);
+  const int pw = p.plane ? w >> 1 : w, ph = p.plane ? h >> 1 : h;
+  const uint32_t poff = (uint32_t)plane_offset(p.plane, w, h);
+  const bool inter = !mt_intra(mt);
+  PredSrc ps;
+  if (inter) {  // prediction source loads first: in flight during the IDCT
+    int dx = 0, dy = 0;
+    if (mt_mf(mt)) {  // chroma MV/2 with C truncation (io.c:268-270)
+      const int mvx = (int)(int8_t)((m >> 16) & 0xff), mvy = (int)(int8_t)(m >> 24);
+      dx = p.plane ? mvx / 2 : mvx;
+      dy = p.plane ? mvy / 2 : mvy;
+    }
+    const int sx = clampi(p.x + dx, 0, pw - 8), sy = clampi(p.y + dy, 0, ph - 8);
+    ps = load_pred(refp + (size_t)p.fi * stride + poff, pw, sx, sy);
+  }
+  int v[64];
+  if (ck) {  // IZigzagMatrix + ICCITT(Flat)Quantize straight from the packed levels
+    const int q = quant_mb[gmb];
+    const int q2 = 2 * q, qq = q - (int)!(q & 1);
+    const uint4 *src = reinterpret_cast<const uint4 *>(coef + gmb * 384 + p.b * 64);
+    uint4 lq[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) lq[k] = src[k];
+    const bool intra = !inter;
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      const uint32_t w4[4] = {lq[k].x, lq[k].y, lq[k].z, lq[k].w};
+#pragma unroll
+      for (int i = 0; i < 8; i++) {
+        const int l = (i & 1) ? (int)w4[i >> 1] >> 16 : (int)(int16_t)(w4[i >> 1] & 0xffff);
+        const int e = k_zz.inv[8 * k + i];
+        v[e] = intra ? dequantise<true>(l, e == 0, q2, qq) : dequantise<false>(l, false, q2, qq);
+      }
+    }
+    idct_block(v);
+  } else {
+#pragma unroll
+    for (int e = 0; e < 64; e++) v[e] = 0;
+  }
+  if (inter) add_pred(ps, mt_filter(mt), v);
+#pragma unroll
+  for (int e = 0; e < 64; e++) v[e] = clampi(v[e], 0, 255);  // BoundIDctMatrix
+  store_block(recp + (size_t)p.fi * stride + poff + (uint32_t)(mul24(p.y, pw) + p.x), pw, v);
+}
+
 // batched 8x8 block operations (one thread per block; shares the device
 // functions of the fused kernels, full 32-bit arithmetic for arbitrary input)
 __global__ void k_block_op(int op, const int32_t *in, int32_t *out, int64_t nblocks, int dcq,
@@ -1584,6 +1906,17 @@ int check_geometry(int w, int h, int nframes, int64_t stride, bool luma_only = f
 }
 
 bool aligned16(const void *p) { return ((uintptr_t)p & 15) == 0; }
+
+// P64GPU_MB_LAYOUT=1 (read once): intra pictures and decoder reconstruction
+// take the one-wave-per-MB kernels (k_encode<0>, k_decode_recon) instead of
+// the block-layout ones -- an A/B and cross-check switch, same results
+bool mb_layout_forced() {
+  static const bool forced = [] {
+    const char *e = getenv("P64GPU_MB_LAYOUT");
+    return e && *e && *e != '0';
+  }();
+  return forced;
+}
 
 }  // namespace
 
@@ -1741,7 +2074,11 @@ static int encode_launch(const p64gpu_encode_args *a, const int32_t *mb_list, in
       mb_list ? (unsigned)count : (unsigned)((int64_t)a->nframes * (a->width / 16) * (a->height / 16));
   hipStream_t st = (hipStream_t)stream;
   const MbDiv kd = mb_div(a->width, a->height);
-  if (a->intra)
+  const int64_t blocks = 6 * (int64_t)grid;
+  if (a->intra && !mb_list && blocks < (1LL << 30) && !mb_layout_forced()) {
+    hipLaunchKernelGGL(k_intra_blk, dim3((unsigned)((blocks + 255) / 256)), dim3(256), 0, st, *a,
+                       blk_div(a->width, a->height), (unsigned)blocks);
+  } else if (a->intra)
     hipLaunchKernelGGL(k_encode<0>, dim3(grid), dim3(64), 0, st, *a, mb_list, kd);
   else if (a->me_mode == P64GPU_ME_FULL)
     hipLaunchKernelGGL(k_encode<2>, dim3(grid), dim3(64), 0, st, *a, mb_list, kd);
@@ -1758,9 +2095,17 @@ int p64gpu_decode_recon(int w, int h, int nframes, int64_t stride, const uint8_t
   if (s) return s;
   if (!ref || !recon || !coef || !mb || !quant_mb || !coded_mask)
     return fail(P64GPU_E_INVALID, "NULL buffer");
+  if (!aligned16(ref) || !aligned16(recon) || !aligned16(coef) || ((uintptr_t)mb & 3))
+    return fail(P64GPU_E_INVALID, "ref/recon/coef must be 16-byte aligned, mb 4-byte aligned");
   const unsigned grid = (unsigned)((int64_t)nframes * (w / 16) * (h / 16));
-  hipLaunchKernelGGL(k_decode_recon, dim3(grid), dim3(64), 0, (hipStream_t)stream, w, h, stride,
-                     ref, recon, coef, mb, quant_mb, coded_mask, mb_div(w, h));
+  const int64_t blocks = 6 * (int64_t)grid;
+  if (blocks < (1LL << 30) && !mb_layout_forced())
+    hipLaunchKernelGGL(k_recon_blk, dim3((unsigned)((blocks + 255) / 256)), dim3(256), 0,
+                       (hipStream_t)stream, w, h, stride, ref, recon, coef, mb, quant_mb, coded_mask,
+                       blk_div(w, h), (unsigned)blocks);
+  else
+    hipLaunchKernelGGL(k_decode_recon, dim3(grid), dim3(64), 0, (hipStream_t)stream, w, h, stride,
+                       ref, recon, coef, mb, quant_mb, coded_mask, mb_div(w, h));
   HIP_TRY(hipGetLastError());
   return P64GPU_OK;
 }

@@ -722,6 +722,11 @@ int p64s_read_picture(p64s_reader *r, p64s_picture_info *info, p64_mb_rec *mb, u
       if (mdu >= 33) BAD("MDU %d out of range in GOB %d", mdu, gn);
       last_mba = mdu;
       const int k = raster_mb(pi.format, g, mdu);
+      if (MF_MT[mt]) { /* the vector must keep the 16x16 source inside the picture */
+        const int mbw = pi.width / 16, px = 16 * (k % mbw) + r->mvx, py = 16 * (k / mbw) + r->mvy;
+        if (px < 0 || px > pi.width - 16 || py < 0 || py > pi.height - 16)
+          BAD("motion vector (%d,%d) points outside the picture at MB %d", r->mvx, r->mvy, k);
+      }
       mb[k].mtype = (int8_t)mt;
       mb[k].cbp = (int8_t)cbp;
       mb[k].mvx = (int8_t)r->mvx;

@@ -136,3 +136,40 @@ def test_two_rank_root_feed_scatter_gather():
         exp = oracle.encode_frame(176, 144, p64_amd.synth_frame(1 + i, 0, 176, 144), None,
                                   np.zeros(99, np.uint8), intra=True, quant=8)[0]
         np.testing.assert_array_equal(got[i], exp)
+
+
+def _bench_json(out: str) -> dict:
+    import json
+    lines = [ln for ln in out.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out
+    return json.loads(lines[0])
+
+
+def test_bench_launcher_spawns_ranks():
+    """`bench.py --gpus 2` with no external launcher starts two ranks itself
+    (torch.distributed.run as a child, before any device call); the dry mode
+    replaces the GPU step by a host stand-in.  The JSON line reports n_gpus 2,
+    the MAX over ranks (rank 1 is slower) and disjoint sequence ranges."""
+    import subprocess
+    import sys
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--dry", "--gpus", "2",
+                        "--steps", "20", "--streams", "8"],
+                       capture_output=True, text=True, timeout=240, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = _bench_json(r.stdout)
+    assert d["n_gpus"] == 2 and d["dry"] is True
+    assert d["seed_ranges"] == [[1, 8], [9, 16]]
+    assert d["elapsed_max_s"] >= 20 * 0.002  # rank 1's 2 ms steps bound the MAX
+    assert abs(d["value"] - 2 * 8 * 396 * 20 / d["elapsed_max_s"]) < 1e-6 * d["value"]
+
+
+def test_bench_refuses_world_mismatch():
+    """Under a launcher whose world size differs from --gpus, bench.py exits
+    non-zero instead of mislabelling the line."""
+    import subprocess
+    import sys
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--dry", "--gpus", "2",
+                        "--steps", "2"], capture_output=True, text=True, timeout=120, env=env)
+    assert r.returncode != 0 and "refusing" in r.stderr + r.stdout

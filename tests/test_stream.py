@@ -94,13 +94,16 @@ def test_reader_round_trip(p64, st, name):
         assert not p.coef[~mask].any()
 
 
-def random_records(p64, rng, nmb, *, mtypes=range(10)):
+def random_records(p64, rng, nmb, width, height, *, mtypes=range(10)):
     mt = rng.choice(list(mtypes), nmb).astype(np.int8)
     mb = np.zeros(nmb, p64.MB_DTYPE)
     mb["mtype"] = mt
     mb["cbp"] = rng.integers(1, 64, nmb)
-    mb["mvx"] = rng.integers(-15, 16, nmb)
-    mb["mvy"] = rng.integers(-15, 16, nmb)
+    # vectors keep the 16x16 source inside the picture (the reader rejects others)
+    x0 = 16 * (np.arange(nmb) % (width // 16))
+    y0 = 16 * (np.arange(nmb) // (width // 16))
+    mb["mvx"] = np.clip(rng.integers(-15, 16, nmb), -x0, width - 16 - x0)
+    mb["mvy"] = np.clip(rng.integers(-15, 16, nmb), -y0, height - 16 - y0)
     coef = np.zeros((nmb, 6, 64), np.int16)
     for k in range(nmb):
         for c in range(6):
@@ -128,7 +131,7 @@ def test_round_trip_escapes_mquant_and_mv_prediction(p64, st):
         nmb = w.nmb
         sent = []
         for t in range(3):
-            mb, coef = random_records(p64, rng, nmb)
+            mb, coef = random_records(p64, rng, nmb, w.width, w.height)
             qm = rng.integers(1, 32, nmb).astype(np.uint8)
             gq = rng.integers(1, 32, w.ngob).astype(np.uint8)
             w.write_picture(5 * t + 30, mb, coef, gq, quant_mb=qm)
@@ -245,6 +248,30 @@ def test_reader_rejects_garbage(p64, st):
     r = st.Reader(b.bytes() + b"\x00\x00")
     with pytest.raises(p64.P64GpuError, match="bitstream"):
         r.read()
+
+
+def test_reader_rejects_vectors_outside_the_picture(p64, st):
+    """A vector that would fetch the 16x16 prediction from outside the picture
+    (H.261 forbids it; a conforming encoder never sends it) is a stream error,
+    so a hostile stream cannot steer the GPU reconstruction out of bounds."""
+    for mbx, mby, mvx, mvy in ((0, 0, -1, 0), (0, 0, 0, -3), (10, 8, 1, 0), (10, 8, 0, 15),
+                               (5, 4, -15, 15), (5, 4, 15, -15), (0, 8, 0, 0)):
+        mb = np.zeros(99, p64.MB_DTYPE)
+        mb["mtype"] = 2          # inter, zero vector, CBP: one coded level per MB
+        mb["cbp"] = 32
+        coef = np.zeros((99, 6, 64), np.int16)
+        coef[:, 0, 0] = 1
+        k = mby * 11 + mbx
+        mb[k] = (4, 0, mvx, mvy)  # MC without coefficients
+        w = st.Writer(st.QCIF)
+        w.write_picture(0, mb, coef, 8)
+        r = st.Reader(w.end(1))
+        x, y = 16 * mbx + mvx, 16 * mby + mvy
+        if 0 <= x <= 176 - 16 and 0 <= y <= 144 - 16:
+            assert tuple(r.read().mb[k])[2:] == (mvx, mvy)
+        else:
+            with pytest.raises(p64.P64GpuError, match="outside the picture"):
+                r.read()
 
 
 def test_writer_rejects_bad_records(p64, st):
