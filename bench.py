@@ -104,6 +104,8 @@ def parse(argv=None):
                    help="local: every rank generates its own sequences (default, no data-path "
                         "collective); root: rank 0 holds all inputs, RCCL-scatters each step's "
                         "pictures and gathers the levels/records back (the timed step includes both)")
+    p.add_argument("--eager", action="store_true",
+                   help="launch every timed step from Python instead of replaying a captured HIP graph")
     p.add_argument("--dry", action="store_true",
                    help="no device: gloo + a host stand-in step (launcher/reduction tests)")
     p.add_argument("--pmc-json", default=os.path.join(REPO, "profiles", "pmc_traffic.json"))
@@ -332,25 +334,10 @@ def load_pmc(path, workload_key):
         return None
 
 
-class LaunchTimer:
-    """HIP events around each timed launch on torch's current stream (the
-    library launches on it), so collectives in the step are not counted."""
-
-    def __init__(self, torch, n):
-        self.ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-                   for _ in range(n)]
-        self.k = 0
-
-    def __enter__(self):
-        self.ev[self.k][0].record()
-
-    def __exit__(self, *exc):
-        self.ev[self.k][1].record()
-        self.k += 1
-
-    def avg_s(self):
-        ts = [a.elapsed_time(b) * 1e-3 for a, b in self.ev[:self.k]]
-        return sum(ts) / len(ts)
+def timing_note(args, root=False):
+    if args.eager or root:
+        return "HIP events around each launch (kernel + launch gap)"
+    return "HIP events around the replay of a graph of the K launches, / K (includes the inter-kernel boundary)"
 
 
 def roofline(bytes_per_launch, kavg, kernel, pmc=None, **extra):
@@ -366,19 +353,55 @@ def roofline(bytes_per_launch, kavg, kernel, pmc=None, **extra):
 # ---------------------------------------------------------------------------
 # the timed configurations
 
-def timed_loop(torch, dist, world, steps, step_fn, t_first):
-    """Barrier + synchronize, K steps, synchronize + barrier; returns wall s."""
+def timed_region(torch, dist, world, steps, t_first, launch, pre=None, post=None, graph=True):
+    """The K timed steps, bracketed by barrier + synchronize on both sides.
+
+    launch(t) issues step t's kernel on torch's current stream (the library
+    launches on it).  graph=True captures the K launches once into a HIP graph
+    (torch.cuda.CUDAGraph) and times its replay: the kernels run back to back
+    with no host launch cost between them (a step of the intra or decode
+    config is shorter than a Python launch).  Eagerly (graph=False, and always
+    when pre/post collectives are part of the step) each launch is bracketed by
+    its own events, so collectives do not count as kernel time.
+    Returns (wall seconds of the timed region, mean kernel seconds per step)."""
+    if pre is not None or post is not None:
+        graph = False
+    g = None
+    if graph:
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            for k in range(steps):
+                launch(t_first + k)
+        torch.cuda.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(1 if graph else steps)]
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for k in range(steps):
-        step_fn(t_first + k)
+    if graph:
+        ev[0][0].record()
+        g.replay()
+        ev[0][1].record()
+    else:
+        for k in range(steps):
+            t = t_first + k
+            if pre is not None:
+                pre(t)
+            ev[k][0].record()
+            launch(t)
+            ev[k][1].record()
+            if post is not None:
+                post(t)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    return time.perf_counter() - t0
+    elapsed = time.perf_counter() - t0
+    kern = sum(a.elapsed_time(b) for a, b in ev) * 1e-3 / steps
+    del g
+    return elapsed, kern
 
 
 def decode_bytes(torch, mb, nmb_all):
@@ -460,28 +483,29 @@ def main(argv=None):
         coef_all = torch.empty((ncoef, S, nmb, 6, 64), dtype=torch.int16, device="cuda")
         mb_all = torch.empty((ncoef, S, nmb, 4), dtype=torch.int8, device="cuda")
         me = torch.empty((S, nmb, 7), dtype=torch.int32, device="cuda")
-        lt = LaunchTimer(torch, args.steps)
-        timing = [False]
-
         def out_of(t):
             i = slot(t) if keep else 0
             return p64_amd.FrameBatchOut(coef=coef_all[i], mb=mb_all[i], me=me)
 
-        def step(t):
-            if root:
-                scatter_pictures(world, rank, all_frames[slot(t)] if rank == 0 else None,
-                                 frames[slot(t)])
-            o = out_of(t)
-            if timing[0]:
-                lt.__enter__()
+        def pre(t):  # --feed root: this step's pictures from rank 0
+            scatter_pictures(world, rank, all_frames[slot(t)] if rank == 0 else None, frames[slot(t)])
+
+        def launch(t):
             p64_amd.encode_frames(frames[slot(t)].reshape(-1), rec[(t + 1) % 2], rec[t % 2], li,
                                   width=w, height=h, intra=(t == 0), quant=args.quant,
-                                  me_mode=mode, search_limit=args.search_limit, out=o)
-            if timing[0]:
-                lt.__exit__()
+                                  me_mode=mode, search_limit=args.search_limit, out=out_of(t))
+
+        def post(t):  # --feed root: levels and records back to rank 0
+            o = out_of(t)
+            gather_outputs(world, rank, o.coef, coef_bufs)
+            gather_outputs(world, rank, o.mb, mb_bufs)
+
+        def step(t):
             if root:
-                gather_outputs(world, rank, o.coef, coef_bufs)
-                gather_outputs(world, rank, o.mb, mb_bufs)
+                pre(t)
+            launch(t)
+            if root:
+                post(t)
 
         for t in range(1 + args.warmup):  # intra picture + warmup, untimed
             step(t)
@@ -492,11 +516,10 @@ def main(argv=None):
             o = out_of(vt)
             snap = (o.coef[0].cpu().numpy(), o.mb[0].cpu().numpy(), me[0].cpu().numpy(),
                     rec[vt % 2][:pic].cpu().numpy())
-        timing[0] = True
         t_first = 1 + args.warmup
-        elapsed = timed_loop(torch, dist, world, args.steps, step, t_first)
-        timing[0] = False
-        kavg = lt.avg_s()
+        elapsed, kavg = timed_region(torch, dist, world, args.steps, t_first, launch,
+                                     pre if root else None, post if root else None,
+                                     graph=not args.eager)
         tmax = max_over_ranks(elapsed, world, device="cuda")
         last = t_first + args.steps - 1
 
@@ -567,7 +590,7 @@ def main(argv=None):
                                        f"dp{world} (rank 0 RCCL-scatters pictures, gathers levels "
                                        f"+ records; roofline times the encode launch alone)")},
             "roofline": roofline(mbs_launch * BYTES_PER_MB, kavg, kernel, pmc,
-                                 algorithmic_bytes_per_mb=BYTES_PER_MB),
+                                 algorithmic_bytes_per_mb=BYTES_PER_MB, timing=timing_note(args, root)),
             "roofline_sad": {"bound": "valu", "achieved": round(sad_rate / 1e12, 3),
                              "peak": round(SAD_PEAK / 1e12, 3), "unit": "T byte-absdiff/s",
                              "frac": round(sad_rate / SAD_PEAK, 4), "candidates_per_mb": cand,
@@ -657,23 +680,14 @@ def run_intra(args, torch, dist, np, p64_amd, world, frames, S, nmb, pic, nslots
     li = torch.zeros(S * nmb, dtype=torch.uint8, device="cuda")
     out = p64_amd.FrameBatchOut(coef=torch.empty((S, nmb, 6, 64), dtype=torch.int16, device="cuda"),
                                 mb=torch.empty((S, nmb, 4), dtype=torch.int8, device="cuda"), me=None)
-    lt = LaunchTimer(torch, args.steps)
-    timing = [False]
-
     def step(t):
-        if timing[0]:
-            lt.__enter__()
         p64_amd.encode_frames(frames[t % nslots].reshape(-1), None, rec, li, width=w, height=h,
                               intra=True, quant=args.quant, out=out)
-        if timing[0]:
-            lt.__exit__()
 
     for t in range(args.warmup):
         step(t)
-    timing[0] = True
-    elapsed = timed_loop(torch, dist, world, args.steps, step, args.warmup)
-    timing[0] = False
-    kavg = lt.avg_s()
+    elapsed, kavg = timed_region(torch, dist, world, args.steps, args.warmup, step,
+                                 graph=not args.eager)
     tmax = max_over_ranks(elapsed, world, device="cuda")
     last = args.warmup + args.steps - 1
     verified = None
@@ -696,7 +710,7 @@ def run_intra(args, torch, dist, np, p64_amd, world, frames, S, nmb, pic, nslots
                        "distinct_input_pictures": nslots},
             "roofline": roofline(mbs * INTRA_BYTES_PER_MB, kavg, "k_intra_blk",
                                  load_pmc(args.pmc_json, key),
-                                 algorithmic_bytes_per_mb=INTRA_BYTES_PER_MB),
+                                 algorithmic_bytes_per_mb=INTRA_BYTES_PER_MB, timing=timing_note(args)),
             "verified_vs_oracle": verified}
 
 
@@ -732,27 +746,18 @@ def run_decode(args, torch, dist, np, p64_amd, world, enc, S, nmb, pic):
     qmb = torch.full((S * nmb,), args.quant, dtype=torch.uint8, device="cuda")
     mask = torch.ones(S * nmb, dtype=torch.uint8, device="cuda")
     dec = [torch.zeros(S * pic, dtype=torch.uint8, device="cuda") for _ in range(2)]
-    lt = LaunchTimer(torch, args.steps)
-    timing = [False]
     nbytes = []
 
     def step(t):
-        if timing[0]:
-            lt.__enter__()
         p64_amd.decode_recon(dec[(t + 1) % 2], dec[t % 2], enc["coef"][t], enc["mb"][t], qmb, mask,
                              width=w, height=h)
-        if timing[0]:
-            lt.__exit__()
 
     first = last - args.steps + 1
     for t in range(first):  # pictures before the timed ones, untimed
         step(t)
     for t in range(first, last + 1):
         nbytes.append(decode_bytes(torch, enc["mb"][t], S * nmb))
-    timing[0] = True
-    elapsed = timed_loop(torch, dist, world, args.steps, step, first)
-    timing[0] = False
-    kavg = lt.avg_s()
+    elapsed, kavg = timed_region(torch, dist, world, args.steps, first, step, graph=not args.eager)
     tmax = max_over_ranks(elapsed, world, device="cuda")
     ok = bool(torch.equal(dec[last % 2], enc["recon_last"]))
     if not all_ranks_ok(ok, world, device="cuda"):
@@ -767,7 +772,7 @@ def run_decode(args, torch, dist, np, p64_amd, world, enc, S, nmb, pic):
                                    f"{args.content}), {S} sequences/GPU, closed loop",
                        "macroblocks_per_step_per_gpu": mbs},
             "roofline": roofline(bpl, kavg, "k_recon_blk", load_pmc(args.pmc_json, key),
-                                 algorithmic_bytes_per_mb=round(bpl / mbs, 1)),
+                                 algorithmic_bytes_per_mb=round(bpl / mbs, 1), timing=timing_note(args)),
             "verified_vs_encoder": {"ok": ok, "note": "last decoded picture == encoder "
                                                       "reconstruction, all sequences"}}
 

@@ -1603,29 +1603,121 @@ __device__ __forceinline__ void idct_block(int v[64]) {
 
 // intra picture (p64.c:635, 770-771: every MB is MTYPE 0, CBP 0x3f), block
 // layout: load -> ChenDct -> BoundDct + CCITTFlatQuantize + FlatBound ->
-// zigzag store -> ICCITTFlatQuantize -> ChenIDct -> BoundIDct -> recon
-__global__ __launch_bounds__(256) BLK_OCC void k_intra_blk(p64gpu_encode_args a, BlkDiv kd, unsigned total) {
-  const unsigned t = blockIdx.x * 256u + threadIdx.x;
-  if (t >= total) return;
-  const int w = a.width, h = a.height, nmb = (w >> 4) * (h >> 4);
-  const BlkPos p = blk_pos(t, w, h, kd);
-  const size_t gmb = (size_t)p.fi * nmb + p.mb;
-  const int pw = p.plane ? w >> 1 : w;
-  const uint32_t off = (uint32_t)(plane_offset(p.plane, w, h) + mul24(p.y, pw) + p.x);
-  const uint8_t *src = a.cur + (size_t)p.fi * a.frame_stride + off;
-  uint2 rows[8];
+// zigzag store -> ICCITTFlatQuantize -> ChenIDct -> BoundIDct -> recon.
+// Persistent: a lane walks blocks t, t + stride, ... and issues the loads of
+// its next block before transforming the current one, so every wave keeps
+// HBM reads in flight under its own VALU work (without it the waves of a round
+// load, compute and store in lock step and the memory system idles while they
+// compute).
+// Levels leave through LDS: a lane's block is 128 bytes of levels, and 64
+// lanes storing their own 16-byte pieces touch 64 cache lines per store
+// instruction (measured: the level stores alone took 44 us of the 63 us a
+// load/store-only version of the intra kernel needed).  Each wave writes its
+// 64 blocks' levels to its own LDS slot, then store instruction k writes
+// blocks 8k..8k+7 with 8 lanes per block: whole 128-byte lines.
+// output stores of the block-layout kernels (-DBLK_NT: non-temporal, probe)
+template <typename T>
+__device__ __forceinline__ void st_out(T *p, const T &v) {
+#if defined(BLK_NT)
+  typedef unsigned int u32 __attribute__((ext_vector_type(sizeof(T) / 4)));
+  __builtin_nontemporal_store(__builtin_bit_cast(u32, v), reinterpret_cast<u32 *>(p));
+#else
+  *p = v;
+#endif
+}
+constexpr int LVL_STRIDE = 144;  // bytes per lane: 128 + 16 pad, conflict-free ds_write_b128
+constexpr int LVL_WAVE = 64 * LVL_STRIDE;
+__device__ __forceinline__ void put_levels(uint8_t *lds, int lane, int k, uint4 v) {
+  *reinterpret_cast<uint4 *>(lds + lane * LVL_STRIDE + k * 16) = v;
+}
+// my_off: byte offset of the lane's own block in the level array
+__device__ __forceinline__ void flush_levels(const uint8_t *lds, int lane, uint32_t my_off, uint8_t *coef) {
+  __builtin_amdgcn_wave_barrier();
 #pragma unroll
-  for (int k = 0; k < 8; k++) rows[k] = *reinterpret_cast<const uint2 *>(src + (uint32_t)mul24(k, pw));
-  const int q = a.quant_mb ? a.quant_mb[gmb] : a.quant;
-  const float rq = c_qrecip.r[q];
+  for (int k = 0; k < 8; k++) {
+    const int blk = 8 * k + (lane >> 3), ch = lane & 7;
+    const uint32_t off = (uint32_t)__shfl((int)my_off, blk);
+    const uint4 v = *reinterpret_cast<const uint4 *>(lds + blk * LVL_STRIDE + ch * 16);
+    st_out(reinterpret_cast<uint4 *>(coef + off + ch * 16), v);
+  }
+  __builtin_amdgcn_wave_barrier();
+}
+
+// dword 3 of a raw buffer resource on gfx9-family parts (CDNA): 32-bit data format
+constexpr int BUF_RSRC_W3 = 0x00020000;
+
+struct IntraFetch {
+  BlkPos p;
+  uint2 rows[8];  // the block's pixels
+  int q;          // UseQuant
+};
+__device__ __forceinline__ IntraFetch intra_fetch(const p64gpu_encode_args &a, const BlkDiv &kd,
+                                                  unsigned t) {
+  const int w = a.width, h = a.height, nmb = (w >> 4) * (h >> 4);
+  IntraFetch f;
+  f.p = blk_pos(t, w, h, kd);
+  const int pw = f.p.plane ? w >> 1 : w;
+  const uint8_t *src = a.cur + (size_t)f.p.fi * a.frame_stride +
+                       (uint32_t)(plane_offset(f.p.plane, w, h) + mul24(f.p.y, pw) + f.p.x);
+#pragma unroll
+  for (int k = 0; k < 8; k++) f.rows[k] = *reinterpret_cast<const uint2 *>(src + (uint32_t)mul24(k, pw));
+  // UseQuant through a buffer load that is out of range (reads 0, touches no
+  // memory) when there is no per-MB array: no branch around the load, so the
+  // wait counts of the loop stay exact (a conditional load made hipcc wait
+  // for the previous block's stores before every block)
+  const __amdgpu_buffer_rsrc_t qr = __builtin_amdgcn_make_buffer_rsrc(
+      (void *)(a.quant_mb ? a.quant_mb : a.cur), (short)0, a.quant_mb ? 0x7fffffff : 0, BUF_RSRC_W3);
+  const int ql = __builtin_amdgcn_raw_buffer_load_b8(qr, (int)(f.p.fi * nmb + f.p.mb), 0, 0);
+  f.q = ql + (a.quant_mb ? 0 : a.quant);  // (an add, not a select: the load always issues)
+  return f;
+}
+// A block's outputs between its computation and its stores: the persistent
+// kernel stores block i in the middle of block i+1's computation (after its
+// forward transform), so the waves' stores drain while they compute instead of
+// in one burst at the end of every block.
+struct IntraOut {
+  uint2 rec[8];     // reconstructed rows
+  uint32_t rec_off; // byte offset of the block's first row from a.recon
+  uint32_t lvl_off; // byte offset of its levels from a.coef
+  uint32_t gmb;     // its macroblock in the launch
+  int pw;           // its plane's width
+};
+__device__ __forceinline__ void intra_store(const p64gpu_encode_args &a, const IntraOut &o, const uint8_t *lds,
+                                            int lane) {
+  flush_levels(lds, lane, o.lvl_off, reinterpret_cast<uint8_t *>(a.coef));
+#pragma unroll
+  for (int k = 0; k < 8; k++)
+    st_out(reinterpret_cast<uint2 *>(a.recon + o.rec_off + (uint32_t)mul24(k, o.pw)), o.rec[k]);
+  // the MB's record and LastIntra (p64.c:909-910) from all six of its lanes
+  // (identical bytes): no branch around a store, so the wait counts of the
+  // persistent loop stay exact
+  p64_mb_rec r;
+  r.mtype = 0;
+  r.cbp = 0x3f;
+  r.mvx = 0;
+  r.mvy = 0;
+  a.mb[o.gmb] = r;
+  a.last_intra[o.gmb] = 0;
+}
+// one block: ChenDct, [the previous block's stores], quantise + zigzag into
+// the LDS staging, dequantise, ChenIDct, reconstruction into `out`
+template <bool PENDING>
+__device__ __forceinline__ void intra_block(const p64gpu_encode_args &a, const IntraFetch &f, uint8_t *lds,
+                                            int lane, IntraOut &out) {
+  const int w = a.width, h = a.height, nmb = (w >> 4) * (h >> 4);
+  const BlkPos &p = f.p;
+  const uint32_t gmb = (uint32_t)(p.fi * nmb + p.mb);
+  const int q = f.q;
+  // c_qrecip.r[q] computed in place (no dependent table load in the loop)
+  const float rq = __builtin_bit_cast(float, __builtin_bit_cast(uint32_t, 1.0f / (float)(2 * q)) + 1u);
   const float rqe = (q & 1) ? 0.0f : rq;
   const int q2 = 2 * q, qq = q - (int)!(q & 1);
   int v[64];
-  fdct_block(rows, v);
+  fdct_block(f.rows, v);
+  if (PENDING) intra_store(a, out, lds, lane);
   // in scan order: quantise (BoundDct + CCITTFlatQuantize + FlatBound), pack
-  // the level pair, dequantise (ICCITTFlatQuantize) in place; one 16-byte
-  // store per 8 levels, so at most 4 packed words are live
-  uint4 *dst = reinterpret_cast<uint4 *>(a.coef + gmb * 384 + p.b * 64);
+  // the level pair, dequantise (ICCITTFlatQuantize) in place; 16 bytes of
+  // levels at a time into the wave's LDS staging
 #pragma unroll
   for (int k = 0; k < 8; k++) {
     uint32_t pk[4];
@@ -1641,44 +1733,103 @@ __global__ __launch_bounds__(256) BLK_OCC void k_intra_blk(p64gpu_encode_args a,
       }
       pk[j] = (uint32_t)(l2[0] & 0xffff) | ((uint32_t)l2[1] << 16);
     }
-    dst[k] = make_uint4(pk[0], pk[1], pk[2], pk[3]);
+    put_levels(lds, lane, k, make_uint4(pk[0], pk[1], pk[2], pk[3]));
     SCHED_FENCE();
   }
   idct_block(v);
 #pragma unroll
   for (int e = 0; e < 64; e++) v[e] = clampi(v[e], 0, 255);  // BoundIDctMatrix
-  store_block(a.recon + (size_t)p.fi * a.frame_stride + off, pw, v);
-  if (p.b == 0) {
-    p64_mb_rec o;
-    o.mtype = 0;
-    o.cbp = 0x3f;
-    o.mvx = 0;
-    o.mvy = 0;
-    a.mb[gmb] = o;
-    a.last_intra[gmb] = 0;  // p64.c:909-910
+#pragma unroll
+  for (int k = 0; k < 8; k++) out.rec[k] = pack8(v + 8 * k);
+  out.pw = p.plane ? w >> 1 : w;
+  out.rec_off = (uint32_t)((int64_t)p.fi * a.frame_stride) + (uint32_t)plane_offset(p.plane, w, h) +
+                (uint32_t)mul24(p.y, out.pw) + (uint32_t)p.x;
+  out.lvl_off = (gmb * 6 + (uint32_t)p.b) * 128;
+  out.gmb = gmb;
+}
+// -DBLK_PERSIST=1: a persistent grid with the next block's fetch in flight
+// (measured slower: 66 vs 61 us per CIF S=256 launch; the persistent grid fits
+// only 2 waves per SIMD, the one-block-per-lane grid 3)
+#ifndef BLK_PERSIST
+#define BLK_PERSIST 0
+#endif
+// one launch covers at most 2 GiB of pictures and of levels (the host splits
+// larger batches), so 32-bit offsets address both
+__global__ __launch_bounds__(256) BLK_OCC void k_intra_blk(p64gpu_encode_args a, BlkDiv kd, unsigned total,
+                                                           unsigned stride) {
+  __shared__ __align__(16) uint8_t lvl[4 * LVL_WAVE];
+  const int lane = threadIdx.x & 63;
+  uint8_t *lds = lvl + (threadIdx.x >> 6) * LVL_WAVE;
+  // lanes past the end redo the last block (identical stores): every lane of
+  // a wave takes part in the level staging, every wave walks its blocks with
+  // a wave-uniform trip count
+  unsigned t = blockIdx.x * 256u + (threadIdx.x & ~63u);  // the wave's first block
+  if (t >= total) return;
+  const unsigned last = total - 1;
+#if defined(P64_TIMING)  // development probe: each wave's start/end shader and real clocks
+  const uint64_t clk0 = __builtin_amdgcn_s_memtime(), rt0 = __builtin_amdgcn_s_memrealtime();
+  uint64_t rtl = 0, rtc = 0;
+#define CLOCK_END()                                                                        \
+  do {                                                                                     \
+    const uint64_t c1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime(); \
+    if (lane == 0 && g_phase_buf) {                                                        \
+      uint32_t *o = g_phase_buf + (size_t)((blockIdx.x * 256u + threadIdx.x) >> 6) * 8;   \
+      o[0] = (uint32_t)rt0;                                                                \
+      o[1] = (uint32_t)r1;                                                                 \
+      o[2] = (uint32_t)(c1 - clk0);                                                        \
+      o[3] = (uint32_t)rtl;                                                                \
+      o[4] = (uint32_t)rtc;                                                                \
+    }                                                                                      \
+  } while (0)
+#define CLOCK_MARK(v) v = __builtin_amdgcn_s_memrealtime()
+#else
+#define CLOCK_END()
+#define CLOCK_MARK(v)
+#endif
+  IntraFetch f = intra_fetch(a, kd, min(t + lane, last));
+  IntraOut o;
+  if (!BLK_PERSIST) {
+#if defined(P64_TIMING)
+    __builtin_amdgcn_s_waitcnt(0);
+#endif
+    CLOCK_MARK(rtl);
+    intra_block<false>(a, f, lds, lane, o);
+    CLOCK_MARK(rtc);
+    intra_store(a, o, lds, lane);
+    CLOCK_END();
+    return;
   }
+  // drain the first fetch here: entering the loop with nothing pending keeps
+  // hipcc's wait counts inside it exact (otherwise it merges the pending
+  // first fetch into the loop header and waits for every store each block)
+  __builtin_amdgcn_s_waitcnt(0);
+#if defined(BLK_STAGGER)
+  if (blockIdx.x & 1)  // development probe: odd workgroups start later
+    for (int i = 0; i < BLK_STAGGER; i++) __builtin_amdgcn_s_sleep(127);
+#endif
+  // the next block's fetch is always in flight; two fetch slots alternate
+  // (unrolled by two) so no loop-carried copy waits for a fetch
+  IntraFetch g = intra_fetch(a, kd, min(t + stride + lane, last));
+  intra_block<false>(a, f, lds, lane, o);
+  for (t += stride; t < total; t += stride) {
+    f = intra_fetch(a, kd, min(t + stride + lane, last));
+    intra_block<true>(a, g, lds, lane, o);
+    t += stride;
+    if (t >= total) break;
+    g = intra_fetch(a, kd, min(t + stride + lane, last));
+    intra_block<true>(a, f, lds, lane, o);
+  }
+  intra_store(a, o, lds, lane);
+  CLOCK_END();
 }
 
 // The source of an 8x8 prediction at (x, y) of a plane (any byte alignment):
-// three aligned dwords per row; the third is read only when the row is
-// misaligned, so no byte past the row's end is touched
+// three aligned dwords per row (the third only matters when the row is
+// misaligned)
 struct PredSrc {
   uint32_t d[8][3];
   int sh;
 };
-__device__ __forceinline__ PredSrc load_pred(const uint8_t *plane, int pw, int x, int y) {
-  const uint8_t *row0 = plane + (uint32_t)(mul24(y, pw) + (x & ~3));
-  PredSrc p;
-  p.sh = x & 3;
-#pragma unroll
-  for (int k = 0; k < 8; k++) {
-    const uint32_t *s = reinterpret_cast<const uint32_t *>(row0 + (uint32_t)mul24(k, pw));
-    p.d[k][0] = s[0];
-    p.d[k][1] = s[1];
-    p.d[k][2] = p.sh ? s[2] : 0u;
-  }
-  return p;
-}
 __device__ __forceinline__ void pred_row(const PredSrc &p, int r, int s[8]) {
   unpack8(align4(p.d[r][1], p.d[r][0], p.sh), align4(p.d[r][2], p.d[r][1], p.sh), s);
 }
@@ -1723,55 +1874,103 @@ __device__ __forceinline__ void add_pred(const PredSrc &p, bool filter, int v[64
 }
 
 // decoder reconstruction (DecompressMDU p64.c:1179-1237 + DecodeSaveMDU
-// p64.c:971-1013), block layout.  MBs whose coded_mask is 0 are left alone.
-// Motion vectors are clamped so that a block's source stays inside its plane:
-// a conforming stream never needs it (H.261 vectors point inside the
-// picture) and a corrupt one cannot make the kernel read outside the buffer.
-__global__ __launch_bounds__(256) BLK_OCC void k_recon_blk(int w, int h, int64_t stride, const uint8_t *refp,
-                                                   uint8_t *recp, const int16_t *coef,
-                                                   const p64_mb_rec *mbr, const uint8_t *quant_mb,
-                                                   const uint8_t *coded_mask, BlkDiv kd, unsigned total) {
-  const unsigned t = blockIdx.x * 256u + threadIdx.x;
-  if (t >= total) return;
+// p64.c:971-1013), block layout, persistent, as a two-stage load pipeline:
+// while block i is transformed, the levels and prediction source of block
+// i+1 (whose record arrived during block i-1) and the record of block i+2 are
+// in flight.  Every load is a buffer load: where a block needs no levels
+// (uncoded) or no prediction (intra MB) its offset is out of range, which
+// reads zeros without touching memory -- no branch around any load, so the
+// wait counts stay exact and only the algorithmic bytes move.
+// MBs whose coded_mask is 0 are left alone.  Motion vectors are clamped so a
+// block's source stays inside its plane: a conforming stream never needs it
+// (H.261 vectors point inside the picture; the reader rejects others) and a
+// corrupt one cannot make the kernel read outside the picture.
+// One launch covers at most 2 GiB of levels and of pictures (the host splits
+// larger batches), so every offset fits the 32-bit buffer range.
+constexpr uint32_t BUF_OOB = 0x80000000u;  // >= every buffer's num_records
+
+struct RecBufs {
+  __amdgpu_buffer_rsrc_t ref, coef, mb, q, mask;
+};
+struct RecStageA {  // the block and its MB's record
+  BlkPos p;
+  uint32_t m;  // p64_mb_rec as one dword
+  int q, coded;
+};
+struct RecStageB {  // what the block's reconstruction reads
+  uint32_t lq[8][4];  // zigzag levels, 8 x 16 bytes (zeros if not coded)
+  PredSrc pred;       // prediction source (zeros if intra)
+  bool ck, inter, filter;
+};
+__device__ __forceinline__ RecStageA rec_stage_a(const RecBufs &B, int w, int h, const BlkDiv &kd,
+                                                 unsigned t) {
   const int nmb = (w >> 4) * (h >> 4);
-  const BlkPos p = blk_pos(t, w, h, kd);
-  const size_t gmb = (size_t)p.fi * nmb + p.mb;
-  if (!coded_mask[gmb]) return;
-  const uint32_t m = *reinterpret_cast<const uint32_t *>(mbr + gmb);
-  const int mt = (int)(int8_t)(m & 0xff);
-  const int cbp = mt_cbp(mt) ? (int)((m >> 8) & 0x3f) : 0x3f;  // p64.c:1200
-  const bool ck = mt_tcoeff(mt) && ((cbp >> (5 - p.b)) & 1);
-  const int pw = p.plane ? w >> 1 : w, ph = p.plane ? h >> 1 : h;
-  const uint32_t poff = (uint32_t)plane_offset(p.plane, w, h);
-  const bool inter = !mt_intra(mt);
-  PredSrc ps;
-  if (inter) {  // prediction source loads first: in flight during the IDCT
-    int dx = 0, dy = 0;
-    if (mt_mf(mt)) {  // chroma MV/2 with C truncation (io.c:268-270)
-      const int mvx = (int)(int8_t)((m >> 16) & 0xff), mvy = (int)(int8_t)(m >> 24);
-      dx = p.plane ? mvx / 2 : mvx;
-      dy = p.plane ? mvy / 2 : mvy;
-    }
-    const int sx = clampi(p.x + dx, 0, pw - 8), sy = clampi(p.y + dy, 0, ph - 8);
-    ps = load_pred(refp + (size_t)p.fi * stride + poff, pw, sx, sy);
-  }
-  int v[64];
-  if (ck) {  // IZigzagMatrix + ICCITT(Flat)Quantize straight from the packed levels
-    const int q = quant_mb[gmb];
-    const int q2 = 2 * q, qq = q - (int)!(q & 1);
-    const uint4 *src = reinterpret_cast<const uint4 *>(coef + gmb * 384 + p.b * 64);
-    uint4 lq[8];
+  RecStageA A;
+  A.p = blk_pos(t, w, h, kd);
+  const int gmb = A.p.fi * nmb + A.p.mb;
+  A.m = __builtin_amdgcn_raw_buffer_load_b32(B.mb, 4 * gmb, 0, 0);
+  A.q = __builtin_amdgcn_raw_buffer_load_b8(B.q, gmb, 0, 0);
+  A.coded = __builtin_amdgcn_raw_buffer_load_b8(B.mask, gmb, 0, 0);
+  return A;
+}
+__device__ __forceinline__ RecStageB rec_stage_b(const RecBufs &B, int w, int h, int64_t stride,
+                                                 const RecStageA &A) {
+  const int nmb = (w >> 4) * (h >> 4);
+  const BlkPos &p = A.p;
+  const int mt = (int)(int8_t)(A.m & 0xff);
+  const int cbp = mt_cbp(mt) ? (int)((A.m >> 8) & 0x3f) : 0x3f;  // p64.c:1200
+  RecStageB S;
+  S.ck = A.coded && mt_tcoeff(mt) && ((cbp >> (5 - p.b)) & 1);
+  S.inter = A.coded && !mt_intra(mt);
+  S.filter = mt_filter(mt);
+  const uint32_t co = S.ck ? (uint32_t)(((p.fi * nmb + p.mb) * 6 + p.b) * 128) : BUF_OOB;
 #pragma unroll
-    for (int k = 0; k < 8; k++) lq[k] = src[k];
-    const bool intra = !inter;
+  for (int k = 0; k < 8; k++) {
+    const auto v = __builtin_amdgcn_raw_buffer_load_b128(B.coef, co + 16 * k, 0, 0);
+    S.lq[k][0] = v[0];
+    S.lq[k][1] = v[1];
+    S.lq[k][2] = v[2];
+    S.lq[k][3] = v[3];
+  }
+  const int pw = p.plane ? w >> 1 : w, ph = p.plane ? h >> 1 : h;
+  int dx = 0, dy = 0;
+  if (mt_mf(mt)) {  // chroma MV/2 with C truncation (io.c:268-270)
+    const int mvx = (int)(int8_t)((A.m >> 16) & 0xff), mvy = (int)(int8_t)(A.m >> 24);
+    dx = p.plane ? mvx / 2 : mvx;
+    dy = p.plane ? mvy / 2 : mvy;
+  }
+  const int sx = clampi(p.x + dx, 0, pw - 8), sy = clampi(p.y + dy, 0, ph - 8);
+  S.pred.sh = sx & 3;
+  const uint32_t po = S.inter ? (uint32_t)((int64_t)p.fi * stride) + (uint32_t)plane_offset(p.plane, w, h) +
+                                    (uint32_t)(mul24(sy, pw) + (sx & ~3))
+                              : BUF_OOB;
+  // the third dword only when the row is misaligned (then it lies inside the
+  // row: sx <= pw - 9); an aligned row at the plane's end would reach past it
+  const uint32_t po3 = S.pred.sh ? po + 8 : BUF_OOB;
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    const auto v = __builtin_amdgcn_raw_buffer_load_b64(B.ref, po + (uint32_t)mul24(k, pw), 0, 0);
+    S.pred.d[k][0] = v[0];
+    S.pred.d[k][1] = v[1];
+    S.pred.d[k][2] = __builtin_amdgcn_raw_buffer_load_b32(B.ref, po3 + (uint32_t)mul24(k, pw), 0, 0);
+  }
+  return S;
+}
+__device__ __forceinline__ void rec_block(int w, int h, int64_t stride, __amdgpu_buffer_rsrc_t rec,
+                                          const RecStageA &A, const RecStageB &S) {
+  const BlkPos &p = A.p;
+  int v[64];
+  if (S.ck) {  // IZigzagMatrix + ICCITT(Flat)Quantize straight from the packed levels
+    const int q = A.q;
+    const int q2 = 2 * q, qq = q - (int)!(q & 1);
 #pragma unroll
     for (int k = 0; k < 8; k++) {
-      const uint32_t w4[4] = {lq[k].x, lq[k].y, lq[k].z, lq[k].w};
 #pragma unroll
       for (int i = 0; i < 8; i++) {
-        const int l = (i & 1) ? (int)w4[i >> 1] >> 16 : (int)(int16_t)(w4[i >> 1] & 0xffff);
+        const uint32_t wd = S.lq[k][i >> 1];
+        const int l = (i & 1) ? (int)wd >> 16 : (int)(int16_t)(wd & 0xffff);
         const int e = k_zz.inv[8 * k + i];
-        v[e] = intra ? dequantise<true>(l, e == 0, q2, qq) : dequantise<false>(l, false, q2, qq);
+        v[e] = S.inter ? dequantise<false>(l, false, q2, qq) : dequantise<true>(l, e == 0, q2, qq);
       }
     }
     idct_block(v);
@@ -1779,10 +1978,59 @@ __global__ __launch_bounds__(256) BLK_OCC void k_recon_blk(int w, int h, int64_t
 #pragma unroll
     for (int e = 0; e < 64; e++) v[e] = 0;
   }
-  if (inter) add_pred(ps, mt_filter(mt), v);
+  if (S.inter) add_pred(S.pred, S.filter, v);
 #pragma unroll
   for (int e = 0; e < 64; e++) v[e] = clampi(v[e], 0, 255);  // BoundIDctMatrix
-  store_block(recp + (size_t)p.fi * stride + poff + (uint32_t)(mul24(p.y, pw) + p.x), pw, v);
+  // buffer stores, out of range (dropped) for MBs that are not coded: no
+  // branch around the stores either
+  const int pw = p.plane ? w >> 1 : w;
+  const uint32_t ro = A.coded ? (uint32_t)((int64_t)p.fi * stride) + (uint32_t)plane_offset(p.plane, w, h) +
+                                    (uint32_t)(mul24(p.y, pw) + p.x)
+                              : BUF_OOB;
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    const uint2 r = pack8(v + 8 * k);
+    typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+    u32x2 d;
+    d[0] = r.x;
+    d[1] = r.y;
+    __builtin_amdgcn_raw_buffer_store_b64(d, rec, ro + (uint32_t)mul24(k, pw), 0, 0);
+  }
+}
+__global__ __launch_bounds__(256) BLK_OCC void k_recon_blk(int w, int h, int64_t stride, const uint8_t *refp,
+                                                           uint8_t *recp, const int16_t *coef,
+                                                           const p64_mb_rec *mbr, const uint8_t *quant_mb,
+                                                           const uint8_t *coded_mask, BlkDiv kd,
+                                                           unsigned total, unsigned gstride) {
+  unsigned t = blockIdx.x * 256u + threadIdx.x;
+  if (t >= total) return;
+  const int nmb = (w >> 4) * (h >> 4), nfr = (int)(total / (unsigned)(6 * nmb));
+  RecBufs B;
+  B.ref = __builtin_amdgcn_make_buffer_rsrc((void *)refp, (short)0, (int)(nfr * stride), BUF_RSRC_W3);
+  B.coef = __builtin_amdgcn_make_buffer_rsrc((void *)coef, (short)0, nfr * nmb * 768, BUF_RSRC_W3);
+  B.mb = __builtin_amdgcn_make_buffer_rsrc((void *)mbr, (short)0, nfr * nmb * 4, BUF_RSRC_W3);
+  B.q = __builtin_amdgcn_make_buffer_rsrc((void *)quant_mb, (short)0, nfr * nmb, BUF_RSRC_W3);
+  B.mask = __builtin_amdgcn_make_buffer_rsrc((void *)coded_mask, (short)0, nfr * nmb, BUF_RSRC_W3);
+  const __amdgpu_buffer_rsrc_t rec =
+      __builtin_amdgcn_make_buffer_rsrc((void *)recp, (short)0, (int)(nfr * stride), BUF_RSRC_W3);
+  const unsigned last = total - 1;
+  RecStageA A = rec_stage_a(B, w, h, kd, t);
+  RecStageA An = rec_stage_a(B, w, h, kd, min(t + gstride, last));
+  RecStageB S = rec_stage_b(B, w, h, stride, A);
+  // drain the pipeline fill: entering the loop with nothing pending keeps
+  // hipcc's wait counts inside it exact (see k_intra_blk)
+  __builtin_amdgcn_s_waitcnt(0);
+  for (;;) {  // every lane reaches t >= total: no lane is left behind
+    const unsigned tn = t + gstride;
+    const RecStageA Ann = rec_stage_a(B, w, h, kd, min(tn + gstride, last));  // block i+2
+    const RecStageB Sn = rec_stage_b(B, w, h, stride, An);                     // block i+1
+    rec_block(w, h, stride, rec, A, S);
+    if (tn >= total) break;
+    A = An;
+    An = Ann;
+    S = Sn;
+    t = tn;
+  }
 }
 
 // batched 8x8 block operations (one thread per block; shares the device
@@ -1906,6 +2154,34 @@ int check_geometry(int w, int h, int nframes, int64_t stride, bool luma_only = f
 }
 
 bool aligned16(const void *p) { return ((uintptr_t)p & 15) == 0; }
+
+// Workgroups of 256 for a persistent block-layout kernel: as many as are
+// resident at once (occupancy x CUs of the current device), at most one per
+// 256 blocks.
+int persistent_grid(const void *kernel, int64_t blocks, unsigned *wg) {
+  static int cus[64], nb_cache[64][4];
+  static const void *kern_cache[64][4];
+  int dev = 0;
+  HIP_TRY(hipGetDevice(&dev));
+  if (dev < 0 || dev >= 64) return fail(P64GPU_E_INVALID, "device %d", dev);
+  if (!cus[dev]) HIP_TRY(hipDeviceGetAttribute(&cus[dev], hipDeviceAttributeMultiprocessorCount, dev));
+  int nb = 0;
+  for (int i = 0; i < 4; i++)
+    if (kern_cache[dev][i] == kernel) nb = nb_cache[dev][i];
+  if (!nb) {
+    HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kernel, 256, 0));
+    if (nb < 1) nb = 1;
+    for (int i = 0; i < 4; i++)
+      if (!kern_cache[dev][i]) {
+        kern_cache[dev][i] = kernel;
+        nb_cache[dev][i] = nb;
+        break;
+      }
+  }
+  const int64_t need = (blocks + 255) / 256, have = (int64_t)nb * cus[dev];
+  *wg = (unsigned)(need < have ? need : have);
+  return P64GPU_OK;
+}
 
 // P64GPU_MB_LAYOUT=1 (read once): intra pictures and decoder reconstruction
 // take the one-wave-per-MB kernels (k_encode<0>, k_decode_recon) instead of
@@ -2076,8 +2352,30 @@ static int encode_launch(const p64gpu_encode_args *a, const int32_t *mb_list, in
   const MbDiv kd = mb_div(a->width, a->height);
   const int64_t blocks = 6 * (int64_t)grid;
   if (a->intra && !mb_list && blocks < (1LL << 30) && !mb_layout_forced()) {
-    hipLaunchKernelGGL(k_intra_blk, dim3((unsigned)((blocks + 255) / 256)), dim3(256), 0, st, *a,
-                       blk_div(a->width, a->height), (unsigned)blocks);
+    // pictures per launch: pictures and levels of a launch within 2 GiB
+    const int nmb = (a->width / 16) * (a->height / 16);
+    const int64_t per = (int64_t)nmb * 768 > a->frame_stride ? (int64_t)nmb * 768 : a->frame_stride;
+    const int chunk = (int)((((int64_t)1 << 31) - 1) / per);
+    for (int f0 = 0; f0 < a->nframes; f0 += chunk) {
+      p64gpu_encode_args c = *a;
+      c.nframes = a->nframes - f0 < chunk ? a->nframes - f0 : chunk;
+      const size_t m0 = (size_t)f0 * nmb;
+      c.cur = a->cur + (size_t)f0 * a->frame_stride;
+      c.recon = a->recon + (size_t)f0 * a->frame_stride;
+      c.last_intra = a->last_intra + m0;
+      c.quant_mb = a->quant_mb ? a->quant_mb + m0 : nullptr;
+      c.coef = a->coef + m0 * 384;
+      c.mb = a->mb + m0;
+      const int64_t nblk = (int64_t)c.nframes * nmb * 6;
+      unsigned wg;
+      int s2 = persistent_grid((const void *)k_intra_blk, nblk, &wg);
+      if (s2) return s2;
+      if (!BLK_PERSIST) wg = (unsigned)((nblk + 255) / 256);
+      hipLaunchKernelGGL(k_intra_blk, dim3(wg), dim3(256), 0, st, c, blk_div(a->width, a->height),
+                         (unsigned)nblk, wg * 256u);
+      HIP_TRY(hipGetLastError());
+    }
+    return P64GPU_OK;
   } else if (a->intra)
     hipLaunchKernelGGL(k_encode<0>, dim3(grid), dim3(64), 0, st, *a, mb_list, kd);
   else if (a->me_mode == P64GPU_ME_FULL)
@@ -2097,14 +2395,29 @@ int p64gpu_decode_recon(int w, int h, int nframes, int64_t stride, const uint8_t
     return fail(P64GPU_E_INVALID, "NULL buffer");
   if (!aligned16(ref) || !aligned16(recon) || !aligned16(coef) || ((uintptr_t)mb & 3))
     return fail(P64GPU_E_INVALID, "ref/recon/coef must be 16-byte aligned, mb 4-byte aligned");
-  const unsigned grid = (unsigned)((int64_t)nframes * (w / 16) * (h / 16));
-  const int64_t blocks = 6 * (int64_t)grid;
-  if (blocks < (1LL << 30) && !mb_layout_forced())
-    hipLaunchKernelGGL(k_recon_blk, dim3((unsigned)((blocks + 255) / 256)), dim3(256), 0,
-                       (hipStream_t)stream, w, h, stride, ref, recon, coef, mb, quant_mb, coded_mask,
-                       blk_div(w, h), (unsigned)blocks);
-  else
-    hipLaunchKernelGGL(k_decode_recon, dim3(grid), dim3(64), 0, (hipStream_t)stream, w, h, stride,
+  const int nmb = (w / 16) * (h / 16);
+  const unsigned grid = (unsigned)((int64_t)nframes * nmb);
+  if (!mb_layout_forced()) {
+    // pictures per launch: every buffer of a launch within the 2 GiB range
+    // of k_recon_blk's 32-bit buffer offsets
+    const int64_t per = (int64_t)nmb * 768 > stride ? (int64_t)nmb * 768 : stride;
+    const int chunk = (int)((((int64_t)1 << 31) - 1) / per);
+    for (int f0 = 0; f0 < nframes; f0 += chunk) {
+      const int nf = nframes - f0 < chunk ? nframes - f0 : chunk;
+      const int64_t blocks = (int64_t)nf * nmb * 6;
+      unsigned wg;
+      int s2 = persistent_grid((const void *)k_recon_blk, blocks, &wg);
+      if (s2) return s2;
+      const size_t m0 = (size_t)f0 * nmb;
+      hipLaunchKernelGGL(k_recon_blk, dim3(wg), dim3(256), 0, (hipStream_t)stream, w, h, stride,
+                         ref + (size_t)f0 * stride, recon + (size_t)f0 * stride, coef + m0 * 384,
+                         mb + m0, quant_mb + m0, coded_mask + m0, blk_div(w, h), (unsigned)blocks,
+                         wg * 256u);
+      HIP_TRY(hipGetLastError());
+    }
+    return P64GPU_OK;
+  }
+  hipLaunchKernelGGL(k_decode_recon, dim3(grid), dim3(64), 0, (hipStream_t)stream, w, h, stride,
                        ref, recon, coef, mb, quant_mb, coded_mask, mb_div(w, h));
   HIP_TRY(hipGetLastError());
   return P64GPU_OK;

@@ -71,6 +71,18 @@ __global__ __launch_bounds__(256) void k(uint32_t seed, int iters, uint32_t* out
         if (OP == 49) asm("v_and_b32_e32 %0, %1, %2" : "=v"(a[j]) : "v"(x), "v"(a[j]));
         if (OP == 50) asm("v_or_b32_e32 %0, %1, %2" : "=v"(a[j]) : "v"(x), "v"(a[j]));
         if (OP == 51) asm("v_max_i32_e32 %0, %1, %2" : "=v"(a[j]) : "v"(x), "v"(a[j]));
+        if (OP == 52) asm("v_dot2c_i32_i16_e32 %0, %1, %2" : "+v"(a[j]) : "v"(x), "v"(y));
+        if (OP == 53) asm("v_dot2c_i32_i16_e32 %0, 0xfe27016a, %1" : "+v"(a[j]) : "v"(x));
+        if (OP == 54) asm("v_dot2_i32_i16 %0, %1, %2, %3" : "=v"(a[j]) : "v"(x), "v"(y), "v"(a[j]));
+        if (OP == 55) asm("v_pk_sub_i16 %0, %1, %2" : "=v"(a[j]) : "v"(x), "v"(a[j]));
+        if (OP == 56) asm("v_pk_ashrrev_i16 %0, 1, %1" : "=v"(a[j]) : "v"(a[j]));
+        if (OP == 57) asm("v_sat_pk_u8_i16_e32 %0, %1" : "=v"(a[j]) : "v"(a[j] ^ x));
+        if (OP == 58) asm("v_mul_lo_u32 %0, %1, %2" : "=v"(a[j]) : "v"(x), "v"(a[j]));
+        if (OP == 59) asm("v_cvt_pk_i16_i32 %0, %1, %2" : "=v"(a[j]) : "v"(x), "v"(a[j]));
+        if (OP == 60) asm("v_lshl_or_b32 %0, %1, 16, %2" : "=v"(a[j]) : "v"(x), "v"(a[j]));
+        if (OP == 61) asm("v_mul_i32_i24_e32 %0, 0x16a, %1" : "=v"(a[j]) : "v"(a[j]));
+        if (OP == 62) asm("v_pk_add_u16 %0, %1, %2 op_sel:[1,0] op_sel_hi:[0,1]" : "=v"(a[j]) : "v"(x), "v"(a[j]));
+        if (OP == 63) asm("v_sub_u32_e32 %0, %1, %2" : "=v"(a[j]) : "v"(x), "v"(a[j]));
       }
     asm volatile("" : "+v"(r[0]), "+v"(r[3]));
   }
@@ -160,5 +172,17 @@ int main() {
   run<49, false>("v_and_b32", d);
   run<50, false>("v_or_b32", d);
   run<51, false>("v_max_i32", d);
+  run<52, false>("v_dot2c_i32_i16_e32", d);
+  run<53, false>("v_dot2c_i32_i16 lit", d);
+  run<54, false>("v_dot2_i32_i16 (vop3p)", d);
+  run<55, false>("v_pk_sub_i16", d);
+  run<56, false>("v_pk_ashrrev_i16", d);
+  run<57, false>("v_sat_pk_u8_i16+xor", d);
+  run<58, false>("v_mul_lo_u32", d);
+  run<59, false>("v_cvt_pk_i16_i32", d);
+  run<60, false>("v_lshl_or_b32", d);
+  run<61, false>("v_mul_i32_i24 lit", d);
+  run<62, false>("v_pk_add_u16 op_sel", d);
+  run<63, false>("v_sub_u32_e32", d);
   return 0;
 }
