@@ -56,6 +56,9 @@ typedef struct {
   int host_vlc;          /* 1: entropy-code on the host (p64stream.h) always;
                             0 (default): pictures coded in one launch are
                             entropy-coded on the GPU (p64gpu_vlc_pictures)     */
+  int verbose;           /* -v: print "BufferContents: %d  New Q1: %d" to
+                            stdout at every rate-control update, as
+                            ExecuteQuantization does (p64.c:466-470)           */
 } p64seq_config;
 
 typedef struct {

@@ -100,7 +100,12 @@ typedef struct p64s_reader p64s_reader;
  * P64GPU_E_STREAM when the stream does not start with a picture start code. */
 int p64s_reader_open(const uint8_t *data, size_t len, p64s_reader **out);
 void p64s_reader_close(p64s_reader *r);
-/* Geometry of the stream (from its first picture header). */
+/* -c ForceCIF (p64.c:308-310, 1071-1072): decode every picture with CIF
+ * geometry and GOB numbering whatever its PTYPE says (a QCIF or NTSC stream
+ * lands in the CIF frame; GOBs it does not send stay as they were).  Call
+ * right after p64s_reader_open. */
+int p64s_reader_force_cif(p64s_reader *r);
+/* Geometry of the stream (from its first picture header, or CIF when forced). */
 int p64s_reader_info(const p64s_reader *r, p64s_picture_info *info);
 /* Decodes the next picture's headers and levels.  Returns 1 with a picture,
  * 0 at the end of the stream (info->tr then holds the temporal reference of

@@ -136,6 +136,7 @@ def lib() -> ctypes.CDLL:
     L.p64s_reader_close.argtypes = [vp]
     L.p64s_reader_close.restype = None
     L.p64s_reader_info.argtypes = [vp, vp]
+    L.p64s_reader_force_cif.argtypes = [vp]
     L.p64s_read_picture.argtypes = [vp, vp, vp, vp, vp, vp]
     # sequence encoder (include/p64seq.h), host C over the GPU path
     L.p64seq_default_config.argtypes = [vp]

@@ -255,6 +255,7 @@ static int call_program(p64seq *s, int v, int mtype, int k, int64_t bc) {
  * MQUANT half has no effect: OracleMQuantEnable is never set) */
 static int execute_quantization(p64seq *s, int g, int m, int *gq) {
   const int64_t bc = buffer_contents(s, g, m);
+  if (s->c.verbose) printf("BufferContents: %d  New Q1: %d\n", (int)bc, s->gquant);
   int q = (int)bc / s->qdfact + s->qoffs;
   if (s->prog) {
     const int st = call_program(s, 1, s->mtype, s->h_lists[g * 33 + m], bc);
@@ -429,6 +430,11 @@ static int encode_per_gob(p64seq *s, p64gpu_encode_args *a, int first) {
       return st;
     for (int m = 0; m < 33; m++) {
       const int k = s->h_lists[g * 33 + m];
+      /* the MDU-level ExecuteQuantization (p64.c:718-728) changes nothing
+       * here (it could only enable MQUANT, which the reference never does);
+       * only its -v line is reproduced */
+      if (s->c.verbose && m && !(m % 11) && !first)
+        printf("BufferContents: %d  New Q1: %d\n", (int)buffer_contents(s, g, m), s->gquant);
       s->h_q[k] = (uint8_t)s->gquant;
       if (buffer_contents(s, g, m) > s->rate / 4) overflow_mb(s, k);
       if ((st = write_mb(s, m, k))) return st;

@@ -528,6 +528,7 @@ struct p64s_reader {
   int have_psc;  /* a start code + GN 0 (picture header) has been consumed */
   int ended, end_tr, last_tr;
   int mt, mvx, mvy; /* ReadMBHeader's persistent MType / MVDH / MVDV */
+  int force_cif;    /* -c: CIF geometry whatever PTYPE says (p64.c:1071-1072) */
 };
 
 /* n <= 25 bits at the current position without consuming them; bytes past
@@ -596,6 +597,14 @@ int p64s_reader_open(const uint8_t *data, size_t len, p64s_reader **out) {
 
 void p64s_reader_close(p64s_reader *r) { free(r); }
 
+int p64s_reader_force_cif(p64s_reader *r) {
+  if (!r) return fail(P64GPU_E_INVALID, "reader_force_cif: NULL reader");
+  r->force_cif = 1;
+  r->first.format = P64S_CIF;
+  p64s_geometry(P64S_CIF, &r->first.width, &r->first.height, &r->first.ngob);
+  return 0;
+}
+
 int p64s_reader_info(const p64s_reader *r, p64s_picture_info *info) {
   if (!r || !info) return fail(P64GPU_E_INVALID, "reader_info: NULL argument");
   *info = r->first;
@@ -663,7 +672,8 @@ int p64s_read_picture(p64s_reader *r, p64s_picture_info *info, p64_mb_rec *mb, u
     return 0;
   }
   read_picture_header(r, &pi);
-  if (((pi.ptype & 0x04) ? (pi.pspare == 0x8c ? P64S_NTSC : P64S_CIF) : P64S_QCIF) != r->first.format)
+  if (!r->force_cif &&
+      ((pi.ptype & 0x04) ? (pi.pspare == 0x8c ? P64S_NTSC : P64S_CIF) : P64S_QCIF) != r->first.format)
     BAD("picture format changes mid-stream");
   r->have_psc = 0;
   /* no start code after the header: it was the trailing picture header

@@ -21,13 +21,21 @@
  *   -s file                 stream file (default <prefix>.p64)
  *   -z suffix               component file suffix (default .y4m with -y4m)
  *   -d                      decode
+ *   -c                      decode: ForceCIF, CIF geometry whatever PTYPE says
+ *                           (p64.c:308-310, 1071-1072)
+ *   -v                      print BufferContents / GQUANT at every rate-control
+ *                           update (ExecuteQuantization p64.c:466-470)
+ *   -l n                    Loud level: accepted; the statistics it prints
+ *                           (stat.c) are not reproduced
+ *   -p                      ParityEnable: accepted; it changes the stream only in
+ *                           the VERSION_1_0 syntax the reference does not build
  *   -                       y4m from stdin
  * Additions: -full / -tss (FastBME vs the shipped StepBME), -D device,
  * -hostvlc (entropy-code on the host instead of the GPU).
  *   -o                      program interpreter: program text on stdin (p64prog.h)
  *   (no -y4m)               raw component files <prefix><n>.Y/.U/.V per picture
- * Not supported here: -p parity (VERSION_1_0 only), -y floating-point reference
- * DCT (a test option).
+ * Not supported here: -y floating-point reference DCT (a test option; see
+ * DESIGN.md).
  *
  * Differences from the reference: a y4m that ends before -b finishes the
  * stream (trailer written) instead of exit(ERROR_BOUNDS) with an unterminated
@@ -81,6 +89,7 @@ static int drain(p64s_writer *wr, FILE *o) {
 typedef struct {
   int format, y4m, first, last, skip, quant, sl, mode, device, decode, from_stdin;
   int rate, file_size_bits, frame_rate, frame_rate_div, oracle, host_vlc;
+  int force_cif, loud, verbose;
   const char *prefix, *suffix, *stream;
 } opts;
 
@@ -158,6 +167,7 @@ static int encode(const opts *o) {
   cfg.device = o->device;
   cfg.program = g_prog;
   cfg.host_vlc = o->host_vlc;
+  cfg.verbose = o->verbose;
   p64seq *sq = NULL;
   if ((s = p64seq_open(&cfg, &sq))) return die("p64seq_open", s);
   p64seq_stats st;
@@ -231,6 +241,7 @@ static int decode(const opts *o) {
   p64s_picture_info info;
   int s;
   if ((s = p64s_reader_open(data, (size_t)len, &rd))) return die("reader_open", s);
+  if (o->force_cif && (s = p64s_reader_force_cif(rd))) return die("reader_force_cif", s);
   p64s_reader_info(rd, &info);
   const int w = info.width, h = info.height, nmb = info.ngob * 33;
   const size_t pic = (size_t)w * h * 3 / 2;
@@ -331,6 +342,10 @@ int main(int argc, char **argv) {
     else if (!strcmp(a, "-d")) o.decode = 1;
     else if (!strcmp(a, "-o")) o.oracle = 1;
     else if (!strcmp(a, "-hostvlc")) o.host_vlc = 1;
+    else if (!strcmp(a, "-c")) o.force_cif = 1;
+    else if (!strcmp(a, "-l") && more) o.loud = atoi(argv[++i]);
+    else if (!strcmp(a, "-p")) (void)0; /* ParityEnable: no stream effect outside VERSION_1_0 */
+    else if (!strcmp(a, "-v")) o.verbose = 1;
     else if (!strcmp(a, "-r") && more) o.rate = atoi(argv[++i]);
     else if (!strcmp(a, "-x") && more) o.file_size_bits = atoi(argv[++i]);
     else if (!strcmp(a, "-f") && more) {
@@ -360,8 +375,9 @@ int main(int argc, char **argv) {
   if (!o.prefix) {
     fprintf(stderr,
             "usage: p64gpu [-NTSC|-CIF|-QCIF] -y4m [-a n] [-b n] [-k n] [-q q] [-i sl] [-full|-tss]\n"
-            "              [-D dev] [-s out.p64] [-z suffix] prefix|-\n"
-            "       p64gpu -d [-y4m] -s in.p64 [-z suffix] prefix\n");
+            "              [-r bits/s | -x bits] [-f rate] [-o] [-v] [-l n] [-p] [-D dev]\n"
+            "              [-s out.p64] [-z suffix] prefix|-\n"
+            "       p64gpu -d [-c] [-y4m] -s in.p64 [-z suffix] prefix\n");
     return 1;
   }
   /* BoundValue (p64.c:341-352); -q absent leaves 0 (default / rate-derived) */

@@ -103,10 +103,12 @@ class Reader:
     """Iterates the pictures of a .p64 byte string; `end_tr` is set once the
     stream is exhausted (temporal reference of the trailing picture header)."""
 
-    def __init__(self, data: bytes):
+    def __init__(self, data: bytes, force_cif: bool = False):
         self._buf = ctypes.create_string_buffer(bytes(data), len(data))
         self._h = ctypes.c_void_p()
         _check(lib().p64s_reader_open(self._buf, len(data), ctypes.byref(self._h)))
+        if force_cif:  # -c ForceCIF (p64.c:308-310, 1071-1072)
+            _check(lib().p64s_reader_force_cif(self._h))
         info = _Info()
         _check(lib().p64s_reader_info(self._h, ctypes.byref(info)))
         self.fmt, self.width, self.height, self.ngob = info.format, info.width, info.height, info.ngob
@@ -182,7 +184,8 @@ class SeqConfig(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int) for n in
                 ("format", "me_mode", "search_limit", "quant", "rate", "file_size_bits",
                  "start_frame", "last_frame", "frame_skip", "frame_rate", "frame_rate_div",
-                 "device")] + [("program", ctypes.c_void_p), ("host_vlc", ctypes.c_int)]
+                 "device")] + [("program", ctypes.c_void_p), ("host_vlc", ctypes.c_int),
+                               ("verbose", ctypes.c_int)]
 
 
 class ProgSettings(ctypes.Structure):
@@ -243,7 +246,8 @@ class SequenceEncoder:
                  search_limit: int = 15, first: int = 0, last: int | None = None, skip: int = 1,
                  rate: int = 0, file_size_bits: int = 0, frame_rate: int = 30000,
                  frame_rate_div: int = 1001, device: int = 0, nframes: int | None = None,
-                 program: "Program | str | bytes | None" = None, host_vlc: bool = False):
+                 program: "Program | str | bytes | None" = None, host_vlc: bool = False,
+                 verbose: bool = False):
         L = lib()
         if program is not None and not isinstance(program, Program):
             program = Program(program)
@@ -268,6 +272,7 @@ class SequenceEncoder:
         c.frame_skip, c.frame_rate, c.frame_rate_div, c.device = skip, frame_rate, frame_rate_div, device
         c.program = program._h if program is not None else None
         c.host_vlc = int(bool(host_vlc))
+        c.verbose = int(bool(verbose))
         self.width, self.height = width, height
         self._h = ctypes.c_void_p()
         _check(L.p64seq_open(ctypes.byref(c), ctypes.byref(self._h)))
@@ -335,13 +340,14 @@ def encode_sequence(frames, width: int, height: int, *, quant: int = 0, me_mode:
         enc.close()
 
 
-def decode_sequence(data: bytes, start_frame: int = 0) -> list[np.ndarray]:
+def decode_sequence(data: bytes, start_frame: int = 0, force_cif: bool = False) -> list[np.ndarray]:
     """p64DecodeSequence (p64.c:1022): host parse + GPU reconstruction; returns
-    the output frames (Y|U|V bytes) in the order the reference writes them."""
+    the output frames (Y|U|V bytes) in the order the reference writes them.
+    force_cif: the -c flag (CIF geometry whatever the stream's PTYPE says)."""
     import torch
 
     from . import decode_recon
-    r = Reader(data)
+    r = Reader(data, force_cif=force_cif)
     w, h, nmb = r.width, r.height, r.nmb
     pic = w * h * 3 // 2
     bufs = [torch.zeros(pic, dtype=torch.uint8, device="cuda") for _ in range(2)]

@@ -243,18 +243,20 @@ def raster_index(fmt, g, m):
 
 
 def prog_path(name):
-    """-o program files: the reference's own (test.*) or ours under progs/."""
-    ours = os.path.join(HERE, "progs", name)
-    return ours if os.path.exists(ours) else os.path.join(REFDIR, name)
+    """-o program files: ours, under progs/ (none of the reference's)."""
+    return os.path.join(HERE, "progs", name)
 
 
 def run_sequence(name, fmt, nframes, seed, *, me="tss", sl=15, q=8, oracle_prog=None, rate=0,
-                 filesize=0):
-    """q=0 leaves -q off (rate control then derives InitialQuant, p64.c:579-586)."""
+                 filesize=0, frames=None):
+    """q=0 leaves -q off (rate control then derives InitialQuant, p64.c:579-586).
+    frames: constructed pictures (seed -1) instead of the seeded generator's."""
     if ONLY and name not in ONLY:
         return None
     w, h = FMT[fmt]
-    frames = [p64_amd.synth_frame(seed, t, w, h) for t in range(nframes)]
+    if frames is None:
+        frames = [p64_amd.synth_frame(seed, t, w, h) for t in range(nframes)]
+    assert len(frames) == nframes
     nmb = (w // 16) * (h // 16)
     with tempfile.TemporaryDirectory() as td:
         write_y4m(os.path.join(td, "in.y4m"), frames, w, h)
@@ -314,6 +316,75 @@ def run_sequence(name, fmt, nframes, seed, *, me="tss", sl=15, q=8, oracle_prog=
     return mbrec
 
 
+def make_tie_frames(mode, sl, seed=21):
+    """QCIF pictures 0..2 in which macroblocks of picture 1 land exactly on the
+    binary64 tie of the MTYPE decision (p64.c:745-756): VAR < 64, OMV >= 768
+    (so x >= 3) and 11 MV == 10 OMV, where `y > x/1.1` is decided by the
+    rounding of x/1.1 -- true for OMV = 11k with k = 71..102, false for
+    k = 70 and k >= 103.  Each target block is the reference (the intra
+    reconstruction of picture 0) displaced by (1, 1) plus small noise, then
+    adjusted pixel by pixel until (OMV, MV) = (11k, 10k) exactly with (1, 1)
+    still the search's choice.  Constructed with the CPU oracle, checked by
+    running the reference on the pictures."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle
+
+    w, h = FMT["QCIF"]
+    rng = np.random.default_rng(1234 + mode)
+    f0 = p64_amd.synth_frame(seed, 0, w, h)
+    f2 = p64_amd.synth_frame(seed, 2, w, h)
+    recon0 = oracle.encode_sequence([f0], w, h, quant=8)[0][3]
+    ry = recon0[:w * h].reshape(h, w).astype(np.int32)
+    f1 = p64_amd.synth_frame(seed, 1, w, h).copy()
+    y1 = f1[:w * h].reshape(h, w)  # view
+    # (mbx, mby, k, noise amplitude): k = 95/100 -> inter (2), 105/110/125 -> MC
+    targets = [(6, 2, 95, 6), (8, 5, 100, 5), (2, 6, 105, 5), (3, 5, 110, 7), (6, 5, 125, 2)]
+    hit = []
+    for mbx, mby, k, amp in targets:
+        x0, y0 = 16 * mbx, 16 * mby
+        r0 = ry[y0:y0 + 16, x0:x0 + 16]
+        rv = ry[y0 + 1:y0 + 17, x0 + 1:x0 + 17]
+        c = np.clip(rv + rng.integers(-amp, amp + 1, (16, 16)), 0, 255)
+        # pull the block toward the zero-vector source until OMV is near 11k
+        for _ in range(20000):
+            sad0, sadv = int(np.abs(c - r0).sum()), int(np.abs(c - rv).sum())
+            if (sad0 + sadv - 21 * k) % 2:  # parity of a unit step is fixed
+                k += 1
+            if sad0 == 11 * k and sadv == 10 * k:
+                break
+            d0, dv = int(np.sign(11 * k - sad0)), int(np.sign(10 * k - sadv))
+            # a unit change of one pixel moves both sums by +-1: pick a pixel
+            # and direction whose effect is (d0, dv) (0 = either, any)
+            done = False
+            for _ in range(64):
+                i, j = rng.integers(0, 16, 2)
+                for step in (1, -1):
+                    v = c[i, j] + step
+                    if not 0 <= v <= 255:
+                        continue
+                    e0 = abs(v - r0[i, j]) - abs(c[i, j] - r0[i, j])
+                    ev = abs(v - rv[i, j]) - abs(c[i, j] - rv[i, j])
+                    if (d0 == 0 or e0 == d0) and (dv == 0 or ev == dv):
+                        c[i, j] = v
+                        done = True
+                        break
+                if done:
+                    break
+        y1[y0:y0 + 16, x0:x0 + 16] = c.astype(np.uint8)
+        hit.append((mby * 11 + mbx, k))
+    me = oracle.motion_estimation(recon0[:w * h], f1[:w * h], w, h, mode, sl)
+    outcomes = set()
+    for mb, k in hit:
+        e = me[mb]
+        ok = (e["sad0"] == 11 * k and e["sad"] == 10 * k and (e["var"] < 64 or e["varor"] > e["var"]))
+        if ok:
+            outcomes.add((10 * k) / 256 > ((11 * k) / 256) / 1.1)
+        print(f"tie MB {mb}: k={k} sad0={e['sad0']} sad={e['sad']} mv=({e['mx']},{e['my']}) "
+              f"var={e['var']} varor={e['varor']} {'OK' if ok else 'MISSED'}")
+    assert outcomes == {True, False}, "both outcomes of the tie must occur"
+    return [f0, f1, f2]
+
+
 def decode_md5():
     with tempfile.TemporaryDirectory() as td:
         subprocess.run([os.path.join(REF_OUT, "p64"), "-d", "-s", os.path.join(REFDIR, "short.p64"),
@@ -325,6 +396,31 @@ def decode_md5():
                 out[f"short{i}.{c}"] = hashlib.md5(open(p, "rb").read()).hexdigest()
     with open(os.path.join(HERE, "decode.json"), "w") as f:
         json.dump(out, f, indent=1, sort_keys=True)
+
+
+def cli_golden():
+    """Outputs of two reference CLI flags (data only):
+      decode_forcecif.json  `p64 -d -c -s short.p64`: plane MD5s of the CIF
+                            frames ForceCIF decodes the NTSC stream into
+      verbose_qcif_rate.txt the BufferContents lines `-v` prints for the
+                            qcif_rate fixture's run (-QCIF -r 30000, seed 3)"""
+    with tempfile.TemporaryDirectory() as td:
+        subprocess.run([os.path.join(REF_OUT, "p64"), "-d", "-c", "-s", os.path.join(HERE, "short.p64"),
+                        os.path.join(td, "sc")], stdout=subprocess.DEVNULL, check=True)
+        out = {}
+        for i in range(7):
+            for c in "YUV":
+                out[f"sc{i}.{c}"] = hashlib.md5(open(os.path.join(td, f"sc{i}.{c}"), "rb").read()).hexdigest()
+        with open(os.path.join(HERE, "decode_forcecif.json"), "w") as f:
+            json.dump(out, f, indent=1, sort_keys=True)
+        w, h = FMT["QCIF"]
+        write_y4m(os.path.join(td, "in.y4m"), [p64_amd.synth_frame(3, t, w, h) for t in range(8)], w, h)
+        r = subprocess.run([os.path.join(REF_OUT, "p64"), "-QCIF", "-y4m", "-a", "0", "-b", "7", "-r", "30000",
+                            "-v", os.path.join(td, "in"), "-z", ".y4m", "-s", os.path.join(td, "out.p64")],
+                           capture_output=True, text=True, check=True)
+        lines = [ln for ln in r.stdout.splitlines() if ln.startswith("BufferContents:")]
+        with open(os.path.join(HERE, "verbose_qcif_rate.txt"), "w") as f:
+            f.write("\n".join(lines) + "\n")
 
 
 ONLY = set()
@@ -349,7 +445,7 @@ def main():
     run_sequence("qcif_clean_full31", "QCIF", 4, 14, me="full", sl=31, q=16)
     run_sequence("qcif_flat_tss", "QCIF", 4, 7, q=8)
     run_sequence("qcif_flat_full31", "QCIF", 4, 15, me="full", sl=31, q=4)
-    run_sequence("qcif_intra", "QCIF", 4, 7, oracle_prog="test.intra")
+    run_sequence("qcif_intra", "QCIF", 4, 7, oracle_prog="intra_only.prog")
     run_sequence("cif_full31", "CIF", 3, 1, me="full", sl=31)
     run_sequence("cif_tss", "CIF", 3, 2)
     run_sequence("ntsc_tss", "NTSC", 3, 9)
@@ -361,15 +457,22 @@ def main():
     run_sequence("cif_rate_full31", "CIF", 5, 2, me="full", sl=31, q=12, rate=300000)
     run_sequence("qcif_filesize", "QCIF", 6, 13, q=0, filesize=60000)
     # -o program interpreter (lexer.l): per-MB MTYPE (program 0), rate (program 1)
-    run_sequence("qcif_mtype", "QCIF", 6, 4, oracle_prog="test.mtype")
-    run_sequence("cif_fil_full31", "CIF", 3, 1, me="full", sl=31, oracle_prog="test.fil")
-    run_sequence("qcif_nof", "QCIF", 4, 12, oracle_prog="test.nof")
-    run_sequence("qcif_orate", "QCIF", 8, 3, q=0, rate=40000, oracle_prog="test.rate")
+    run_sequence("qcif_mtype", "QCIF", 6, 4, oracle_prog="decide.prog")
+    run_sequence("cif_fil_full31", "CIF", 3, 1, me="full", sl=31, oracle_prog="mc_filtered.prog")
+    run_sequence("qcif_nof", "QCIF", 4, 12, oracle_prog="mc_plain.prog")
+    run_sequence("qcif_orate", "QCIF", 8, 3, q=0, rate=40000, oracle_prog="rate_bc.prog")
+    # the binary64 tie of the MTYPE decision (p64.c:749), both outcomes
+    if not ONLY or {"qcif_tie_full31", "qcif_tie_tss"} & ONLY:
+        run_sequence("qcif_tie_full31", "QCIF", 3, -1, me="full", sl=31,
+                     frames=make_tie_frames(1, 31))
+        run_sequence("qcif_tie_tss", "QCIF", 3, -1, me="tss", sl=15, frames=make_tie_frames(0, 15))
     run_sequence("qcif_prog_mq", "QCIF", 5, 5, q=10, oracle_prog="mquant_bc.prog")
     run_sequence("qcif_prog_mq_rate", "QCIF", 5, 6, q=10, rate=60000, oracle_prog="mquant_bc.prog")
     run_sequence("qcif_prog_words", "QCIF", 4, 9, me="full", sl=31, oracle_prog="words.prog")
     if not ONLY:
         decode_md5()
+    if not ONLY or "cli" in ONLY:
+        cli_golden()
 
 
 if __name__ == "__main__":

@@ -7,7 +7,8 @@ import numpy as np
 import pytest
 
 from conftest import GOLDEN
-from test_oracle_golden import SEQS, check_sequence_outputs, load, sequence_frames, sequence_params
+from test_oracle_golden import (SEQS, check_sequence_outputs, load, sequence_frames, sequence_params,
+                                tie_mbs)
 
 pytestmark = pytest.mark.gpu
 
@@ -177,6 +178,26 @@ def test_sequence_golden_device(p64, torch_dev, name):
     w, h = int(z["width"]), int(z["height"])
     frames = sequence_frames(p64, z)
     outs = run_device_sequence(p64, torch_dev, frames, w, h, **sequence_params(z))
+    check_sequence_outputs(z, outs, name)
+
+
+@pytest.mark.parametrize("name", ["qcif_tie_full31", "qcif_tie_tss"])
+def test_mtype_tie_branch_on_device(p64, torch_dev, name):
+    """k_encode reaches the binary64 tie of the MTYPE decision (decide_mtype:
+    11 MV == 10 OMV with VAR < 64, p64.c:745-756) on the constructed fixture
+    and takes both outcomes exactly as the reference did: MTYPE 2 where the
+    rounded x/1.1 falls below y, motion compensation (8) where it does not."""
+    z = load(f"seq_{name}.npz")
+    w, h = int(z["width"]), int(z["height"])
+    outs = run_device_sequence(p64, torch_dev, sequence_frames(p64, z), w, h, **sequence_params(z))
+    coef, mb, me, _ = outs[1]
+    got = np.stack([me[f] for f in me.dtype.names], axis=1)
+    np.testing.assert_array_equal(got, z["merec"][1])
+    mbs = tie_mbs(z, 1)
+    assert len(mbs) >= 4
+    mt = mb["mtype"].astype(int)[mbs]
+    np.testing.assert_array_equal(mt, z["mb"][1][mbs, 0])
+    assert 2 in mt and 8 in mt
     check_sequence_outputs(z, outs, name)
 
 

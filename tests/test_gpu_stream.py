@@ -90,6 +90,32 @@ def test_cli_decode_short_p64_md5(p64, torch_dev, tmp_path):
         assert hashlib.md5((tmp_path / name).read_bytes()).hexdigest() == md5, name
 
 
+def test_cli_decode_force_cif_md5(p64, torch_dev, tmp_path):
+    """`p64gpu -d -c -s short.p64 sc`: ForceCIF (p64.c:308-310, 1071-1072)
+    decodes the NTSC stream into CIF frames; the reference's 7 x 3 MD5s."""
+    exp = json.load(open(os.path.join(GOLDEN, "decode_forcecif.json")))
+    subprocess.run([CLI, "-d", "-c", "-s", os.path.join(GOLDEN, "short.p64"), str(tmp_path / "sc")],
+                   check=True, stdout=subprocess.DEVNULL, timeout=120)
+    for name, md5 in exp.items():
+        assert hashlib.md5((tmp_path / name).read_bytes()).hexdigest() == md5, name
+
+
+def test_cli_verbose_loud_parity_flags(p64, torch_dev, tmp_path):
+    """-v prints the reference's `BufferContents: n  New Q1: q` line at every
+    rate-control update (p64.c:466-470), in the same order with the same
+    values; -l n and -p are accepted and leave the stream byte-identical."""
+    z = load("seq_qcif_rate.npz")
+    w, h = int(z["width"]), int(z["height"])
+    write_y4m(tmp_path / "in.y4m", sequence_frames(p64, z), w, h)
+    r = subprocess.run([CLI, "-QCIF", "-y4m", "-a", "0", "-b", "7", "-r", "30000", "-v", "-l", "1", "-p",
+                        str(tmp_path / "in"), "-z", ".y4m", "-s", str(tmp_path / "o.p64")],
+                       check=True, capture_output=True, text=True, timeout=300)
+    got = [ln for ln in r.stdout.splitlines() if ln.startswith("BufferContents:")]
+    exp = open(os.path.join(GOLDEN, "verbose_qcif_rate.txt")).read().splitlines()
+    assert got == exp
+    assert hashlib.sha256((tmp_path / "o.p64").read_bytes()).hexdigest() == str(z["stream_sha256"])
+
+
 def test_python_decode_short_p64_md5(p64, torch_dev):
     from p64_amd import stream
     exp = json.load(open(os.path.join(GOLDEN, "decode.json")))

@@ -82,11 +82,12 @@ def _program(name):
     return str(np.load(os.path.join(GOLDEN, f"seq_{name}.npz"))["oracle"])
 
 
-# -o runs other than test.intra (a constant MTYPE) are driven by the program
-# interpreter and pin the sequence encoder as well
-SEQS = [s for s in ALL_SEQS if _rate_controlled(s) == (0, 0) and _program(s) in ("", "test.intra")]
+# -o runs other than intra_only.prog (a constant MTYPE) are driven by the
+# program interpreter and pin the sequence encoder as well
+INTRA_PROG = "intra_only.prog"
+SEQS = [s for s in ALL_SEQS if _rate_controlled(s) == (0, 0) and _program(s) in ("", INTRA_PROG)]
 RATE_SEQS = [s for s in ALL_SEQS if _rate_controlled(s) != (0, 0) and not _program(s)]
-PROG_SEQS = [s for s in ALL_SEQS if _program(s) not in ("", "test.intra")]
+PROG_SEQS = [s for s in ALL_SEQS if _program(s) not in ("", INTRA_PROG)]
 
 
 def check_sequence_outputs(z, outs, label):
@@ -116,14 +117,17 @@ def check_sequence_outputs(z, outs, label):
 def sequence_params(z):
     me_mode = 1 if str(z["me"]) == "full" else 0
     ov = None
-    if str(z["oracle"]) == "test.intra":  # program 0 stores MTYPE 0 (test.intra)
+    if str(z["oracle"]) == INTRA_PROG:  # program 0 stores MTYPE 0
         ov = np.zeros(int(z["mb"].shape[1]), np.int8)
     return dict(quant=int(z["q"]), me_mode=me_mode, search_limit=int(z["sl"]), mtype_override=ov)
 
 
 def sequence_frames(p64, z):
     w, h = int(z["width"]), int(z["height"])
-    frames = [p64.synth_frame(int(z["seed"]), t, w, h) for t in range(int(z["nframes"]))]
+    if int(z["seed"]) < 0:  # constructed pictures (make_golden.py make_tie_frames), kept as data
+        frames = [np.ascontiguousarray(f) for f in z["frames"]]
+    else:
+        frames = [p64.synth_frame(int(z["seed"]), t, w, h) for t in range(int(z["nframes"]))]
     for t, f in enumerate(frames):  # pins the synthetic generator
         assert hashlib.sha256(f.tobytes()).hexdigest() == z["frames_sha256"][t]
     return frames
@@ -140,6 +144,32 @@ def test_sequence_golden(oracle_mod, p64, name):
     if "recon" in z.files:
         for t in range(int(z["nframes"])):
             np.testing.assert_array_equal(outs[t][3], z["recon"][t])
+
+
+def tie_mbs(z, t):
+    """Macroblocks of picture t that reach the binary64 tie of the MTYPE
+    decision (p64.c:745-756): VAR < 64 or VAROR > VAR, x = OMV/256 >= 3 (so
+    neither earlier inter test fires) and 11 MV == 10 OMV, where `y > x/1.1`
+    is decided by the rounding of the double quotient."""
+    me = z["merec"][t]
+    sad, sad0, var, varor = me[:, 2], me[:, 3], me[:, 4], me[:, 5]
+    return np.nonzero((11 * sad == 10 * sad0) & ((var < 64) | (varor > var)) & (sad0 >= 768))[0]
+
+
+@pytest.mark.parametrize("name", ["qcif_tie_full31", "qcif_tie_tss"])
+def test_mtype_tie_fixture_covers_both_outcomes(name):
+    """The constructed fixture reaches the tie with both results of the double
+    comparison: MTYPE 2 (y > x/1.1 true) and MC (false), as the reference chose."""
+    z = load(f"seq_{name}.npz")
+    mbs = tie_mbs(z, 1)
+    assert len(mbs) >= 4
+    got = set()
+    for k in mbs:
+        omv = int(z["merec"][1][k, 3])
+        inter = (omv * 10 // 11) / 256 > (omv / 256) / 1.1
+        assert int(z["mb"][1][k, 0]) in ((2,) if inter else (5, 8))
+        got.add(inter)
+    assert got == {True, False}
 
 
 def test_fixture_coverage():

@@ -294,12 +294,15 @@ def test_output_schedule_matches_reference_rules(st):
     assert st.output_schedule([30, 31, 0, 1], 2) == [1, 1, 1, 1]  # TR wraps mod 32
 
 
-def test_decode_short_p64_matches_reference_md5(p64, st, oracle_mod):
+@pytest.mark.parametrize("force_cif", [False, True])
+def test_decode_short_p64_matches_reference_md5(p64, st, oracle_mod, force_cif):
+    """Plain decode, and -c (ForceCIF, p64.c:1071-1072): the NTSC stream decoded
+    into CIF frames, GOBs 11-12 never sent (reference MD5s of `p64 -d -c`)."""
     data = open(os.path.join(GOLDEN, "short.p64"), "rb").read()
-    exp = json.load(open(os.path.join(GOLDEN, "decode.json")))
-    r = st.Reader(data)
+    exp = json.load(open(os.path.join(GOLDEN, "decode_forcecif.json" if force_cif else "decode.json")))
+    r = st.Reader(data, force_cif=force_cif)
     w, h = r.width, r.height
-    assert (r.fmt, w, h) == (st.NTSC, 352, 240)
+    assert (r.fmt, w, h) == ((st.CIF, 352, 288) if force_cif else (st.NTSC, 352, 240))
     prev = np.zeros(w * h * 3 // 2, np.uint8)
     pics, trs = [], []
     for p in r:
@@ -317,4 +320,5 @@ def test_decode_short_p64_matches_reference_md5(p64, st, oracle_mod):
     for i, pic in enumerate(out):
         planes = (pic[:w * h], pic[w * h:w * h * 5 // 4], pic[w * h * 5 // 4:])
         for c, a in zip("YUV", planes):
-            assert hashlib.md5(a.tobytes()).hexdigest() == exp[f"short{i}.{c}"], f"short{i}.{c}"
+            key = f"{'sc' if force_cif else 'short'}{i}.{c}"
+            assert hashlib.md5(a.tobytes()).hexdigest() == exp[key], key
