@@ -1500,6 +1500,7 @@ struct BlkDiv {
   uint32_t mp, sp;  // picture: 6 nmb blocks
   uint32_t mb, sb;  // luma block row: w/8 blocks
   uint32_t mw, sw;  // MB row: w/16 MBs
+  uint32_t mn, sn;  // picture: nmb MBs
 };
 static inline void magic_div(uint32_t d, uint32_t &m, uint32_t &s) {
   s = 31 - (uint32_t)__builtin_clz(d);
@@ -1511,6 +1512,7 @@ static inline BlkDiv blk_div(int w, int h) {
   magic_div((uint32_t)(6 * (w >> 4) * (h >> 4)), k.mp, k.sp);
   magic_div((uint32_t)(w >> 3), k.mb, k.sb);
   magic_div((uint32_t)(w >> 4), k.mw, k.sw);
+  magic_div((uint32_t)((w >> 4) * (h >> 4)), k.mn, k.sn);
   return k;
 }
 __device__ __forceinline__ unsigned mdiv(unsigned n, uint32_t m, uint32_t s) { return __umulhi(n, m) >> s; }
@@ -1547,6 +1549,24 @@ __device__ __forceinline__ BlkPos blk_pos(unsigned t, int w, int h, const BlkDiv
   }
   return p;
 }
+// MB-grouped block layout: wave w takes macroblocks 10w .. 10w+9 of the
+// launch, lane 6m + b block b of its m-th MB (lanes 60..63 repeat lane 59).
+// A wave's levels are then 7,680 contiguous bytes and its pixel rows and
+// records contiguous runs per plane: its HBM traffic is a few long runs
+// instead of 64 blocks scattered over a block row.
+constexpr int MBS_PER_WAVE = 10;
+__device__ __forceinline__ BlkPos blk_pos_mb(unsigned gmb, int b, int w, int h, const BlkDiv &k) {
+  const int mbw = w >> 4;
+  BlkPos p;
+  p.fi = (int)mdiv(gmb, k.mn, k.sn);
+  p.mb = (int)(gmb - (unsigned)p.fi * (unsigned)(mbw * (h >> 4)));
+  const int mby = (int)mdiv((unsigned)p.mb, k.mw, k.sw), mbx = p.mb - mby * mbw;
+  p.b = b;
+  p.plane = b < 4 ? 0 : b - 3;
+  p.x = b < 4 ? 16 * mbx + 8 * (b & 1) : 8 * mbx;
+  p.y = b < 4 ? 16 * mby + 8 * (b >> 1) : 8 * mby;
+  return p;
+}
 
 // 64 reconstructed values (already in 0..255) -> 8 row stores
 __device__ __forceinline__ void store_block(uint8_t *dst, int pw, const int v[64]) {
@@ -1574,10 +1594,76 @@ __device__ __forceinline__ void fdct_block(const uint2 rows[8], int v[64]) {
     int o[8];
     fwd_row<true>(v + 8 * r, o);
 #pragma unroll
-    for (int k = 0; k < 8; k++) v[8 * r + k] = o[k];
+    for (int k = 0; k < 8; k++) v[8 * r + k] = opaque(o[k]);  // see fdct_block_pk
     SCHED_FENCE();
   }
 }
+// The same ChenDct with the row pass in packed 16-bit arithmetic: the column
+// pass (scalar) leaves each row as four (column 2j, 2j+1) int16 pairs -- its
+// outputs stay within +-5,800 for pixel or +-255 residual input -- and the
+// row pass runs the butterfly of fwd8 on pairs: v_pk_add/sub/ashr for the
+// sums, and every product pair C_a x + C_b y as ONE v_dot2_i32_i16 with the
+// constant pair as its literal (the two products and their sum exact in
+// 32 bits, the same ms9 rounding after).  Row-pass intermediates stay below
+// 2^15: sums <= 11,600, u = d + r <= 14,000.  Half the registers of the
+// scalar form between the passes.
+typedef short s16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ s16x2 pk16(int lo, int hi) {  // two values that fit int16
+  return __builtin_bit_cast(s16x2, (uint32_t)(lo & 0xffff) | ((uint32_t)hi << 16));
+}
+__device__ __forceinline__ int dot2(s16x2 a, short ca, short cb) {
+  const s16x2 c = {ca, cb};
+  return __builtin_amdgcn_sdot2(a, c, 0, false);
+}
+// row pass of one row given as (x0,x1), (x2,x3), (x4,x5), (x6,x7)
+__device__ __forceinline__ void fwd_row_pk(const s16x2 p[4], int o[8]) {
+  const s16x2 s01 = (p[0] + p[3].yx) >> 1, s23 = (p[1] + p[2].yx) >> 1;  // (s0,s1) (s2,s3)
+  const s16x2 d01 = (p[0] - p[3].yx) >> 1, d23 = (p[1] - p[2].yx) >> 1;  // (d0,d1) (d2,d3)
+  const s16x2 e01 = s01 + s23.yx, e32 = s01 - s23.yx;                    // (e0,e1) (e3,e2)
+  o[0] = ms9(dot2(e01, C1D4, C1D4));
+  o[4] = ms9(dot2(e01, C1D4, -C1D4));
+  o[2] = ms9(dot2(e32, C1D8, C3D8));   // C3D8 e2 + C1D8 e3
+  o[6] = ms9(dot2(e32, C3D8, -C1D8));  // C3D8 e3 - C1D8 e2
+  const s16x2 q = __builtin_shufflevector(d01, d23, 1, 2);   // (d1, d2)
+  const int r1 = ms9(dot2(q, C1D4, C1D4)), r0 = ms9(dot2(q, C1D4, -C1D4));
+  const s16x2 dd = __builtin_shufflevector(d23, d01, 1, 2);  // (d3, d0)
+  const s16x2 rr = pk16(r0, r1);
+  const s16x2 u03 = dd + rr, u12 = dd - rr;                   // (u0,u3) (u1,u2)
+  o[1] = ms9(dot2(u03, C7D16, C1D16));
+  o[7] = ms9(dot2(u03, -C1D16, C7D16));
+  o[3] = ms9(dot2(u12, -C5D16, C3D16));
+  o[5] = ms9(dot2(u12, C3D16, C5D16));
+}
+// (the final rounding dct_final(v) reads the sign of v = X >> 9; hipcc then
+// takes it from X itself and keeps all 64 pre-shift sums alive next to the
+// shifted coefficients until quantisation -- 64 extra VGPRs.  The opaque copy
+// ends X's life at the shift.)
+__device__ __forceinline__ void fdct_block_pk(const uint2 rows[8], int v[64]) {
+  s16x2 p[8][4];  // [row][column pair]
+#pragma unroll
+  for (int c = 0; c < 8; c += 2) {
+    int x[8], y[8], o[8], u[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      const uint32_t wd = c < 4 ? rows[k].x : rows[k].y;
+      x[k] = (int)((wd >> (8 * (c & 3))) & 255);
+      y[k] = (int)((wd >> (8 * ((c + 1) & 3))) & 255);
+    }
+    fwd_col<true>(x, o);
+    fwd_col<true>(y, u);
+#pragma unroll
+    for (int k = 0; k < 8; k++) p[k][c >> 1] = pk16(o[k], u[k]);
+    SCHED_FENCE();
+  }
+#pragma unroll
+  for (int r = 0; r < 8; r++) {
+    fwd_row_pk(p[r], v + 8 * r);
+#pragma unroll
+    for (int k = 0; k < 8; k++) v[8 * r + k] = opaque(v[8 * r + k]);
+    SCHED_FENCE();
+  }
+}
+
 // ChenIDct (chendct.c:217-375) on a register block: column pass (inputs <<2,
 // folded into the constants), row pass, final rounding
 __device__ __forceinline__ void idct_block(int v[64]) {
@@ -1643,6 +1729,23 @@ __device__ __forceinline__ void flush_levels(const uint8_t *lds, int lane, uint3
   __builtin_amdgcn_wave_barrier();
 }
 
+// MB-grouped waves: the wave's levels are `nbytes` contiguous bytes at
+// coef + off (uniform); store k writes bytes 1024k .. 1024k+1023 of them,
+// 16 per lane, from the staging slot of the lane that owns them
+__device__ __forceinline__ void flush_levels_run(const uint8_t *lds, int lane, uint32_t off, uint32_t nbytes,
+                                                 uint8_t *coef) {
+  __builtin_amdgcn_wave_barrier();
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    const uint32_t o = 1024u * k + 16u * lane;
+    if (o < nbytes) {
+      const uint4 v = *reinterpret_cast<const uint4 *>(lds + (o >> 7) * LVL_STRIDE + (o & 127));
+      st_out(reinterpret_cast<uint4 *>(coef + off + o), v);
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+}
+
 // dword 3 of a raw buffer resource on gfx9-family parts (CDNA): 32-bit data format
 constexpr int BUF_RSRC_W3 = 0x00020000;
 
@@ -1651,25 +1754,27 @@ struct IntraFetch {
   uint2 rows[8];  // the block's pixels
   int q;          // UseQuant
 };
-__device__ __forceinline__ IntraFetch intra_fetch(const p64gpu_encode_args &a, const BlkDiv &kd,
-                                                  unsigned t) {
+// QMB: a per-MB UseQuant array is given (else a.quant, uniform, no load)
+template <bool QMB>
+__device__ __forceinline__ IntraFetch intra_fetch_at(const p64gpu_encode_args &a, const BlkPos &pos) {
   const int w = a.width, h = a.height, nmb = (w >> 4) * (h >> 4);
   IntraFetch f;
-  f.p = blk_pos(t, w, h, kd);
+  f.p = pos;
   const int pw = f.p.plane ? w >> 1 : w;
   const uint8_t *src = a.cur + (size_t)f.p.fi * a.frame_stride +
                        (uint32_t)(plane_offset(f.p.plane, w, h) + mul24(f.p.y, pw) + f.p.x);
 #pragma unroll
   for (int k = 0; k < 8; k++) f.rows[k] = *reinterpret_cast<const uint2 *>(src + (uint32_t)mul24(k, pw));
-  // UseQuant through a buffer load that is out of range (reads 0, touches no
-  // memory) when there is no per-MB array: no branch around the load, so the
-  // wait counts of the loop stay exact (a conditional load made hipcc wait
-  // for the previous block's stores before every block)
-  const __amdgpu_buffer_rsrc_t qr = __builtin_amdgcn_make_buffer_rsrc(
-      (void *)(a.quant_mb ? a.quant_mb : a.cur), (short)0, a.quant_mb ? 0x7fffffff : 0, BUF_RSRC_W3);
-  const int ql = __builtin_amdgcn_raw_buffer_load_b8(qr, (int)(f.p.fi * nmb + f.p.mb), 0, 0);
-  f.q = ql + (a.quant_mb ? 0 : a.quant);  // (an add, not a select: the load always issues)
+#if defined(PROBE_NOLOAD)
+  for (int k = 0; k < 8; k++) f.rows[k] = make_uint2(pos.x * 0x01010101u + k, pos.y * 0x03050709u ^ pos.fi);
+#endif
+  f.q = QMB ? a.quant_mb[f.p.fi * nmb + f.p.mb] : a.quant;
   return f;
+}
+template <bool QMB>
+__device__ __forceinline__ IntraFetch intra_fetch(const p64gpu_encode_args &a, const BlkDiv &kd,
+                                                  unsigned t) {
+  return intra_fetch_at<QMB>(a, blk_pos(t, a.width, a.height, kd));
 }
 // A block's outputs between its computation and its stores: the persistent
 // kernel stores block i in the middle of block i+1's computation (after its
@@ -1713,7 +1818,11 @@ __device__ __forceinline__ void intra_block(const p64gpu_encode_args &a, const I
   const float rqe = (q & 1) ? 0.0f : rq;
   const int q2 = 2 * q, qq = q - (int)!(q & 1);
   int v[64];
+#if defined(BLK_SCALAR_FDCT)
   fdct_block(f.rows, v);
+#else
+  fdct_block_pk(f.rows, v);
+#endif
   if (PENDING) intra_store(a, out, lds, lane);
   // in scan order: quantise (BoundDct + CCITTFlatQuantize + FlatBound), pack
   // the level pair, dequantise (ICCITTFlatQuantize) in place; 16 bytes of
@@ -1753,8 +1862,44 @@ __device__ __forceinline__ void intra_block(const p64gpu_encode_args &a, const I
 #ifndef BLK_PERSIST
 #define BLK_PERSIST 0
 #endif
+// intra picture, MB-grouped block layout (blk_pos_mb): one wave = 10 MBs, a
+// lane per block; levels leave as one contiguous 7,680-byte run per wave
+template <bool QMB>
+__global__ __launch_bounds__(256) BLK_OCC void k_intra_mbg(p64gpu_encode_args a, BlkDiv kd, unsigned nmbs) {
+  __shared__ __align__(16) uint8_t lvl[4 * LVL_WAVE];
+  const int lane = threadIdx.x & 63;
+  uint8_t *lds = lvl + (threadIdx.x >> 6) * LVL_WAVE;
+  const unsigned gmb0 = (blockIdx.x * 4u + (threadIdx.x >> 6)) * MBS_PER_WAVE;
+  if (gmb0 >= nmbs) return;  // whole wave
+  const int l = min(lane, 6 * MBS_PER_WAVE - 1);
+  const unsigned gmb = min(gmb0 + (unsigned)(l / 6), nmbs - 1);  // tail lanes repeat the last MB
+  const IntraFetch f = intra_fetch_at<QMB>(a, blk_pos_mb(gmb, l % 6, a.width, a.height, kd));
+  IntraOut o;
+  intra_block<false>(a, f, lds, lane, o);
+  const uint32_t nvalid = min((unsigned)MBS_PER_WAVE, nmbs - gmb0);
+#if defined(PROBE_NOCOEF)  // development probes: drop one output stream (the work stays)
+  if (o.rec[0].x == 0x12345678u)
+#endif
+  flush_levels_run(lds, lane, gmb0 * 768u, nvalid * 768u, reinterpret_cast<uint8_t *>(a.coef));
+#if defined(PROBE_NOREC)
+  if (o.rec[0].x == 0x12345678u)
+#endif
+#pragma unroll
+  for (int k = 0; k < 8; k++)
+    st_out(reinterpret_cast<uint2 *>(a.recon + o.rec_off + (uint32_t)mul24(k, o.pw)), o.rec[k]);
+  if (l % 6 == 0 && lane < 6 * MBS_PER_WAVE && gmb0 + (unsigned)(l / 6) < nmbs) {
+    p64_mb_rec r;  // p64.c:909-910: MTYPE 0, CBP 0x3f, LastIntra reset
+    r.mtype = 0;
+    r.cbp = 0x3f;
+    r.mvx = 0;
+    r.mvy = 0;
+    a.mb[gmb] = r;
+    a.last_intra[gmb] = 0;
+  }
+}
 // one launch covers at most 2 GiB of pictures and of levels (the host splits
 // larger batches), so 32-bit offsets address both
+template <bool QMB>
 __global__ __launch_bounds__(256) BLK_OCC void k_intra_blk(p64gpu_encode_args a, BlkDiv kd, unsigned total,
                                                            unsigned stride) {
   __shared__ __align__(16) uint8_t lvl[4 * LVL_WAVE];
@@ -1786,7 +1931,7 @@ __global__ __launch_bounds__(256) BLK_OCC void k_intra_blk(p64gpu_encode_args a,
 #define CLOCK_END()
 #define CLOCK_MARK(v)
 #endif
-  IntraFetch f = intra_fetch(a, kd, min(t + lane, last));
+  IntraFetch f = intra_fetch<QMB>(a, kd, min(t + lane, last));
   IntraOut o;
   if (!BLK_PERSIST) {
 #if defined(P64_TIMING)
@@ -1807,18 +1952,31 @@ __global__ __launch_bounds__(256) BLK_OCC void k_intra_blk(p64gpu_encode_args a,
   if (blockIdx.x & 1)  // development probe: odd workgroups start later
     for (int i = 0; i < BLK_STAGGER; i++) __builtin_amdgcn_s_sleep(127);
 #endif
+#if defined(BLK_PERSIST_DEFER)
   // the next block's fetch is always in flight; two fetch slots alternate
-  // (unrolled by two) so no loop-carried copy waits for a fetch
-  IntraFetch g = intra_fetch(a, kd, min(t + stride + lane, last));
+  // (unrolled by two) so no loop-carried copy waits for a fetch; each block's
+  // stores are issued inside the next block's computation
+  IntraFetch g = intra_fetch<QMB>(a, kd, min(t + stride + lane, last));
   intra_block<false>(a, f, lds, lane, o);
   for (t += stride; t < total; t += stride) {
-    f = intra_fetch(a, kd, min(t + stride + lane, last));
+    f = intra_fetch<QMB>(a, kd, min(t + stride + lane, last));
     intra_block<true>(a, g, lds, lane, o);
     t += stride;
     if (t >= total) break;
-    g = intra_fetch(a, kd, min(t + stride + lane, last));
+    g = intra_fetch<QMB>(a, kd, min(t + stride + lane, last));
     intra_block<true>(a, f, lds, lane, o);
   }
+#else
+  // the next block's fetch is in flight while this one is transformed
+  for (;;) {
+    const IntraFetch fn = intra_fetch<QMB>(a, kd, min(t + stride + lane, last));
+    intra_block<false>(a, f, lds, lane, o);
+    t += stride;
+    if (t >= total) break;
+    intra_store(a, o, lds, lane);
+    f = fn;
+  }
+#endif
   intra_store(a, o, lds, lane);
   CLOCK_END();
 }
@@ -2367,12 +2525,28 @@ static int encode_launch(const p64gpu_encode_args *a, const int32_t *mb_list, in
       c.coef = a->coef + m0 * 384;
       c.mb = a->mb + m0;
       const int64_t nblk = (int64_t)c.nframes * nmb * 6;
+#if !defined(BLK_MBMAP) || BLK_MBMAP
+      const int64_t nm = (int64_t)c.nframes * nmb, waves = (nm + MBS_PER_WAVE - 1) / MBS_PER_WAVE;
+      if (c.quant_mb)
+        hipLaunchKernelGGL(k_intra_mbg<true>, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, st, c,
+                           blk_div(a->width, a->height), (unsigned)nm);
+      else
+        hipLaunchKernelGGL(k_intra_mbg<false>, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, st, c,
+                           blk_div(a->width, a->height), (unsigned)nm);
+      (void)nblk;
+#else
       unsigned wg;
-      int s2 = persistent_grid((const void *)k_intra_blk, nblk, &wg);
+      const void *kfn = c.quant_mb ? (const void *)k_intra_blk<true> : (const void *)k_intra_blk<false>;
+      int s2 = persistent_grid(kfn, nblk, &wg);
       if (s2) return s2;
       if (!BLK_PERSIST) wg = (unsigned)((nblk + 255) / 256);
-      hipLaunchKernelGGL(k_intra_blk, dim3(wg), dim3(256), 0, st, c, blk_div(a->width, a->height),
-                         (unsigned)nblk, wg * 256u);
+      if (c.quant_mb)
+        hipLaunchKernelGGL(k_intra_blk<true>, dim3(wg), dim3(256), 0, st, c, blk_div(a->width, a->height),
+                           (unsigned)nblk, wg * 256u);
+      else
+        hipLaunchKernelGGL(k_intra_blk<false>, dim3(wg), dim3(256), 0, st, c, blk_div(a->width, a->height),
+                           (unsigned)nblk, wg * 256u);
+#endif
       HIP_TRY(hipGetLastError());
     }
     return P64GPU_OK;
