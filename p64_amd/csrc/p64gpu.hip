@@ -1155,13 +1155,15 @@ __device__ __forceinline__ void blk_put(MbLds &L, int k, int e, int v) {
 // the one rounding of the exact (c + sign c) * rq that the reference division
 // truncates (c_qrecip: trunc of that product == C's c / 2q; for c = 0 both
 // give 0).  INTRA selects the flat DC quantiser (dc: lane holds the DC).
-template <bool INTRA>
+// TIGHT: the caller's AC bounds are already +-quant_bound(q), which makes the
+// +-127 level clamp redundant (quant_bound).
+template <bool INTRA, bool TIGHT = false>
 __device__ __forceinline__ int quantise(int raw, int lo, int hi, bool dc, float rq, float rqe) {
   int v;  // clamp to [lo, hi] (per-lane bounds: one v_med3 instead of max + min)
   asm("v_med3_i32 %0, %1, %2, %3" : "=v"(v) : "v"(dct_final(raw)), "v"(lo), "v"(hi));
   const float x = (float)v;
   int l = (int)__builtin_fmaf(x, rq, __builtin_copysignf(rqe, x));
-  l = clampi(l, -127, 127);
+  if (!TIGHT) l = clampi(l, -127, 127);
   if (INTRA) l = dc ? clampi(dct_final(v), 1, 254) : l;  // (DC +- 4) / 8, transform.c:321-325
   return l;
 }
@@ -1169,12 +1171,37 @@ __device__ __forceinline__ int quantise(int raw, int lo, int hi, bool dc, float 
 // sg = sign(l) (0 for l = 0) the reconstruction (2l + sg) q, minus sg for even
 // q, is l * q2 + sg * qq with q2 = 2q and qq = q - [q even]; 0 stays 0.  An
 // uncoded block passes q2 = qq = 0 (uniform per block).  Intra DC: DC * 8.
-template <bool INTRA>
+// The quantiser l(c) = trunc((c + [q even] sign c) / 2q) is odd and monotone,
+// l(256q - 1 - e) = 127 and l(256q - e) = 128 (e = [q even]): clamping c to
+// +-min(1023, 256q - 1 - e) before it gives exactly clamp(l(clamp(c, +-1023)),
+// +-127), with one v_med3 instead of two.
+__device__ __forceinline__ int quant_bound(int q) { return min(1023, 256 * q - 1 - (int)!(q & 1)); }
+// MED3: sign(l) as one v_med3 (clampi compiles to two compares + two selects
+// on a 32-bit l; on int16 levels straight from memory the compares take the
+// half-word by SDWA for free, so the decoder keeps clampi)
+template <bool INTRA, bool MED3 = false>
 __device__ __forceinline__ int dequantise(int l, bool dc, int q2, int qq) {
-  const int sg = clampi(l, -1, 1);
+  int sg;
+  if (MED3)
+    asm("v_med3_i32 %0, %1, -1, 1" : "=v"(sg) : "v"(l));
+  else
+    sg = clampi(l, -1, 1);
   int v = __mul24(l, q2) + __mul24(sg, qq);
   if (INTRA) v = dc ? l * 8 : v;
   return v;
+}
+
+// dequantise for two int16 levels at once (decoder): packed 16-bit
+// arithmetic is exact for |level| <= 528 (|l q2 + sg qq| <= 528 * 62 + 31 <
+// 2^15); H.261 levels are at most 127 in magnitude (escape: 8-bit signed) and
+// the intra DC, at most 254, is handled by the caller.  q2/qq packed pairs.
+__device__ __forceinline__ uint32_t dequantise_pk(uint32_t l, uint32_t q2, uint32_t qq) {
+  uint32_t sg, m, r;
+  asm("v_pk_min_i16 %0, %1, %2" : "=v"(sg) : "v"(l), "s"(0x00010001u));
+  asm("v_pk_max_i16 %0, %1, %2" : "=v"(sg) : "v"(sg), "s"(0xffffffffu));
+  asm("v_pk_mul_lo_u16 %0, %1, %2" : "=v"(m) : "v"(l), "s"(q2));
+  asm("v_pk_mad_i16 %0, %1, %2, %3" : "=v"(r) : "v"(sg), "s"(qq), "v"(m));
+  return r;
 }
 
 // CBP decision from the six blocks' levels (p64.c:887-908), with wave ballots:
@@ -1612,8 +1639,12 @@ __device__ __forceinline__ s16x2 pk16(int lo, int hi) {  // two values that fit 
   return __builtin_bit_cast(s16x2, (uint32_t)(lo & 0xffff) | ((uint32_t)hi << 16));
 }
 __device__ __forceinline__ int dot2(s16x2 a, short ca, short cb) {
-  const s16x2 c = {ca, cb};
-  return __builtin_amdgcn_sdot2(a, c, 0, false);
+  // VOP3P with the constant pair in an SGPR and an inline-0 accumulator: the
+  // builtin becomes v_mov 0 + v_dot2c (6 clocks per wave instead of 4)
+  const uint32_t c = (uint32_t)(uint16_t)ca | ((uint32_t)(uint16_t)cb << 16);
+  int r;
+  asm("v_dot2_i32_i16 %0, %1, %2, 0" : "=v"(r) : "v"(a), "s"(c));
+  return r;
 }
 // row pass of one row given as (x0,x1), (x2,x3), (x4,x5), (x6,x7)
 __device__ __forceinline__ void fwd_row_pk(const s16x2 p[4], int o[8]) {
@@ -1816,7 +1847,7 @@ __device__ __forceinline__ void intra_block(const p64gpu_encode_args &a, const I
   // c_qrecip.r[q] computed in place (no dependent table load in the loop)
   const float rq = __builtin_bit_cast(float, __builtin_bit_cast(uint32_t, 1.0f / (float)(2 * q)) + 1u);
   const float rqe = (q & 1) ? 0.0f : rq;
-  const int q2 = 2 * q, qq = q - (int)!(q & 1);
+  const int q2 = 2 * q, qq = q - (int)!(q & 1), qb = quant_bound(q);
   int v[64];
 #if defined(BLK_SCALAR_FDCT)
   fdct_block(f.rows, v);
@@ -1837,10 +1868,10 @@ __device__ __forceinline__ void intra_block(const p64gpu_encode_args &a, const I
       for (int i = 0; i < 2; i++) {
         const int e = k_zz.inv[8 * k + 2 * j + i];
         const bool dc = e == 0;
-        l2[i] = quantise<true>(v[e], dc ? -0x7fffffff : -1023, dc ? 2047 : 1023, dc, rq, rqe);
-        v[e] = dequantise<true>(l2[i], dc, q2, qq);
+        l2[i] = quantise<true, true>(v[e], dc ? -0x7fffffff : -qb, dc ? 2047 : qb, dc, rq, rqe);
+        v[e] = dequantise<true, true>(l2[i], dc, q2, qq);
       }
-      pk[j] = (uint32_t)(l2[0] & 0xffff) | ((uint32_t)l2[1] << 16);
+      pk[j] = __builtin_amdgcn_perm((uint32_t)l2[1], (uint32_t)l2[0], 0x05040100u);
     }
     put_levels(lds, lane, k, make_uint4(pk[0], pk[1], pk[2], pk[3]));
     SCHED_FENCE();
@@ -2120,17 +2151,17 @@ __device__ __forceinline__ void rec_block(int w, int h, int64_t stride, __amdgpu
   int v[64];
   if (S.ck) {  // IZigzagMatrix + ICCITT(Flat)Quantize straight from the packed levels
     const int q = A.q;
-    const int q2 = 2 * q, qq = q - (int)!(q & 1);
+    const uint32_t q2 = 0x20002u * (uint32_t)q, qq = 0x10001u * (uint32_t)(q - (int)!(q & 1));
 #pragma unroll
     for (int k = 0; k < 8; k++) {
 #pragma unroll
-      for (int i = 0; i < 8; i++) {
-        const uint32_t wd = S.lq[k][i >> 1];
-        const int l = (i & 1) ? (int)wd >> 16 : (int)(int16_t)(wd & 0xffff);
-        const int e = k_zz.inv[8 * k + i];
-        v[e] = S.inter ? dequantise<false>(l, false, q2, qq) : dequantise<true>(l, e == 0, q2, qq);
+      for (int j = 0; j < 4; j++) {
+        const uint32_t d = dequantise_pk(S.lq[k][j], q2, qq);
+#pragma unroll
+        for (int i = 0; i < 2; i++) v[k_zz.inv[8 * k + 2 * j + i]] = i ? (int)d >> 16 : (int)(int16_t)(d & 0xffff);
       }
     }
+    if (!S.inter) v[0] = (int)(int16_t)(S.lq[0][0] & 0xffff) * 8;  // intra DC
     idct_block(v);
   } else {
 #pragma unroll
@@ -2172,22 +2203,26 @@ __global__ __launch_bounds__(256) BLK_OCC void k_recon_blk(int w, int h, int64_t
   const __amdgpu_buffer_rsrc_t rec =
       __builtin_amdgcn_make_buffer_rsrc((void *)recp, (short)0, (int)(nfr * stride), BUF_RSRC_W3);
   const unsigned last = total - 1;
-  RecStageA A = rec_stage_a(B, w, h, kd, t);
-  RecStageA An = rec_stage_a(B, w, h, kd, min(t + gstride, last));
-  RecStageB S = rec_stage_b(B, w, h, stride, A);
+  RecStageA A0 = rec_stage_a(B, w, h, kd, t);
+  RecStageA A1 = rec_stage_a(B, w, h, kd, min(t + gstride, last));
+  RecStageB S0 = rec_stage_b(B, w, h, stride, A0);
   // drain the pipeline fill: entering the loop with nothing pending keeps
   // hipcc's wait counts inside it exact (see k_intra_blk)
   __builtin_amdgcn_s_waitcnt(0);
+  // unrolled by two so the stage-B registers alternate between S0 and S1
+  // instead of being copied (and waited for) at the back-edge
   for (;;) {  // every lane reaches t >= total: no lane is left behind
-    const unsigned tn = t + gstride;
-    const RecStageA Ann = rec_stage_a(B, w, h, kd, min(tn + gstride, last));  // block i+2
-    const RecStageB Sn = rec_stage_b(B, w, h, stride, An);                     // block i+1
-    rec_block(w, h, stride, rec, A, S);
-    if (tn >= total) break;
-    A = An;
-    An = Ann;
-    S = Sn;
-    t = tn;
+    const RecStageA A2 = rec_stage_a(B, w, h, kd, min(t + 2 * gstride, last));  // block i+2
+    const RecStageB S1 = rec_stage_b(B, w, h, stride, A1);                      // block i+1
+    rec_block(w, h, stride, rec, A0, S0);
+    if (t + gstride >= total) break;
+    const RecStageA A3 = rec_stage_a(B, w, h, kd, min(t + 3 * gstride, last));  // block i+3
+    S0 = rec_stage_b(B, w, h, stride, A2);                                      // block i+2
+    rec_block(w, h, stride, rec, A1, S1);
+    if (t + 2 * gstride >= total) break;
+    A0 = A2;
+    A1 = A3;
+    t += 2 * gstride;
   }
 }
 
