@@ -1181,12 +1181,16 @@ __device__ __forceinline__ int quant_bound(int q) { return min(1023, 256 * q - 1
 // half-word by SDWA for free, so the decoder keeps clampi)
 template <bool INTRA, bool MED3 = false>
 __device__ __forceinline__ int dequantise(int l, bool dc, int q2, int qq) {
-  int sg;
-  if (MED3)
+  int sg, v;
+  if (MED3) {  // the 24-bit multiplies spelled out: behind the asm sign hipcc
+               // loses the operand ranges and falls back to v_mad_u64_u32
     asm("v_med3_i32 %0, %1, -1, 1" : "=v"(sg) : "v"(l));
-  else
+    asm("v_mul_i32_i24 %0, %1, %2" : "=v"(v) : "v"(sg), "v"(qq));
+    asm("v_mad_i32_i24 %0, %1, %2, %3" : "=v"(v) : "v"(l), "v"(q2), "v"(v));
+  } else {
     sg = clampi(l, -1, 1);
-  int v = __mul24(l, q2) + __mul24(sg, qq);
+    v = __mul24(l, q2) + __mul24(sg, qq);
+  }
   if (INTRA) v = dc ? l * 8 : v;
   return v;
 }
