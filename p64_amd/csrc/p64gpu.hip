@@ -1519,6 +1519,20 @@ constexpr ZigZag k_zz = make_zigzag();  // compile-time copy for register renami
 #define SCHED_FENCE() __builtin_amdgcn_sched_barrier(0)
 #endif
 
+// A wave issues its loads at raised priority (-DNO_SETPRIO: not), so a freshly
+// launched wave gets its requests out ahead of the older waves' arithmetic
+#if !defined(NO_SETPRIO)
+#define PRIO_HIGH() __builtin_amdgcn_s_setprio(3)
+#define PRIO_LOW() __builtin_amdgcn_s_setprio(0)
+#else
+#define PRIO_HIGH()
+#define PRIO_LOW()
+#endif
+#if defined(SETPRIO_ST)  // and its stores
+#define PRIO_ST() __builtin_amdgcn_s_setprio(3)
+#else
+#define PRIO_ST()
+#endif
 // occupancy hint for the block-layout kernels (-DBLK_WAVES=n: at least n waves
 // per SIMD, i.e. at most 512/n VGPRs)
 #if defined(BLK_WAVES) && BLK_WAVES > 0
@@ -1906,12 +1920,15 @@ __global__ __launch_bounds__(256) BLK_OCC void k_intra_mbg(p64gpu_encode_args a,
   uint8_t *lds = lvl + (threadIdx.x >> 6) * LVL_WAVE;
   const unsigned gmb0 = (blockIdx.x * 4u + (threadIdx.x >> 6)) * MBS_PER_WAVE;
   if (gmb0 >= nmbs) return;  // whole wave
+  PRIO_HIGH();
   const int l = min(lane, 6 * MBS_PER_WAVE - 1);
   const unsigned gmb = min(gmb0 + (unsigned)(l / 6), nmbs - 1);  // tail lanes repeat the last MB
   const IntraFetch f = intra_fetch_at<QMB>(a, blk_pos_mb(gmb, l % 6, a.width, a.height, kd));
+  PRIO_LOW();
   IntraOut o;
   intra_block<false>(a, f, lds, lane, o);
   const uint32_t nvalid = min((unsigned)MBS_PER_WAVE, nmbs - gmb0);
+  PRIO_ST();
 #if defined(PROBE_NOCOEF)  // development probes: drop one output stream (the work stays)
   if (o.rec[0].x == 0x12345678u)
 #endif
@@ -2106,24 +2123,33 @@ __device__ __forceinline__ RecStageA rec_stage_a(const RecBufs &B, int w, int h,
   A.coded = __builtin_amdgcn_raw_buffer_load_b8(B.mask, gmb, 0, 0);
   return A;
 }
+// does block p.b of the MB carry levels (MTYPE with TCOEFF, CBP bit; p64.c:1200)
+__device__ __forceinline__ bool rec_block_coded(const RecStageA &A) {
+  const int mt = (int)(int8_t)(A.m & 0xff);
+  const int cbp = mt_cbp(mt) ? (int)((A.m >> 8) & 0x3f) : 0x3f;
+  return A.coded && mt_tcoeff(mt) && ((cbp >> (5 - A.p.b)) & 1);
+}
+// LEVELS: load the block's levels into S.lq (else the caller fills them)
+template <bool LEVELS = true>
 __device__ __forceinline__ RecStageB rec_stage_b(const RecBufs &B, int w, int h, int64_t stride,
                                                  const RecStageA &A) {
   const int nmb = (w >> 4) * (h >> 4);
   const BlkPos &p = A.p;
   const int mt = (int)(int8_t)(A.m & 0xff);
-  const int cbp = mt_cbp(mt) ? (int)((A.m >> 8) & 0x3f) : 0x3f;  // p64.c:1200
   RecStageB S;
-  S.ck = A.coded && mt_tcoeff(mt) && ((cbp >> (5 - p.b)) & 1);
+  S.ck = rec_block_coded(A);
   S.inter = A.coded && !mt_intra(mt);
   S.filter = mt_filter(mt);
-  const uint32_t co = S.ck ? (uint32_t)(((p.fi * nmb + p.mb) * 6 + p.b) * 128) : BUF_OOB;
+  if (LEVELS) {
+    const uint32_t co = S.ck ? (uint32_t)(((p.fi * nmb + p.mb) * 6 + p.b) * 128) : BUF_OOB;
 #pragma unroll
-  for (int k = 0; k < 8; k++) {
-    const auto v = __builtin_amdgcn_raw_buffer_load_b128(B.coef, co + 16 * k, 0, 0);
-    S.lq[k][0] = v[0];
-    S.lq[k][1] = v[1];
-    S.lq[k][2] = v[2];
-    S.lq[k][3] = v[3];
+    for (int k = 0; k < 8; k++) {
+      const auto v = __builtin_amdgcn_raw_buffer_load_b128(B.coef, co + 16 * k, 0, 0);
+      S.lq[k][0] = v[0];
+      S.lq[k][1] = v[1];
+      S.lq[k][2] = v[2];
+      S.lq[k][3] = v[3];
+    }
   }
   const int pw = p.plane ? w >> 1 : w, ph = p.plane ? h >> 1 : h;
   int dx = 0, dy = 0;
@@ -2174,6 +2200,7 @@ __device__ __forceinline__ void rec_block(int w, int h, int64_t stride, __amdgpu
   if (S.inter) add_pred(S.pred, S.filter, v);
 #pragma unroll
   for (int e = 0; e < 64; e++) v[e] = clampi(v[e], 0, 255);  // BoundIDctMatrix
+  PRIO_ST();
   // buffer stores, out of range (dropped) for MBs that are not coded: no
   // branch around the stores either
   const int pw = p.plane ? w >> 1 : w;
@@ -2228,6 +2255,80 @@ __global__ __launch_bounds__(256) BLK_OCC void k_recon_blk(int w, int h, int64_t
     A1 = A3;
     t += 2 * gstride;
   }
+}
+
+#ifndef RECON_WAVES
+#define RECON_WAVES 3
+#endif
+#define RECON_OCC __attribute__((amdgpu_waves_per_eu(RECON_WAVES)))
+// decoder reconstruction, MB-grouped block layout (blk_pos_mb), one block per
+// lane and no loop: 10 MBs per wave, each lane loads its MB's record, then its
+// levels and prediction, reconstructs and stores.  Without the persistent
+// kernel's in-flight registers it fits 4 waves per SIMD, and those waves hide
+// each other's two dependent load latencies (measured faster than
+// k_recon_blk, whose 237 VGPRs allow 2).  Lanes past the batch (and lanes
+// 60..63) get coded = 0: every load and store of theirs is out of range.
+__global__ __launch_bounds__(256) RECON_OCC void k_recon_mbg(int w, int h, int64_t stride, const uint8_t *refp,
+                                                           uint8_t *recp, const int16_t *coef,
+                                                           const p64_mb_rec *mbr, const uint8_t *quant_mb,
+                                                           const uint8_t *coded_mask, BlkDiv kd, unsigned nmbs) {
+#if defined(RECON_LDS_LEVELS)
+  __shared__ __align__(16) uint8_t lvl[4 * LVL_WAVE];
+  uint8_t *lds = lvl + (threadIdx.x >> 6) * LVL_WAVE;
+#endif
+  const int lane = threadIdx.x & 63;
+  const unsigned gmb0 = (blockIdx.x * 4u + (threadIdx.x >> 6)) * MBS_PER_WAVE;
+  if (gmb0 >= nmbs) return;  // whole wave
+  const int nmb = (w >> 4) * (h >> 4), nfr = (int)(nmbs / (unsigned)nmb);
+  RecBufs B;
+  B.ref = __builtin_amdgcn_make_buffer_rsrc((void *)refp, (short)0, (int)(nfr * stride), BUF_RSRC_W3);
+  B.coef = __builtin_amdgcn_make_buffer_rsrc((void *)coef, (short)0, nfr * nmb * 768, BUF_RSRC_W3);
+  B.mb = __builtin_amdgcn_make_buffer_rsrc((void *)mbr, (short)0, nfr * nmb * 4, BUF_RSRC_W3);
+  B.q = __builtin_amdgcn_make_buffer_rsrc((void *)quant_mb, (short)0, nfr * nmb, BUF_RSRC_W3);
+  B.mask = __builtin_amdgcn_make_buffer_rsrc((void *)coded_mask, (short)0, nfr * nmb, BUF_RSRC_W3);
+  const __amdgpu_buffer_rsrc_t rec =
+      __builtin_amdgcn_make_buffer_rsrc((void *)recp, (short)0, (int)(nfr * stride), BUF_RSRC_W3);
+  PRIO_HIGH();
+  const int l = min(lane, 6 * MBS_PER_WAVE - 1);
+  const unsigned g = gmb0 + (unsigned)(l / 6);
+  const bool valid = lane < 6 * MBS_PER_WAVE && g < nmbs;
+  const unsigned gmb = min(g, nmbs - 1);
+  RecStageA A;
+  A.p = blk_pos_mb(gmb, l % 6, w, h, kd);
+  A.m = __builtin_amdgcn_raw_buffer_load_b32(B.mb, 4 * gmb, 0, 0);
+  A.q = __builtin_amdgcn_raw_buffer_load_b8(B.q, gmb, 0, 0);
+  A.coded = __builtin_amdgcn_raw_buffer_load_b8(B.mask, valid ? gmb : BUF_OOB, 0, 0);
+#if !defined(RECON_LDS_LEVELS)
+  const RecStageB S = rec_stage_b(B, w, h, stride, A);
+  PRIO_LOW();
+#else
+  // -DRECON_LDS_LEVELS (measured slower, 42.3 vs 38.3 us): the wave's levels
+  // are one contiguous run of 7,680 bytes: read it with whole-line loads (16
+  // bytes per lane, consecutive lanes consecutive) into the LDS staging, 144
+  // bytes per block, skipping the chunks of blocks that carry no levels
+  // (their offsets out of range: zeros, no traffic); a lane then takes its
+  // block's 128 bytes from LDS.
+  RecStageB S = rec_stage_b<false>(B, w, h, stride, A);
+  const uint64_t ckm = __ballot(S.ck);
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    const int c = lane + 64 * k, j = c >> 3;  // 16-byte chunk, its block (lane)
+    const bool on = c < 8 * 6 * MBS_PER_WAVE && ((ckm >> j) & 1);
+    const auto v = __builtin_amdgcn_raw_buffer_load_b128(B.coef, on ? gmb0 * 768u + 16u * c : BUF_OOB, 0, 0);
+    if (c < 8 * 6 * MBS_PER_WAVE)
+      *reinterpret_cast<uint4 *>(lds + j * LVL_STRIDE + (c & 7) * 16) = make_uint4(v[0], v[1], v[2], v[3]);
+  }
+  __builtin_amdgcn_wave_barrier();
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    const uint4 v = *reinterpret_cast<const uint4 *>(lds + lane * LVL_STRIDE + k * 16);
+    S.lq[k][0] = v.x;
+    S.lq[k][1] = v.y;
+    S.lq[k][2] = v.z;
+    S.lq[k][3] = v.w;
+  }
+#endif
+  rec_block(w, h, stride, rec, A, S);
 }
 
 // batched 8x8 block operations (one thread per block; shares the device
@@ -2389,6 +2490,15 @@ bool mb_layout_forced() {
     return e && *e && *e != '0';
   }();
   return forced;
+}
+// P64GPU_RECON_PERSISTENT=1: the persistent pipelined decoder k_recon_blk
+// instead of k_recon_mbg (kept for A/B measurements)
+bool recon_persistent() {
+  static const bool on = [] {
+    const char *e = getenv("P64GPU_RECON_PERSISTENT");
+    return e && *e && *e != '0';
+  }();
+  return on;
 }
 
 }  // namespace
@@ -2612,20 +2722,28 @@ int p64gpu_decode_recon(int w, int h, int nframes, int64_t stride, const uint8_t
   const unsigned grid = (unsigned)((int64_t)nframes * nmb);
   if (!mb_layout_forced()) {
     // pictures per launch: every buffer of a launch within the 2 GiB range
-    // of k_recon_blk's 32-bit buffer offsets
+    // of the block kernels' 32-bit buffer offsets
     const int64_t per = (int64_t)nmb * 768 > stride ? (int64_t)nmb * 768 : stride;
     const int chunk = (int)((((int64_t)1 << 31) - 1) / per);
     for (int f0 = 0; f0 < nframes; f0 += chunk) {
       const int nf = nframes - f0 < chunk ? nframes - f0 : chunk;
       const int64_t blocks = (int64_t)nf * nmb * 6;
-      unsigned wg;
-      int s2 = persistent_grid((const void *)k_recon_blk, blocks, &wg);
-      if (s2) return s2;
       const size_t m0 = (size_t)f0 * nmb;
-      hipLaunchKernelGGL(k_recon_blk, dim3(wg), dim3(256), 0, (hipStream_t)stream, w, h, stride,
-                         ref + (size_t)f0 * stride, recon + (size_t)f0 * stride, coef + m0 * 384,
-                         mb + m0, quant_mb + m0, coded_mask + m0, blk_div(w, h), (unsigned)blocks,
-                         wg * 256u);
+      if (recon_persistent()) {
+        unsigned wg;
+        int s2 = persistent_grid((const void *)k_recon_blk, blocks, &wg);
+        if (s2) return s2;
+        hipLaunchKernelGGL(k_recon_blk, dim3(wg), dim3(256), 0, (hipStream_t)stream, w, h, stride,
+                           ref + (size_t)f0 * stride, recon + (size_t)f0 * stride, coef + m0 * 384,
+                           mb + m0, quant_mb + m0, coded_mask + m0, blk_div(w, h), (unsigned)blocks,
+                           wg * 256u);
+      } else {
+        const unsigned nmbs = (unsigned)((int64_t)nf * nmb);
+        const unsigned waves = (nmbs + MBS_PER_WAVE - 1) / MBS_PER_WAVE;
+        hipLaunchKernelGGL(k_recon_mbg, dim3((waves + 3) / 4), dim3(256), 0, (hipStream_t)stream, w, h,
+                           stride, ref + (size_t)f0 * stride, recon + (size_t)f0 * stride, coef + m0 * 384,
+                           mb + m0, quant_mb + m0, coded_mask + m0, blk_div(w, h), nmbs);
+      }
       HIP_TRY(hipGetLastError());
     }
     return P64GPU_OK;

@@ -83,6 +83,14 @@ __global__ __launch_bounds__(256) void k(uint32_t seed, int iters, uint32_t* out
         if (OP == 61) asm("v_mul_i32_i24_e32 %0, 0x16a, %1" : "=v"(a[j]) : "v"(a[j]));
         if (OP == 62) asm("v_pk_add_u16 %0, %1, %2 op_sel:[1,0] op_sel_hi:[0,1]" : "=v"(a[j]) : "v"(x), "v"(a[j]));
         if (OP == 63) asm("v_sub_u32_e32 %0, %1, %2" : "=v"(a[j]) : "v"(x), "v"(a[j]));
+        if (OP == 64) asm("v_mad_u64_u32 %0, s[2:3], %1, %2, %3" : "=v"(*(uint64_t*)&a[j & 6]) : "v"(x), "v"(a[(j + 1) & 7]), "v"(*(uint64_t*)&a[j & 6]) : "s2", "s3");
+        if (OP == 65) asm("v_pk_min_i16 %0, %1, %2" : "=v"(a[j]) : "v"(x), "v"(a[j]));
+        if (OP == 66) asm("v_pk_mul_lo_u16 %0, %1, %2" : "=v"(a[j]) : "v"(x), "v"(a[j]));
+        if (OP == 67) asm("v_add_u32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_1 src1_sel:DWORD" : "=v"(a[j]) : "v"(x), "v"(a[j]));
+        if (OP == 68) asm("v_mul_i32_i24_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_1 src1_sel:DWORD" : "=v"(a[j]) : "v"(x), "v"(a[j]));
+        if (OP == 69) asm("v_mov_b32_e32 %0, %1" : "=v"(a[j]) : "v"(a[j] ^ x));
+        if (OP == 70) asm("v_bfe_i32 %0, %1, 0, 16" : "=v"(a[j]) : "v"(a[j]));
+        if (OP == 71) asm("v_mul_hi_u32 %0, %1, %2" : "=v"(a[j]) : "v"(x), "v"(a[j]));
       }
     asm volatile("" : "+v"(r[0]), "+v"(r[3]));
   }
@@ -117,8 +125,22 @@ void run(const char* name, uint32_t* d) {
          name, SOP ? "sgpr" : "vgpr", best, winstr / best / 1e9, ghz, ghz * 1e9 / per_simd);
 }
 
-int main() {
+int main(int argc, char** argv) {
   uint32_t* d; (void)hipMalloc(&d, 256 * 4096 * 4 * 4);
+  if (argc > 1) {  // only the later additions (and the PMC calibration pair)
+    run<1, false>("v_add3_u32", d);
+    run<64, false>("v_mad_u64_u32", d);
+    run<65, false>("v_pk_min_i16", d);
+    run<66, false>("v_pk_mul_lo_u16", d);
+    run<67, false>("v_add_u32_sdwa", d);
+    run<68, false>("v_mul_i32_i24_sdwa", d);
+    run<69, false>("v_mov_b32+xor", d);
+    run<70, false>("v_bfe_i32", d);
+    run<71, false>("v_mul_hi_u32", d);
+    run<29, false>("v_add_u32_e32", d);
+    run<58, false>("v_mul_lo_u32", d);
+    return 0;
+  }
   run<1, false>("v_add3_u32", d);
   run<0, true>("v_sad_u8", d);
   run<0, false>("v_sad_u8", d);
