@@ -28,6 +28,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 
 #include "../../include/p64gpu.h"
 
@@ -1687,7 +1688,9 @@ __device__ __forceinline__ void fwd_row_pk(const s16x2 p[4], int o[8]) {
 // takes it from X itself and keeps all 64 pre-shift sums alive next to the
 // shifted coefficients until quantisation -- 64 extra VGPRs.  The opaque copy
 // ends X's life at the shift.)
-__device__ __forceinline__ void fdct_block_pk(const uint2 rows[8], int v[64]) {
+// RES: the input is the residual rows - prow (both packed pixel rows)
+template <bool RES = false>
+__device__ __forceinline__ void fdct_block_pk(const uint2 rows[8], int v[64], const uint2 *prow = nullptr) {
   s16x2 p[8][4];  // [row][column pair]
 #pragma unroll
   for (int c = 0; c < 8; c += 2) {
@@ -1697,6 +1700,11 @@ __device__ __forceinline__ void fdct_block_pk(const uint2 rows[8], int v[64]) {
       const uint32_t wd = c < 4 ? rows[k].x : rows[k].y;
       x[k] = (int)((wd >> (8 * (c & 3))) & 255);
       y[k] = (int)((wd >> (8 * ((c + 1) & 3))) & 255);
+      if (RES) {
+        const uint32_t pd = c < 4 ? prow[k].x : prow[k].y;
+        x[k] -= (int)((pd >> (8 * (c & 3))) & 255);
+        y[k] -= (int)((pd >> (8 * ((c + 1) & 3))) & 255);
+      }
     }
     fwd_col<true>(x, o);
     fwd_col<true>(y, u);
@@ -2257,6 +2265,10 @@ __global__ __launch_bounds__(256) BLK_OCC void k_recon_blk(int w, int h, int64_t
   }
 }
 
+#ifndef INTER_WAVES
+#define INTER_WAVES 3
+#endif
+#define INTER_OCC __attribute__((amdgpu_waves_per_eu(INTER_WAVES)))
 #ifndef RECON_WAVES
 #define RECON_WAVES 3
 #endif
@@ -2329,6 +2341,196 @@ __global__ __launch_bounds__(256) RECON_OCC void k_recon_mbg(int w, int h, int64
   }
 #endif
   rec_block(w, h, stride, rec, A, S);
+}
+
+// ---------------------------------------------------------------------------
+// inter picture, second stage of the split encoder: k_motion writes every
+// MB's ME record, then this block-layout kernel does the rest of
+// ReadCompressMDU / CompressMDU (p64.c:734-1013) with one lane per 8x8 block
+// (10 MBs per wave, lane = 6m + b, as k_intra_mbg): MTYPE decision from the
+// ME record, prediction (MC, loop filter), ChenDct of the residual,
+// quantisation, the CBP decision across the MB's six lanes (wave ballots),
+// zigzag levels through the LDS staging, dequantisation, ChenIDct and the
+// reconstruction.  The fused one-wave-per-MB k_encode spends 40% of its time
+// in this half with 48 of 64 lanes busy on LDS-exchanged row passes; here
+// every lane holds its block in registers.
+struct InterMe {  // the fields of p64_me_rec the decision needs
+  int mx, my, sad, sad0, var, varor;
+};
+// prediction of the lane's block for MTYPE mt / vector (mvx, mvy), packed rows
+__device__ __forceinline__ void inter_pred(const RecBufs &B, int w, int h, int64_t stride, const BlkPos &p,
+                                           int mt, int mvx, int mvy, uint2 prow[8]) {
+  RecStageA A;
+  A.p = p;
+  A.m = (uint32_t)(mt & 0xff) | ((uint32_t)(mvx & 0xff) << 16) | ((uint32_t)(mvy & 0xff) << 24);
+  A.q = 0;
+  A.coded = 1;
+  const RecStageB S = rec_stage_b<false>(B, w, h, stride, A);  // source OOB (zeros) if intra
+  const PredSrc &P = S.pred;
+  if (S.filter) {  // add_pred's loop filter, one packed row at a time
+    int hp[8], hc[8], hn[8];
+    hz_row(P, 0, hc);
+    hz_row(P, 1, hn);
+#pragma unroll
+    for (int r = 0; r < 8; r++) {
+      int o[8];
+#pragma unroll
+      for (int k = 0; k < 8; k++)
+        o[k] = (r == 0 || r == 7) ? ((hc[k] << 2) + 8) >> 4 : (hp[k] + 2 * hc[k] + hn[k] + 8) >> 4;
+      prow[r] = pack8(o);
+#pragma unroll
+      for (int k = 0; k < 8; k++) {
+        hp[k] = hc[k];
+        hc[k] = hn[k];
+      }
+      if (r + 2 < 8) hz_row(P, r + 2, hn);
+    }
+  } else {  // the source rows as they are
+#pragma unroll
+    for (int r = 0; r < 8; r++)
+      prow[r] = make_uint2(align4(P.d[r][1], P.d[r][0], P.sh), align4(P.d[r][2], P.d[r][1], P.sh));
+  }
+}
+template <bool QMB>
+__global__ __launch_bounds__(256) INTER_OCC void k_inter_mbg(p64gpu_encode_args a, BlkDiv kd, unsigned nmbs,
+                                                             const p64_me_rec *me) {
+  __shared__ __align__(16) uint8_t lvl[4 * LVL_WAVE];
+  const int lane = threadIdx.x & 63;
+  uint8_t *lds = lvl + (threadIdx.x >> 6) * LVL_WAVE;
+  const unsigned gmb0 = (blockIdx.x * 4u + (threadIdx.x >> 6)) * MBS_PER_WAVE;
+  if (gmb0 >= nmbs) return;  // whole wave
+  const int w = a.width, h = a.height, nmb = (w >> 4) * (h >> 4), nfr = (int)(nmbs / (unsigned)nmb);
+  const int64_t stride = a.frame_stride;
+  RecBufs B;
+  B.ref = __builtin_amdgcn_make_buffer_rsrc((void *)a.ref, (short)0, (int)(nfr * stride), BUF_RSRC_W3);
+  PRIO_HIGH();
+  const int l = min(lane, 6 * MBS_PER_WAVE - 1), b = l % 6;
+  const unsigned gmb = min(gmb0 + (unsigned)(l / 6), nmbs - 1);  // tail lanes repeat the last MB
+  const BlkPos pos = blk_pos_mb(gmb, b, w, h, kd);
+  const IntraFetch f = intra_fetch_at<QMB>(a, pos);  // current rows, q
+  const __amdgpu_buffer_rsrc_t mer =
+      __builtin_amdgcn_make_buffer_rsrc((void *)me, (short)0, (int)(nmbs * sizeof(p64_me_rec)), BUF_RSRC_W3);
+  const uint32_t mo = gmb * (uint32_t)sizeof(p64_me_rec);
+  InterMe m;
+  m.mx = (int)__builtin_amdgcn_raw_buffer_load_b32(mer, mo + 0, 0, 0);
+  m.my = (int)__builtin_amdgcn_raw_buffer_load_b32(mer, mo + 4, 0, 0);
+  m.sad = (int)__builtin_amdgcn_raw_buffer_load_b32(mer, mo + 8, 0, 0);
+  m.sad0 = (int)__builtin_amdgcn_raw_buffer_load_b32(mer, mo + 12, 0, 0);
+  m.var = (int)__builtin_amdgcn_raw_buffer_load_b32(mer, mo + 16, 0, 0);
+  m.varor = (int)__builtin_amdgcn_raw_buffer_load_b32(mer, mo + 20, 0, 0);
+  const int li = a.last_intra[gmb];
+  const int ov = a.mtype_override ? (int)a.mtype_override[gmb] : -1;
+
+  // MTYPE (p64.c:734-772): the decision, the -o override, the intra refresh
+  MeOut mo_;
+  mo_.mx = m.mx;
+  mo_.my = m.my;
+  mo_.sad = m.sad;
+  mo_.sad0 = m.sad0;
+  mo_.var = m.var;
+  mo_.varor = m.varor;
+  mo_.mwor = 0;
+  int mt = decide_mtype(mo_);
+  if (ov >= 0) mt = ov;
+  if (li > 131) mt = 0;
+  const int mvx = m.mx, mvy = m.my;
+  uint2 prow[8];
+  inter_pred(B, w, h, stride, pos, mt, mvx, mvy, prow);
+  PRIO_LOW();
+
+  const bool intra = mt_intra(mt), tc = mt_tcoeff(mt);
+  const int q = f.q;
+  const float rq = __builtin_bit_cast(float, __builtin_bit_cast(uint32_t, 1.0f / (float)(2 * q)) + 1u);
+  const float rqe = (q & 1) ? 0.0f : rq;
+  const int qe = (int)!(q & 1), qbr = 256 * q - 1 - qe, qb = min(1023, qbr);
+  int v[64];
+  fdct_block_pk<true>(f.rows, v, prow);
+  // quantise in scan order into the LDS staging (levels of a block whose MB
+  // type carries no coefficients are 0); Σ l^2 for the CBP decision:
+  // Σ|l| > 1 <=> Σ l^2 > 1 and Σ|l| > 0 <=> Σ l^2 > 0 for integers
+  int ss = 0;
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    uint32_t pk[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      int l2[2];
+#pragma unroll
+      for (int i = 0; i < 2; i++) {
+        const int e = k_zz.inv[8 * k + 2 * j + i];
+        if (e == 0) {  // DC: intra (DC +- 4) / 8 in 1..254, inter as AC with DC bounds
+          const int c = dct_final(v[0]);
+          int vi;
+          asm("v_med3_i32 %0, %1, %2, %3" : "=v"(vi) : "v"(c), "v"(-qbr), "v"(min(2047, qbr)));
+          const float x = (float)vi;
+          const int li_ = (int)__builtin_fmaf(x, rq, __builtin_copysignf(rqe, x));
+          const int ld = clampi(dct_final(min(c, 2047)), 1, 254);
+          l2[i] = intra ? ld : li_;
+        } else {
+          l2[i] = quantise<false, true>(v[e], -qb, qb, false, rq, rqe);
+        }
+        l2[i] = tc ? l2[i] : 0;
+      }
+      pk[j] = __builtin_amdgcn_perm((uint32_t)l2[1], (uint32_t)l2[0], 0x05040100u);
+      ss = __builtin_amdgcn_sdot2(__builtin_bit_cast(s16x2, pk[j]), __builtin_bit_cast(s16x2, pk[j]), ss, false);
+      v[k_zz.inv[8 * k + 2 * j]] = l2[0];
+      v[k_zz.inv[8 * k + 2 * j + 1]] = l2[1];
+    }
+    put_levels(lds, lane, k, make_uint4(pk[0], pk[1], pk[2], pk[3]));
+    SCHED_FENCE();
+  }
+  // CBP (p64.c:887-908): block coded if Σ|l| > 1; none such -> the first
+  // block with a nonzero level; no nonzero level at all -> MC without
+  // coefficients (MTYPE 4 / 7), vector kept, CBP 0x3f
+  const int sh = 6 * (l / 6);
+  const uint32_t big = (uint32_t)(__ballot(ss > 1) >> sh) & 63u, any = (uint32_t)(__ballot(ss > 0) >> sh) & 63u;
+  int cbp = 0x3f;
+  bool repred = false;  // 2/3 -> 4 switches from the zero vector to the ME vector
+  if (mt_cbp(mt)) {
+    if (any == 0) {
+      repred = !mt_mf(mt);
+      mt = mt_filter(mt) ? 7 : 4;
+    } else {
+      const uint32_t sel = big ? big : (any & (0u - any));  // lane-bit b = block b
+      cbp = (int)(__builtin_bitreverse32(sel) >> 26);           // block b -> bit 5 - b
+    }
+  }
+  const bool ck = mt_tcoeff(mt) && ((cbp >> (5 - b)) & 1);
+  const int q2 = ck ? 2 * q : 0, qq = ck ? q - qe : 0;
+#pragma unroll
+  for (int e = 0; e < 64; e++) {
+    const int dv = dequantise<false, true>(v[e], false, q2, qq);
+    v[e] = (e == 0 && intra) ? v[0] * 8 : dv;
+  }
+  idct_block(v);  // all-zero levels give zero (uncoded blocks)
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+#pragma unroll
+    for (int c = 0; c < 8; c++) {
+      const uint32_t pd = c < 4 ? prow[k].x : prow[k].y;
+      v[8 * k + c] = clampi(v[8 * k + c] + (int)((pd >> (8 * (c & 3))) & 255), 0, 255);
+    }
+    prow[k] = pack8(v + 8 * k);  // now the reconstructed rows
+  }
+  // no levels at all in the MB: the reconstruction is the new prediction
+  // (late, so its registers do not overlap the block's)
+  if (repred) inter_pred(B, w, h, stride, pos, mt, mvx, mvy, prow);
+  const uint32_t nvalid = min((unsigned)MBS_PER_WAVE, nmbs - gmb0);
+  flush_levels_run(lds, lane, gmb0 * 768u, nvalid * 768u, reinterpret_cast<uint8_t *>(a.coef));
+  const int pw = pos.plane ? w >> 1 : w;
+  const uint32_t ro = (uint32_t)((int64_t)pos.fi * stride) + (uint32_t)plane_offset(pos.plane, w, h) +
+                      (uint32_t)mul24(pos.y, pw) + (uint32_t)pos.x;
+#pragma unroll
+  for (int k = 0; k < 8; k++) st_out(reinterpret_cast<uint2 *>(a.recon + ro + (uint32_t)mul24(k, pw)), prow[k]);
+  if (b == 0 && lane < 6 * MBS_PER_WAVE && gmb0 + (unsigned)(l / 6) < nmbs) {
+    p64_mb_rec r;  // p64.c:909-910
+    r.mtype = (int8_t)mt;
+    r.cbp = (int8_t)cbp;
+    r.mvx = (int8_t)(mt_mf(mt) ? mvx : 0);
+    r.mvy = (int8_t)(mt_mf(mt) ? mvy : 0);
+    a.mb[gmb] = r;
+    a.last_intra[gmb] = mt_intra(mt) ? 0 : (uint8_t)(li + 1);
+  }
 }
 
 // batched 8x8 block operations (one thread per block; shares the device
@@ -2491,6 +2693,46 @@ bool mb_layout_forced() {
   }();
   return forced;
 }
+// P64GPU_FUSED=1: inter pictures through the fused one-wave-per-MB k_encode
+// instead of k_motion + k_inter_mbg (kept for A/B measurements and as the
+// path of mb-list encodes)
+bool fused_forced() {
+  static const bool on = [] {
+    const char *e = getenv("P64GPU_FUSED");
+    return e && *e && *e != '0';
+  }();
+  return on;
+}
+// device scratch for the ME records of the split inter encoder when the
+// caller does not ask for them (args.me == NULL): grown outside stream
+// capture only (NULL during a capture that would need a larger one: the
+// caller then takes the fused kernel), one per process and device
+static std::mutex g_me_mu;
+static p64_me_rec *g_me_buf = nullptr;
+static size_t g_me_cap = 0;
+static int g_me_dev = -1;
+static p64_me_rec *me_scratch(size_t n, hipStream_t st) {
+  std::lock_guard<std::mutex> lk(g_me_mu);
+  int dev = -1;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  if (g_me_buf && g_me_dev == dev && n <= g_me_cap) return g_me_buf;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
+  if (g_me_buf && g_me_dev != dev) return nullptr;  // first device keeps it
+  if (g_me_buf) {
+    if (hipDeviceSynchronize() != hipSuccess) return nullptr;  // in-flight users of the old one
+    (void)hipFree(g_me_buf);
+    g_me_buf = nullptr;
+    g_me_cap = 0;
+  }
+  void *p = nullptr;
+  if (hipMalloc(&p, n * sizeof(p64_me_rec)) != hipSuccess) return nullptr;
+  g_me_buf = static_cast<p64_me_rec *>(p);
+  g_me_cap = n;
+  g_me_dev = dev;
+  return g_me_buf;
+}
+
 // P64GPU_RECON_PERSISTENT=1: the persistent pipelined decoder k_recon_blk
 // instead of k_recon_mbg (kept for A/B measurements)
 bool recon_persistent() {
@@ -2699,7 +2941,47 @@ static int encode_launch(const p64gpu_encode_args *a, const int32_t *mb_list, in
       HIP_TRY(hipGetLastError());
     }
     return P64GPU_OK;
-  } else if (a->intra)
+  } else if (!a->intra && !mb_list && blocks < (1LL << 30) && !mb_layout_forced() && !fused_forced()) {
+    // split encoder: ME for the whole batch, then the block-layout rest
+    const int nmb = (a->width / 16) * (a->height / 16);
+    p64_me_rec *me = a->me ? a->me : me_scratch((size_t)a->nframes * nmb, st);
+    if (me) {
+      const int mode = a->me_mode == P64GPU_ME_FULL ? 2 : 1;
+      if (mode == 2)
+        hipLaunchKernelGGL(k_motion<2>, dim3(grid), dim3(64), 0, st, a->width, a->height, a->frame_stride,
+                           a->ref, a->cur, a->search_limit, me, kd);
+      else
+        hipLaunchKernelGGL(k_motion<1>, dim3(grid), dim3(64), 0, st, a->width, a->height, a->frame_stride,
+                           a->ref, a->cur, a->search_limit, me, kd);
+      HIP_TRY(hipGetLastError());
+      const int64_t per = (int64_t)nmb * 768 > a->frame_stride ? (int64_t)nmb * 768 : a->frame_stride;
+      const int chunk = (int)((((int64_t)1 << 31) - 1) / per);
+      for (int f0 = 0; f0 < a->nframes; f0 += chunk) {
+        p64gpu_encode_args c = *a;
+        c.nframes = a->nframes - f0 < chunk ? a->nframes - f0 : chunk;
+        const size_t m0 = (size_t)f0 * nmb;
+        c.cur = a->cur + (size_t)f0 * a->frame_stride;
+        c.ref = a->ref + (size_t)f0 * a->frame_stride;
+        c.recon = a->recon + (size_t)f0 * a->frame_stride;
+        c.last_intra = a->last_intra + m0;
+        c.quant_mb = a->quant_mb ? a->quant_mb + m0 : nullptr;
+        c.mtype_override = a->mtype_override ? a->mtype_override + m0 : nullptr;
+        c.coef = a->coef + m0 * 384;
+        c.mb = a->mb + m0;
+        c.me = nullptr;
+        const int64_t nm = (int64_t)c.nframes * nmb, waves = (nm + MBS_PER_WAVE - 1) / MBS_PER_WAVE;
+        if (c.quant_mb)
+          hipLaunchKernelGGL(k_inter_mbg<true>, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, st, c,
+                             blk_div(a->width, a->height), (unsigned)nm, me + m0);
+        else
+          hipLaunchKernelGGL(k_inter_mbg<false>, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, st, c,
+                             blk_div(a->width, a->height), (unsigned)nm, me + m0);
+        HIP_TRY(hipGetLastError());
+      }
+      return P64GPU_OK;
+    }
+  }
+  if (a->intra)
     hipLaunchKernelGGL(k_encode<0>, dim3(grid), dim3(64), 0, st, *a, mb_list, kd);
   else if (a->me_mode == P64GPU_ME_FULL)
     hipLaunchKernelGGL(k_encode<2>, dim3(grid), dim3(64), 0, st, *a, mb_list, kd);
