@@ -2443,6 +2443,9 @@ __global__ __launch_bounds__(256) INTER_OCC void k_inter_mbg(p64gpu_encode_args 
   const float rq = __builtin_bit_cast(float, __builtin_bit_cast(uint32_t, 1.0f / (float)(2 * q)) + 1u);
   const float rqe = (q & 1) ? 0.0f : rq;
   const int qe = (int)!(q & 1), qbr = 256 * q - 1 - qe, qb = min(1023, qbr);
+  // levels & tcm: 0 when the MB type carries no coefficients (through an
+  // opaque mask: as a select hipcc branches around every quantisation)
+  const int tcm = opaque(tc ? -1 : 0);
   int v[64];
   fdct_block_pk<true>(f.rows, v, prow);
   // quantise in scan order into the LDS staging (levels of a block whose MB
@@ -2469,7 +2472,7 @@ __global__ __launch_bounds__(256) INTER_OCC void k_inter_mbg(p64gpu_encode_args 
         } else {
           l2[i] = quantise<false, true>(v[e], -qb, qb, false, rq, rqe);
         }
-        l2[i] = tc ? l2[i] : 0;
+        l2[i] &= tcm;
       }
       pk[j] = __builtin_amdgcn_perm((uint32_t)l2[1], (uint32_t)l2[0], 0x05040100u);
       ss = __builtin_amdgcn_sdot2(__builtin_bit_cast(s16x2, pk[j]), __builtin_bit_cast(s16x2, pk[j]), ss, false);
