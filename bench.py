@@ -576,7 +576,26 @@ def main(argv=None):
         key = f"{w}x{h}_{args.mode}{args.search_limit}_q{args.quant}_S{S}" + \
             ("" if args.content == "synth" else f"_{args.content}")
         pmc = load_pmc(args.pmc_json, key)
-        kernel = "k_encode<%d>" % (2 if args.mode == "full" else 1)
+        kme, kin = "k_motion<%d>" % (2 if args.mode == "full" else 1), "k_inter_mbg<false>"
+        pmc_me, pmc_in = load_pmc(args.pmc_json, key + "_me"), load_pmc(args.pmc_json, key + "_inter")
+        if os.environ.get("P64GPU_FUSED", "0") in ("", "0"):  # split: k_motion, k_inter_mbg
+            kernel = f"{kme} + {kin} (one step)"
+            prof = os.path.join(REPO, "profiles", "r02_kernel_stats.csv")
+            split = {"dominant": kme,
+                     "dominant_note": "k_motion is VALU-bound (roofline_sad, valu_busy); the HBM "
+                                      "roofline is taken over the whole step, both kernels",
+                     "kernels_us_rocprof": rocprof_avg_us(prof, (kme, kin)) if key.endswith(
+                         "S256") else None,
+                     "kernels_us_source": "profiles/r02_kernel_stats.csv (rocprofv3 --kernel-trace "
+                                          "--stats of this default bench command)"}
+            pmc = None  # (an entry under `key` would be the fused kernel's)
+            if pmc_me and pmc_in:
+                pmc = {"hbm_bytes_per_launch": pmc_me["hbm_bytes_per_launch"] +
+                       pmc_in["hbm_bytes_per_launch"],
+                       "valu_busy": {kme: pmc_me.get("valu_busy"), kin: pmc_in.get("valu_busy")}}
+        else:
+            kernel = "k_encode<%d>" % (2 if args.mode == "full" else 1)
+            split = {}
         result = {
             "metric": METRICS[args.config], "value": round(value, 1),
             "ms_per_step": round(tmax / args.steps * 1e3, 4),
@@ -590,7 +609,8 @@ def main(argv=None):
                                        f"dp{world} (rank 0 RCCL-scatters pictures, gathers levels "
                                        f"+ records; roofline times the encode launch alone)")},
             "roofline": roofline(mbs_launch * BYTES_PER_MB, kavg, kernel, pmc,
-                                 algorithmic_bytes_per_mb=BYTES_PER_MB, timing=timing_note(args, root)),
+                                 algorithmic_bytes_per_mb=BYTES_PER_MB, timing=timing_note(args, root),
+                                 **split),
             "roofline_sad": {"bound": "valu", "achieved": round(sad_rate / 1e12, 3),
                              "peak": round(SAD_PEAK / 1e12, 3), "unit": "T byte-absdiff/s",
                              "frac": round(sad_rate / SAD_PEAK, 4), "candidates_per_mb": cand,
@@ -635,6 +655,22 @@ def main(argv=None):
 def strip(r):
     """A nested config line: everything but the top-level contract keys."""
     return {k: v for k, v in r.items() if k not in ("with_vlc",)}
+
+
+def rocprof_avg_us(path, names):
+    """Average launch duration (us) of the named kernels in a committed
+    rocprofv3 --kernel-trace --stats summary (profiles/), or None."""
+    try:
+        import csv
+        out = {}
+        with open(path) as f:
+            for r in csv.DictReader(f):
+                n = r["Name"].replace("(anonymous namespace)::", "").replace("void ", "").split("(")[0]
+                if n in names:
+                    out[n] = round(float(r["AverageNs"]) / 1e3, 2)
+        return out if len(out) == len(names) else None
+    except (OSError, KeyError, ValueError):
+        return None
 
 
 def measure_vlc(args, torch, p64_amd, step, out_of, S, nmb, w, h):
@@ -708,7 +744,7 @@ def run_intra(args, torch, dist, np, p64_amd, world, frames, S, nmb, pic, nslots
             "config": {"workload": f"{w}x{h} intra pictures, q={args.quant}, content {args.content}, "
                                    f"{S} pictures/step/GPU", "macroblocks_per_step_per_gpu": mbs,
                        "distinct_input_pictures": nslots},
-            "roofline": roofline(mbs * INTRA_BYTES_PER_MB, kavg, "k_intra_blk",
+            "roofline": roofline(mbs * INTRA_BYTES_PER_MB, kavg, "k_intra_mbg<false>",
                                  load_pmc(args.pmc_json, key),
                                  algorithmic_bytes_per_mb=INTRA_BYTES_PER_MB, timing=timing_note(args)),
             "verified_vs_oracle": verified}
@@ -771,7 +807,7 @@ def run_decode(args, torch, dist, np, p64_amd, world, enc, S, nmb, pic):
                                    f"(FULL SL={args.search_limit}, q={args.quant}, content "
                                    f"{args.content}), {S} sequences/GPU, closed loop",
                        "macroblocks_per_step_per_gpu": mbs},
-            "roofline": roofline(bpl, kavg, "k_recon_blk", load_pmc(args.pmc_json, key),
+            "roofline": roofline(bpl, kavg, "k_recon_mbg", load_pmc(args.pmc_json, key),
                                  algorithmic_bytes_per_mb=round(bpl / mbs, 1), timing=timing_note(args)),
             "verified_vs_encoder": {"ok": ok, "note": "last decoded picture == encoder "
                                                       "reconstruction, all sequences"}}

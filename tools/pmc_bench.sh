@@ -1,7 +1,7 @@
 #!/bin/bash
 # PMC evidence for bench.py's roofline.traffic and valu_busy (GPU box):
 # one rocprofv3 --pmc pass per counter group (never with tracing), over the
-# default workload (k_encode<2>, k_intra_mbg, k_recon_blk on synth content)
+# default workload (k_motion<2>, k_inter_mbg, k_intra_mbg, k_recon_mbg on synth content)
 # and the stress contents, plus a calibration pass over tools/ubench_valu
 # (kernels of known VALU issue rate).  tools/pmc_merge.py turns the output
 # into profiles/pmc_traffic.json entries.
