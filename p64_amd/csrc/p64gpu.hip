@@ -2265,6 +2265,51 @@ __global__ __launch_bounds__(256) BLK_OCC void k_recon_blk(int w, int h, int64_t
   }
 }
 
+// pred_rows (below) + dequantise + ChenIDct + reconstruction for the
+// non-persistent decoder: the prediction is formed first and kept as 8 packed
+// rows (16 registers instead of the 24-dword source), the dequantisation and
+// IDCT run unconditionally (an uncoded block's levels were read as zeros and
+// give a zero residual), so the register peak is the IDCT's
+__device__ __forceinline__ void pred_rows(const PredSrc &P, bool filter, uint2 prow[8]);
+__device__ __forceinline__ void rec_block_pk(int w, int h, int64_t stride, __amdgpu_buffer_rsrc_t rec,
+                                             const RecStageA &A, const RecStageB &S) {
+  const BlkPos &p = A.p;
+  uint2 prow[8];
+  pred_rows(S.pred, S.filter && S.inter, prow);  // zeros for intra (source not loaded)
+  int v[64];
+  const int q = A.q;
+  const uint32_t q2 = 0x20002u * (uint32_t)q, qq = 0x10001u * (uint32_t)(q - (int)!(q & 1));
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      const uint32_t d = dequantise_pk(S.lq[k][j], q2, qq);
+#pragma unroll
+      for (int i = 0; i < 2; i++) v[k_zz.inv[8 * k + 2 * j + i]] = i ? (int)d >> 16 : (int)(int16_t)(d & 0xffff);
+    }
+  }
+  if (!S.inter) v[0] = (int)(int16_t)(S.lq[0][0] & 0xffff) * 8;  // intra DC
+  idct_block(v);
+  PRIO_ST();
+  const int pw = p.plane ? w >> 1 : w;
+  const uint32_t ro = A.coded ? (uint32_t)((int64_t)p.fi * stride) + (uint32_t)plane_offset(p.plane, w, h) +
+                                    (uint32_t)(mul24(p.y, pw) + p.x)
+                              : BUF_OOB;
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+#pragma unroll
+    for (int c = 0; c < 8; c++) {
+      const uint32_t pd = c < 4 ? prow[k].x : prow[k].y;
+      v[8 * k + c] = clampi(v[8 * k + c] + (int)((pd >> (8 * (c & 3))) & 255), 0, 255);  // BoundIDctMatrix
+    }
+    const uint2 r = pack8(v + 8 * k);
+    typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+    u32x2 d;
+    d[0] = r.x;
+    d[1] = r.y;
+    __builtin_amdgcn_raw_buffer_store_b64(d, rec, ro + (uint32_t)mul24(k, pw), 0, 0);
+  }
+}
 #ifndef INTER_WAVES
 #define INTER_WAVES 3
 #endif
@@ -2291,6 +2336,16 @@ __global__ __launch_bounds__(256) RECON_OCC void k_recon_mbg(int w, int h, int64
   const int lane = threadIdx.x & 63;
   const unsigned gmb0 = (blockIdx.x * 4u + (threadIdx.x >> 6)) * MBS_PER_WAVE;
   if (gmb0 >= nmbs) return;  // whole wave
+#if defined(RECON_STAGGER)  // experiment: de-phase the first round of workgroups
+  if (blockIdx.x < 768u) {
+    const unsigned k = blockIdx.x >> 8;
+    if (k == 1) __builtin_amdgcn_s_sleep(RECON_STAGGER);
+    if (k == 2) {
+      __builtin_amdgcn_s_sleep(RECON_STAGGER);
+      __builtin_amdgcn_s_sleep(RECON_STAGGER);
+    }
+  }
+#endif
   const int nmb = (w >> 4) * (h >> 4), nfr = (int)(nmbs / (unsigned)nmb);
   RecBufs B;
   B.ref = __builtin_amdgcn_make_buffer_rsrc((void *)refp, (short)0, (int)(nfr * stride), BUF_RSRC_W3);
@@ -2340,7 +2395,7 @@ __global__ __launch_bounds__(256) RECON_OCC void k_recon_mbg(int w, int h, int64
     S.lq[k][3] = v.w;
   }
 #endif
-  rec_block(w, h, stride, rec, A, S);
+  rec_block_pk(w, h, stride, rec, A, S);
 }
 
 // ---------------------------------------------------------------------------
@@ -2354,6 +2409,7 @@ __global__ __launch_bounds__(256) RECON_OCC void k_recon_mbg(int w, int h, int64
 // reconstruction.  The fused one-wave-per-MB k_encode spends 40% of its time
 // in this half with 48 of 64 lanes busy on LDS-exchanged row passes; here
 // every lane holds its block in registers.
+__device__ __forceinline__ void pred_rows(const PredSrc &P, bool filter, uint2 prow[8]);
 struct InterMe {  // the fields of p64_me_rec the decision needs
   int mx, my, sad, sad0, var, varor;
 };
@@ -2366,8 +2422,11 @@ __device__ __forceinline__ void inter_pred(const RecBufs &B, int w, int h, int64
   A.q = 0;
   A.coded = 1;
   const RecStageB S = rec_stage_b<false>(B, w, h, stride, A);  // source OOB (zeros) if intra
-  const PredSrc &P = S.pred;
-  if (S.filter) {  // add_pred's loop filter, one packed row at a time
+  pred_rows(S.pred, S.filter, prow);
+}
+// the prediction as packed rows (all zero when the source was not loaded)
+__device__ __forceinline__ void pred_rows(const PredSrc &P, bool filter, uint2 prow[8]) {
+  if (filter) {  // add_pred's loop filter, one packed row at a time
     int hp[8], hc[8], hn[8];
     hz_row(P, 0, hc);
     hz_row(P, 1, hn);
