@@ -1721,6 +1721,26 @@ __device__ __forceinline__ void fdct_block_pk(const uint2 rows[8], int v[64], co
   }
 }
 
+// 8 IDCT row outputs o (before the final rounding) -> BoundIDct(idct_final(o))
+// as 8 packed bytes.  For o < 0 idct_final(o) <= 0 and (o + 8) >> 4 <= 0 alike,
+// so after the clamp to 0..255 the final rounding's sign term drops out:
+// clamp((o + 8) >> 4).  The clamp + pack is v_cvt_pk_i16_i32 (saturating) +
+// v_sat_pk_u8_i16 per pair and one v_perm per 4 pixels (inline asm: hipcc's
+// own clamp+pack fusion is the miscompiled v_ashr_pk_u8_i32 form, see pack8).
+__device__ __forceinline__ uint32_t sat4(const int x[4]) {
+  uint32_t p01, p23, s01, s23;
+  asm("v_cvt_pk_i16_i32 %0, %1, %2" : "=v"(p01) : "v"(x[0]), "v"(x[1]));
+  asm("v_cvt_pk_i16_i32 %0, %1, %2" : "=v"(p23) : "v"(x[2]), "v"(x[3]));
+  asm("v_sat_pk_u8_i16 %0, %1" : "=v"(s01) : "v"(p01));
+  asm("v_sat_pk_u8_i16 %0, %1" : "=v"(s23) : "v"(p23));
+  return __builtin_amdgcn_perm(s23, s01, 0x05040100u);
+}
+__device__ __forceinline__ uint2 final_clamp_pack8(const int o[8]) {
+  int x[8];
+#pragma unroll
+  for (int k = 0; k < 8; k++) x[k] = (o[k] + 8) >> 4;
+  return make_uint2(sat4(x), sat4(x + 4));
+}
 // ChenIDct (chendct.c:217-375) on a register block: column pass (inputs <<2,
 // folded into the constants), row pass, final rounding
 __device__ __forceinline__ void idct_block(int v[64]) {
@@ -1740,6 +1760,27 @@ __device__ __forceinline__ void idct_block(int v[64]) {
     inv8<true>(v + 8 * r, o);
 #pragma unroll
     for (int k = 0; k < 8; k++) v[8 * r + k] = idct_final(o[k]);
+    SCHED_FENCE();
+  }
+}
+// the same ChenIDct followed by BoundIDctMatrix with nothing added (intra
+// blocks of an intra picture): packed reconstructed rows
+__device__ __forceinline__ void idct_block_rec(int v[64], uint2 rec[8]) {
+#pragma unroll
+  for (int c = 0; c < 8; c++) {
+    int x[8], o[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) x[k] = v[8 * k + c];
+    inv8<true, 4>(x, o);
+#pragma unroll
+    for (int k = 0; k < 8; k++) v[8 * k + c] = o[k];
+    SCHED_FENCE();
+  }
+#pragma unroll
+  for (int r = 0; r < 8; r++) {
+    int o[8];
+    inv8<true>(v + 8 * r, o);
+    rec[r] = final_clamp_pack8(o);
     SCHED_FENCE();
   }
 }
@@ -1818,10 +1859,17 @@ __device__ __forceinline__ IntraFetch intra_fetch_at(const p64gpu_encode_args &a
   IntraFetch f;
   f.p = pos;
   const int pw = f.p.plane ? w >> 1 : w;
-  const uint8_t *src = a.cur + (size_t)f.p.fi * a.frame_stride +
-                       (uint32_t)(plane_offset(f.p.plane, w, h) + mul24(f.p.y, pw) + f.p.x);
+  // buffer loads: 32-bit offsets (a launch covers < 2 GiB of pictures), no
+  // 64-bit address arithmetic per row
+  const __amdgpu_buffer_rsrc_t cur = __builtin_amdgcn_make_buffer_rsrc(
+      (void *)a.cur, (short)0, (int)((int64_t)a.nframes * a.frame_stride), BUF_RSRC_W3);
+  const uint32_t o = (uint32_t)((int64_t)f.p.fi * a.frame_stride) +
+                     (uint32_t)(plane_offset(f.p.plane, w, h) + mul24(f.p.y, pw) + f.p.x);
 #pragma unroll
-  for (int k = 0; k < 8; k++) f.rows[k] = *reinterpret_cast<const uint2 *>(src + (uint32_t)mul24(k, pw));
+  for (int k = 0; k < 8; k++) {
+    const auto v = __builtin_amdgcn_raw_buffer_load_b64(cur, o + (uint32_t)mul24(k, pw), 0, 0);
+    f.rows[k] = make_uint2(v[0], v[1]);
+  }
 #if defined(PROBE_NOLOAD)
   for (int k = 0; k < 8; k++) f.rows[k] = make_uint2(pos.x * 0x01010101u + k, pos.y * 0x03050709u ^ pos.fi);
 #endif
@@ -1902,11 +1950,7 @@ __device__ __forceinline__ void intra_block(const p64gpu_encode_args &a, const I
     put_levels(lds, lane, k, make_uint4(pk[0], pk[1], pk[2], pk[3]));
     SCHED_FENCE();
   }
-  idct_block(v);
-#pragma unroll
-  for (int e = 0; e < 64; e++) v[e] = clampi(v[e], 0, 255);  // BoundIDctMatrix
-#pragma unroll
-  for (int k = 0; k < 8; k++) out.rec[k] = pack8(v + 8 * k);
+  idct_block_rec(v, out.rec);  // + BoundIDctMatrix
   out.pw = p.plane ? w >> 1 : w;
   out.rec_off = (uint32_t)((int64_t)p.fi * a.frame_stride) + (uint32_t)plane_offset(p.plane, w, h) +
                 (uint32_t)mul24(p.y, out.pw) + (uint32_t)p.x;
@@ -2311,7 +2355,7 @@ __device__ __forceinline__ void rec_block_pk(int w, int h, int64_t stride, __amd
   }
 }
 #ifndef INTER_WAVES
-#define INTER_WAVES 3
+#define INTER_WAVES 4
 #endif
 #define INTER_OCC __attribute__((amdgpu_waves_per_eu(INTER_WAVES)))
 #ifndef RECON_WAVES
