@@ -1844,8 +1844,31 @@ __device__ __forceinline__ void flush_levels_run(const uint8_t *lds, int lane, u
   __builtin_amdgcn_wave_barrier();
 }
 
+// Half staging (k_intra_mbg): scan positions 0..31 of every lane, flushed,
+// then 32..63 -- 80 bytes per lane (64 + 16 pad, conflict-free for
+// ds_write_b128 at 16 lanes per cycle: starting banks 20·lane mod 64 are
+// distinct), 5 KB per wave, which lets 5 waves per SIMD fit the LDS.  A half
+// is 64 bytes of each block's 128: the run flush writes them as 16-byte
+// pieces (4 per block), consecutive lanes consecutive pieces.
+constexpr int LVLH_STRIDE = 80;
+constexpr int LVLH_WAVE = 64 * LVLH_STRIDE;
+__device__ __forceinline__ void flush_levels_half(const uint8_t *lds, int lane, uint32_t off, uint32_t nblk,
+                                                  int half, uint8_t *coef) {
+  __builtin_amdgcn_wave_barrier();
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    const uint32_t pc = 64u * i + (uint32_t)lane, blk = pc >> 2, sub = pc & 3;
+    if (blk < nblk) {
+      const uint4 v = *reinterpret_cast<const uint4 *>(lds + blk * LVLH_STRIDE + sub * 16);
+      st_out(reinterpret_cast<uint4 *>(coef + off + blk * 128 + half * 64 + sub * 16), v);
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+}
+
 // dword 3 of a raw buffer resource on gfx9-family parts (CDNA): 32-bit data format
 constexpr int BUF_RSRC_W3 = 0x00020000;
+constexpr uint32_t BUF_OOB = 0x80000000u;  // >= every buffer's num_records: loads 0, stores dropped
 
 struct IntraFetch {
   BlkPos p;
@@ -1911,9 +1934,11 @@ __device__ __forceinline__ void intra_store(const p64gpu_encode_args &a, const I
 }
 // one block: ChenDct, [the previous block's stores], quantise + zigzag into
 // the LDS staging, dequantise, ChenIDct, reconstruction into `out`
-template <bool PENDING>
+// HALF: half staging (flush_levels_half) of a run of run_blk blocks at
+// coef + run_off, flushed from here
+template <bool PENDING, bool HALF = false>
 __device__ __forceinline__ void intra_block(const p64gpu_encode_args &a, const IntraFetch &f, uint8_t *lds,
-                                            int lane, IntraOut &out) {
+                                            int lane, IntraOut &out, uint32_t run_off = 0, uint32_t run_blk = 0) {
   const int w = a.width, h = a.height, nmb = (w >> 4) * (h >> 4);
   const BlkPos &p = f.p;
   const uint32_t gmb = (uint32_t)(p.fi * nmb + p.mb);
@@ -1947,7 +1972,12 @@ __device__ __forceinline__ void intra_block(const p64gpu_encode_args &a, const I
       }
       pk[j] = __builtin_amdgcn_perm((uint32_t)l2[1], (uint32_t)l2[0], 0x05040100u);
     }
-    put_levels(lds, lane, k, make_uint4(pk[0], pk[1], pk[2], pk[3]));
+    if (HALF) {
+      *reinterpret_cast<uint4 *>(lds + lane * LVLH_STRIDE + (k & 3) * 16) = make_uint4(pk[0], pk[1], pk[2], pk[3]);
+      if ((k & 3) == 3) flush_levels_half(lds, lane, run_off, run_blk, k >> 2, reinterpret_cast<uint8_t *>(a.coef));
+    } else {
+      put_levels(lds, lane, k, make_uint4(pk[0], pk[1], pk[2], pk[3]));
+    }
     SCHED_FENCE();
   }
   idct_block_rec(v, out.rec);  // + BoundIDctMatrix
@@ -1966,10 +1996,14 @@ __device__ __forceinline__ void intra_block(const p64gpu_encode_args &a, const I
 // intra picture, MB-grouped block layout (blk_pos_mb): one wave = 10 MBs, a
 // lane per block; levels leave as one contiguous 7,680-byte run per wave
 template <bool QMB>
+#ifndef INTRA_HALF
+#define INTRA_HALF 0
+#endif
 __global__ __launch_bounds__(256) BLK_OCC void k_intra_mbg(p64gpu_encode_args a, BlkDiv kd, unsigned nmbs) {
-  __shared__ __align__(16) uint8_t lvl[4 * LVL_WAVE];
+  constexpr int LW = INTRA_HALF ? LVLH_WAVE : LVL_WAVE;
+  __shared__ __align__(16) uint8_t lvl[4 * LW];
   const int lane = threadIdx.x & 63;
-  uint8_t *lds = lvl + (threadIdx.x >> 6) * LVL_WAVE;
+  uint8_t *lds = lvl + (threadIdx.x >> 6) * LW;
   const unsigned gmb0 = (blockIdx.x * 4u + (threadIdx.x >> 6)) * MBS_PER_WAVE;
   if (gmb0 >= nmbs) return;  // whole wave
   PRIO_HIGH();
@@ -1978,13 +2012,15 @@ __global__ __launch_bounds__(256) BLK_OCC void k_intra_mbg(p64gpu_encode_args a,
   const IntraFetch f = intra_fetch_at<QMB>(a, blk_pos_mb(gmb, l % 6, a.width, a.height, kd));
   PRIO_LOW();
   IntraOut o;
-  intra_block<false>(a, f, lds, lane, o);
   const uint32_t nvalid = min((unsigned)MBS_PER_WAVE, nmbs - gmb0);
+  intra_block<false, (bool)INTRA_HALF>(a, f, lds, lane, o, gmb0 * 768u, 6 * nvalid);
   PRIO_ST();
+#if !INTRA_HALF
 #if defined(PROBE_NOCOEF)  // development probes: drop one output stream (the work stays)
   if (o.rec[0].x == 0x12345678u)
 #endif
   flush_levels_run(lds, lane, gmb0 * 768u, nvalid * 768u, reinterpret_cast<uint8_t *>(a.coef));
+#endif
 #if defined(PROBE_NOREC)
   if (o.rec[0].x == 0x12345678u)
 #endif
@@ -2149,7 +2185,6 @@ __device__ __forceinline__ void add_pred(const PredSrc &p, bool filter, int v[64
 // corrupt one cannot make the kernel read outside the picture.
 // One launch covers at most 2 GiB of levels and of pictures (the host splits
 // larger batches), so every offset fits the 32-bit buffer range.
-constexpr uint32_t BUF_OOB = 0x80000000u;  // >= every buffer's num_records
 
 struct RecBufs {
   __amdgpu_buffer_rsrc_t ref, coef, mb, q, mask;
