@@ -1204,8 +1204,8 @@ __device__ __forceinline__ uint32_t dequantise_pk(uint32_t l, uint32_t q2, uint3
   uint32_t sg, m, r;
   asm("v_pk_min_i16 %0, %1, %2" : "=v"(sg) : "v"(l), "s"(0x00010001u));
   asm("v_pk_max_i16 %0, %1, %2" : "=v"(sg) : "v"(sg), "s"(0xffffffffu));
-  asm("v_pk_mul_lo_u16 %0, %1, %2" : "=v"(m) : "v"(l), "s"(q2));
-  asm("v_pk_mad_i16 %0, %1, %2, %3" : "=v"(r) : "v"(sg), "s"(qq), "v"(m));
+  asm("v_pk_mul_lo_u16 %0, %1, %2" : "=v"(m) : "v"(l), "v"(q2));  // q2, qq per lane (per MB)
+  asm("v_pk_mad_i16 %0, %1, %2, %3" : "=v"(r) : "v"(sg), "v"(qq), "v"(m));
   return r;
 }
 
@@ -1763,6 +1763,70 @@ __device__ __forceinline__ void idct_block(int v[64]) {
     SCHED_FENCE();
   }
 }
+// ICCITTFlatQuantize + ChenIDct + BoundIDctMatrix of an intra block from its
+// levels (natural order in v; the DC dequantised as DC x 8): the dequantiser
+// runs on natural level pairs (x_k, x_k') of a column in packed 16-bit
+// arithmetic (dequantise_pk; |value| <= 7,905) and the column pass takes
+// every product pair C_a x_k + C_b x_k' as one v_dot2_i32_i16 on those pairs
+// (the <<2 input scale folded into the constants, <= 2,008: products and sums
+// exact in 32 bits); row pass and final stage as idct_block_rec
+__device__ __forceinline__ uint32_t pk2(int lo, int hi) { return __builtin_amdgcn_perm((uint32_t)hi, (uint32_t)lo, 0x05040100u); }
+// the column pass of that from natural level pairs: pair(e, e') returns the
+// levels of natural positions e (low half) and e' (high half) packed; q2/qq
+// packed per lane (0 for a block without coefficients); dcfix: the DC is
+// the intra DC (dequantised as dc8 = DC x 8)
+template <class PairFn>
+__device__ __forceinline__ void iq_idct_cols(PairFn pair, uint32_t q2, uint32_t qq, bool dcfix, int dc8,
+                                             int v[64]) {
+#pragma unroll
+  for (int c = 0; c < 8; c++) {
+    uint32_t p04 = dequantise_pk(pair(c, 32 + c), q2, qq);
+    if (c == 0) p04 = dcfix ? __builtin_amdgcn_perm(p04, (uint32_t)dc8, 0x07060100u) : p04;  // (DC x 8, x4)
+    const s16x2 a04 = __builtin_bit_cast(s16x2, p04);
+    const s16x2 a17 = __builtin_bit_cast(s16x2, dequantise_pk(pair(8 + c, 56 + c), q2, qq));
+    const s16x2 a53 = __builtin_bit_cast(s16x2, dequantise_pk(pair(40 + c, 24 + c), q2, qq));
+    const s16x2 a26 = __builtin_bit_cast(s16x2, dequantise_pk(pair(16 + c, 48 + c), q2, qq));
+    const int p0 = ms9(dot2(a17, 4 * C7D16, -4 * C1D16)), p3 = ms9(dot2(a17, 4 * C1D16, 4 * C7D16));
+    const int p1 = ms9(dot2(a53, 4 * C3D16, -4 * C5D16)), p2 = ms9(dot2(a53, 4 * C5D16, 4 * C3D16));
+    const int q0 = ms9(dot2(a04, 4 * C1D4, 4 * C1D4)), q1 = ms9(dot2(a04, 4 * C1D4, -4 * C1D4));
+    const int q2_ = ms9(dot2(a26, 4 * C3D8, -4 * C1D8)), q3 = ms9(dot2(a26, 4 * C1D8, 4 * C3D8));
+    const int e0 = q0 + q3, e1 = q1 + q2_, e2 = q1 - q2_, e3 = q0 - q3;
+    const int f0 = p0 + p1, f1 = p0 - p1, f2 = p3 - p2, f3 = p3 + p2;
+    const int g1 = ms9(kmul<true>(C1D4, f2 - f1)), g2 = ms9(kmul<true>(C1D4, f2 + f1));
+    v[c] = e0 + f3;
+    v[8 + c] = e1 + g2;
+    v[16 + c] = e2 + g1;
+    v[24 + c] = e3 + f0;
+    v[32 + c] = e3 - f0;
+    v[40 + c] = e2 - g1;
+    v[48 + c] = e1 - g2;
+    v[56 + c] = e0 - f3;
+    SCHED_FENCE();
+  }
+}
+// row pass + idct_final (the residual, to be added to a prediction)
+__device__ __forceinline__ void idct_rows(int v[64]) {
+#pragma unroll
+  for (int r = 0; r < 8; r++) {
+    int o[8];
+    inv8<true>(v + 8 * r, o);
+#pragma unroll
+    for (int k = 0; k < 8; k++) v[8 * r + k] = idct_final(o[k]);
+    SCHED_FENCE();
+  }
+}
+// levels (ints, natural order) in v -> reconstructed rows of an intra block
+__device__ __forceinline__ void iq_idct_intra_rec(int v[64], int q, uint2 rec[8]) {
+  const uint32_t q2 = 0x20002u * (uint32_t)q, qq = 0x10001u * (uint32_t)(q - (int)!(q & 1));
+  iq_idct_cols([&](int e, int f) { return pk2(v[e], v[f]); }, q2, qq, true, v[0] * 8, v);
+#pragma unroll
+  for (int r = 0; r < 8; r++) {
+    int o[8];
+    inv8<true>(v + 8 * r, o);
+    rec[r] = final_clamp_pack8(o);
+    SCHED_FENCE();
+  }
+}
 // the same ChenIDct followed by BoundIDctMatrix with nothing added (intra
 // blocks of an intra picture): packed reconstructed rows
 __device__ __forceinline__ void idct_block_rec(int v[64], uint2 rec[8]) {
@@ -1946,7 +2010,10 @@ __device__ __forceinline__ void intra_block(const p64gpu_encode_args &a, const I
   // c_qrecip.r[q] computed in place (no dependent table load in the loop)
   const float rq = __builtin_bit_cast(float, __builtin_bit_cast(uint32_t, 1.0f / (float)(2 * q)) + 1u);
   const float rqe = (q & 1) ? 0.0f : rq;
-  const int q2 = 2 * q, qq = q - (int)!(q & 1), qb = quant_bound(q);
+  const int qb = quant_bound(q);
+#if defined(INTRA_SCALAR_IQ)
+  const int q2 = 2 * q, qq = q - (int)!(q & 1);
+#endif
   int v[64];
 #if defined(BLK_SCALAR_FDCT)
   fdct_block(f.rows, v);
@@ -1968,7 +2035,11 @@ __device__ __forceinline__ void intra_block(const p64gpu_encode_args &a, const I
         const int e = k_zz.inv[8 * k + 2 * j + i];
         const bool dc = e == 0;
         l2[i] = quantise<true, true>(v[e], dc ? -0x7fffffff : -qb, dc ? 2047 : qb, dc, rq, rqe);
+#if defined(INTRA_SCALAR_IQ)
         v[e] = dequantise<true, true>(l2[i], dc, q2, qq);
+#else
+        v[e] = l2[i];  // dequantised in pairs by iq_idct_intra_rec
+#endif
       }
       pk[j] = __builtin_amdgcn_perm((uint32_t)l2[1], (uint32_t)l2[0], 0x05040100u);
     }
@@ -1980,7 +2051,11 @@ __device__ __forceinline__ void intra_block(const p64gpu_encode_args &a, const I
     }
     SCHED_FENCE();
   }
+#if defined(INTRA_SCALAR_IQ)
   idct_block_rec(v, out.rec);  // + BoundIDctMatrix
+#else
+  iq_idct_intra_rec(v, q, out.rec);
+#endif
   out.pw = p.plane ? w >> 1 : w;
   out.rec_off = (uint32_t)((int64_t)p.fi * a.frame_stride) + (uint32_t)plane_offset(p.plane, w, h) +
                 (uint32_t)mul24(p.y, out.pw) + (uint32_t)p.x;
@@ -2015,27 +2090,57 @@ __global__ __launch_bounds__(256) BLK_OCC void k_intra_mbg(p64gpu_encode_args a,
   const uint32_t nvalid = min((unsigned)MBS_PER_WAVE, nmbs - gmb0);
   intra_block<false, (bool)INTRA_HALF>(a, f, lds, lane, o, gmb0 * 768u, 6 * nvalid);
   PRIO_ST();
+  // buffer stores throughout (32-bit offsets, out of range instead of a
+  // branch for the tail of the levels run and for the record lanes)
+  const int nfr = (int)(nmbs / (unsigned)((a.width >> 4) * (a.height >> 4)));
 #if !INTRA_HALF
-#if defined(PROBE_NOCOEF)  // development probes: drop one output stream (the work stays)
-  if (o.rec[0].x == 0x12345678u)
-#endif
-  flush_levels_run(lds, lane, gmb0 * 768u, nvalid * 768u, reinterpret_cast<uint8_t *>(a.coef));
-#endif
-#if defined(PROBE_NOREC)
-  if (o.rec[0].x == 0x12345678u)
-#endif
+  {
+    const __amdgpu_buffer_rsrc_t coef =
+        __builtin_amdgcn_make_buffer_rsrc((void *)a.coef, (short)0, (int)(nmbs * 768u), BUF_RSRC_W3);
+    const uint32_t nbytes = nvalid * 768u;
+    __builtin_amdgcn_wave_barrier();
 #pragma unroll
-  for (int k = 0; k < 8; k++)
-    st_out(reinterpret_cast<uint2 *>(a.recon + o.rec_off + (uint32_t)mul24(k, o.pw)), o.rec[k]);
-  if (l % 6 == 0 && lane < 6 * MBS_PER_WAVE && gmb0 + (unsigned)(l / 6) < nmbs) {
-    p64_mb_rec r;  // p64.c:909-910: MTYPE 0, CBP 0x3f, LastIntra reset
-    r.mtype = 0;
-    r.cbp = 0x3f;
-    r.mvx = 0;
-    r.mvy = 0;
-    a.mb[gmb] = r;
-    a.last_intra[gmb] = 0;
+    for (int k = 0; k < 8; k++) {
+      const uint32_t ob = 1024u * k + 16u * lane;
+      const uint4 v = *reinterpret_cast<const uint4 *>(lds + (ob >> 7) * LVL_STRIDE + (ob & 127));
+      typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+      u32x4 d;
+      d[0] = v.x;
+      d[1] = v.y;
+      d[2] = v.z;
+      d[3] = v.w;
+#if defined(PROBE_NOCOEF)  // development probes: drop one output stream (the work stays)
+      __builtin_amdgcn_raw_buffer_store_b128(d, coef, BUF_OOB, 0, 0);
+#else
+      __builtin_amdgcn_raw_buffer_store_b128(d, coef, ob < nbytes ? gmb0 * 768u + ob : BUF_OOB, 0, 0);
+#endif
+    }
+    __builtin_amdgcn_wave_barrier();
   }
+#endif
+  const __amdgpu_buffer_rsrc_t rec =
+      __builtin_amdgcn_make_buffer_rsrc((void *)a.recon, (short)0, (int)(nfr * a.frame_stride), BUF_RSRC_W3);
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+    u32x2 d;
+    d[0] = o.rec[k].x;
+    d[1] = o.rec[k].y;
+#if defined(PROBE_NOREC)
+    __builtin_amdgcn_raw_buffer_store_b64(d, rec, BUF_OOB, 0, 0);
+#else
+    __builtin_amdgcn_raw_buffer_store_b64(d, rec, o.rec_off + (uint32_t)mul24(k, o.pw), 0, 0);
+#endif
+  }
+  // the MB's record and LastIntra (p64.c:909-910: MTYPE 0, CBP 0x3f) from
+  // lane b = 0 of each MB
+  const bool rl = l % 6 == 0 && lane < 6 * MBS_PER_WAVE && gmb0 + (unsigned)(l / 6) < nmbs;
+  const __amdgpu_buffer_rsrc_t mbr =
+      __builtin_amdgcn_make_buffer_rsrc((void *)a.mb, (short)0, (int)(nmbs * 4u), BUF_RSRC_W3);
+  const __amdgpu_buffer_rsrc_t lir =
+      __builtin_amdgcn_make_buffer_rsrc((void *)a.last_intra, (short)0, (int)nmbs, BUF_RSRC_W3);
+  __builtin_amdgcn_raw_buffer_store_b32(0x3f00u, mbr, rl ? 4u * gmb : BUF_OOB, 0, 0);
+  __builtin_amdgcn_raw_buffer_store_b8((uint8_t)0, lir, rl ? gmb : BUF_OOB, 0, 0);
 }
 // one launch covers at most 2 GiB of pictures and of levels (the host splits
 // larger batches), so 32-bit offsets address both
@@ -2358,17 +2463,14 @@ __device__ __forceinline__ void rec_block_pk(int w, int h, int64_t stride, __amd
   int v[64];
   const int q = A.q;
   const uint32_t q2 = 0x20002u * (uint32_t)q, qq = 0x10001u * (uint32_t)(q - (int)!(q & 1));
-#pragma unroll
-  for (int k = 0; k < 8; k++) {
-#pragma unroll
-    for (int j = 0; j < 4; j++) {
-      const uint32_t d = dequantise_pk(S.lq[k][j], q2, qq);
-#pragma unroll
-      for (int i = 0; i < 2; i++) v[k_zz.inv[8 * k + 2 * j + i]] = i ? (int)d >> 16 : (int)(int16_t)(d & 0xffff);
-    }
-  }
-  if (!S.inter) v[0] = (int)(int16_t)(S.lq[0][0] & 0xffff) * 8;  // intra DC
-  idct_block(v);
+  // natural level pairs straight from the packed zigzag words (one v_perm each)
+  auto pair = [&](int e, int f) {
+    const int s1 = k_zz.pos[e], s2 = k_zz.pos[f];
+    const uint32_t sel = ((s1 & 1) ? 0x0302u : 0x0100u) | (((s2 & 1) ? 0x0706u : 0x0504u) << 16);
+    return __builtin_amdgcn_perm(S.lq[s2 >> 3][(s2 >> 1) & 3], S.lq[s1 >> 3][(s1 >> 1) & 3], sel);
+  };
+  iq_idct_cols(pair, q2, qq, !S.inter, (int)(int16_t)(S.lq[0][0] & 0xffff) * 8, v);
+  idct_rows(v);
   PRIO_ST();
   const int pw = p.plane ? w >> 1 : w;
   const uint32_t ro = A.coded ? (uint32_t)((int64_t)p.fi * stride) + (uint32_t)plane_offset(p.plane, w, h) +
@@ -2637,13 +2739,10 @@ __global__ __launch_bounds__(256) INTER_OCC void k_inter_mbg(p64gpu_encode_args 
     }
   }
   const bool ck = mt_tcoeff(mt) && ((cbp >> (5 - b)) & 1);
-  const int q2 = ck ? 2 * q : 0, qq = ck ? q - qe : 0;
-#pragma unroll
-  for (int e = 0; e < 64; e++) {
-    const int dv = dequantise<false, true>(v[e], false, q2, qq);
-    v[e] = (e == 0 && intra) ? v[0] * 8 : dv;
-  }
-  idct_block(v);  // all-zero levels give zero (uncoded blocks)
+  const uint32_t q2 = ck ? 0x20002u * (uint32_t)q : 0u, qq = ck ? 0x10001u * (uint32_t)(q - qe) : 0u;
+  // IQ in level pairs + ChenIDct (all-zero levels / q2 = qq = 0 give zero)
+  iq_idct_cols([&](int e, int f) { return pk2(v[e], v[f]); }, q2, qq, intra, v[0] * 8, v);
+  idct_rows(v);
 #pragma unroll
   for (int k = 0; k < 8; k++) {
 #pragma unroll
