@@ -1815,14 +1815,28 @@ __device__ __forceinline__ void idct_rows(int v[64]) {
     SCHED_FENCE();
   }
 }
-// levels (ints, natural order) in v -> reconstructed rows of an intra block
+// levels (ints, natural order) in v -> reconstructed rows of an intra block.
+// The row pass takes its product pairs by v_dot2 too: in an intra picture
+// the dequantised inputs are bounded by the quantiser (|AC| <= 1,023 + q <=
+// 1,054, DC <= 254 x 8 = 2,032), which bounds the column-pass outputs by
+// 25,062 (every sign pattern at those magnitudes) < 2^15; a decoder or an
+// inter residual may exceed that (up to 167,072), so only here.
 __device__ __forceinline__ void iq_idct_intra_rec(int v[64], int q, uint2 rec[8]) {
   const uint32_t q2 = 0x20002u * (uint32_t)q, qq = 0x10001u * (uint32_t)(q - (int)!(q & 1));
   iq_idct_cols([&](int e, int f) { return pk2(v[e], v[f]); }, q2, qq, true, v[0] * 8, v);
 #pragma unroll
   for (int r = 0; r < 8; r++) {
-    int o[8];
-    inv8<true>(v + 8 * r, o);
+    const int *x = v + 8 * r;
+    const s16x2 a04 = __builtin_bit_cast(s16x2, pk2(x[0], x[4])), a17 = __builtin_bit_cast(s16x2, pk2(x[1], x[7]));
+    const s16x2 a53 = __builtin_bit_cast(s16x2, pk2(x[5], x[3])), a26 = __builtin_bit_cast(s16x2, pk2(x[2], x[6]));
+    const int p0 = ms9(dot2(a17, C7D16, -C1D16)), p3 = ms9(dot2(a17, C1D16, C7D16));
+    const int p1 = ms9(dot2(a53, C3D16, -C5D16)), p2 = ms9(dot2(a53, C5D16, C3D16));
+    const int q0 = ms9(dot2(a04, C1D4, C1D4)), q1 = ms9(dot2(a04, C1D4, -C1D4));
+    const int q2_ = ms9(dot2(a26, C3D8, -C1D8)), q3 = ms9(dot2(a26, C1D8, C3D8));
+    const int e0 = q0 + q3, e1 = q1 + q2_, e2 = q1 - q2_, e3 = q0 - q3;
+    const int f0 = p0 + p1, f1 = p0 - p1, f2 = p3 - p2, f3 = p3 + p2;
+    const int g1 = ms9(kmul<true>(C1D4, f2 - f1)), g2 = ms9(kmul<true>(C1D4, f2 + f1));
+    const int o[8] = {e0 + f3, e1 + g2, e2 + g1, e3 + f0, e3 - f0, e2 - g1, e1 - g2, e0 - f3};
     rec[r] = final_clamp_pack8(o);
     SCHED_FENCE();
   }
