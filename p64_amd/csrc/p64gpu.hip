@@ -1431,12 +1431,15 @@ __global__ __launch_bounds__(64, ENCODE_WAVES_PER_SIMD) void k_motion(int w, int
   const int lane = threadIdx.x;
   const int mbw = w >> 4, nmb = mbw * (h >> 4);
   const unsigned gid = xcd_remap(blockIdx.x, gridDim.x);
+  TIMING_BEGIN(gid);
   const MbPos ps = mb_pos(gid, nmb, mbw, kd);
   const int fi = ps.fi, x0 = 16 * ps.mbx, y0 = 16 * ps.mby;
   put_luma(L, fetch_luma(ref_y + (size_t)fi * stride, cur_y + (size_t)fi * stride, w, h, x0, y0, lane),
            lane);
   __syncthreads();
+  SECTION("m_fetched");
   const MeOut me = motion_estimate<MODE>(L, cur_y + (size_t)fi * stride, w, h, x0, y0, sl, lane);
+  SECTION("m_me_done");
   if (lane == 0) {
     p64_me_rec o;
     o.mx = me.mx;
@@ -1448,6 +1451,7 @@ __global__ __launch_bounds__(64, ENCODE_WAVES_PER_SIMD) void k_motion(int w, int
     o.mwor = me.mwor;
     out[gid] = o;
   }
+  TIMING_END();
 }
 
 // decoder-side reconstruction of coded macroblocks (DecompressMDU p64.c:1179 +
@@ -2082,6 +2086,59 @@ __device__ __forceinline__ void intra_block(const p64gpu_encode_args &a, const I
 #ifndef BLK_PERSIST
 #define BLK_PERSIST 0
 #endif
+// the stores of an MB-grouped wave (k_intra_mbg, k_inter_mbg), all buffer
+// stores with out-of-range offsets instead of branches: the wave's levels run
+// (nvalid MBs x 768 bytes at coef + gmb0 x 768) from the LDS staging, the
+// lane's 8 reconstructed rows (rec_off, plane width pw), and from the record
+// lanes (rl) the MB record dword and the LastIntra byte of MB gmb
+__device__ __forceinline__ void mbg_store(const p64gpu_encode_args &a, const uint8_t *lds, int lane,
+                                          unsigned nmbs, unsigned gmb0, uint32_t nvalid, uint32_t rec_off,
+                                          int pw, const uint2 rows[8], bool rl, unsigned gmb, uint32_t mbw,
+                                          uint8_t li) {
+  const int nfr = (int)(nmbs / (unsigned)((a.width >> 4) * (a.height >> 4)));
+  const __amdgpu_buffer_rsrc_t coef =
+      __builtin_amdgcn_make_buffer_rsrc((void *)a.coef, (short)0, (int)(nmbs * 768u), BUF_RSRC_W3);
+  const uint32_t nbytes = nvalid * 768u;
+  __builtin_amdgcn_wave_barrier();
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    const uint32_t ob = 1024u * k + 16u * lane;
+    const uint4 v = *reinterpret_cast<const uint4 *>(lds + (ob >> 7) * LVL_STRIDE + (ob & 127));
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    u32x4 d;
+    d[0] = v.x;
+    d[1] = v.y;
+    d[2] = v.z;
+    d[3] = v.w;
+#if defined(PROBE_NOCOEF)  // development probes: drop one output stream (the work stays)
+    __builtin_amdgcn_raw_buffer_store_b128(d, coef, BUF_OOB, 0, 0);
+#else
+    __builtin_amdgcn_raw_buffer_store_b128(d, coef, ob < nbytes ? gmb0 * 768u + ob : BUF_OOB, 0, 0);
+#endif
+  }
+  __builtin_amdgcn_wave_barrier();
+  const __amdgpu_buffer_rsrc_t rec =
+      __builtin_amdgcn_make_buffer_rsrc((void *)a.recon, (short)0, (int)(nfr * a.frame_stride), BUF_RSRC_W3);
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+    u32x2 d;
+    d[0] = rows[k].x;
+    d[1] = rows[k].y;
+#if defined(PROBE_NOREC)
+    __builtin_amdgcn_raw_buffer_store_b64(d, rec, BUF_OOB, 0, 0);
+#else
+    __builtin_amdgcn_raw_buffer_store_b64(d, rec, rec_off + (uint32_t)mul24(k, pw), 0, 0);
+#endif
+  }
+  const __amdgpu_buffer_rsrc_t mbr =
+      __builtin_amdgcn_make_buffer_rsrc((void *)a.mb, (short)0, (int)(nmbs * 4u), BUF_RSRC_W3);
+  const __amdgpu_buffer_rsrc_t lir =
+      __builtin_amdgcn_make_buffer_rsrc((void *)a.last_intra, (short)0, (int)nmbs, BUF_RSRC_W3);
+  __builtin_amdgcn_raw_buffer_store_b32(mbw, mbr, rl ? 4u * gmb : BUF_OOB, 0, 0);
+  __builtin_amdgcn_raw_buffer_store_b8(li, lir, rl ? gmb : BUF_OOB, 0, 0);
+}
+
 // intra picture, MB-grouped block layout (blk_pos_mb): one wave = 10 MBs, a
 // lane per block; levels leave as one contiguous 7,680-byte run per wave
 template <bool QMB>
@@ -2104,57 +2161,14 @@ __global__ __launch_bounds__(256) BLK_OCC void k_intra_mbg(p64gpu_encode_args a,
   const uint32_t nvalid = min((unsigned)MBS_PER_WAVE, nmbs - gmb0);
   intra_block<false, (bool)INTRA_HALF>(a, f, lds, lane, o, gmb0 * 768u, 6 * nvalid);
   PRIO_ST();
-  // buffer stores throughout (32-bit offsets, out of range instead of a
-  // branch for the tail of the levels run and for the record lanes)
-  const int nfr = (int)(nmbs / (unsigned)((a.width >> 4) * (a.height >> 4)));
-#if !INTRA_HALF
-  {
-    const __amdgpu_buffer_rsrc_t coef =
-        __builtin_amdgcn_make_buffer_rsrc((void *)a.coef, (short)0, (int)(nmbs * 768u), BUF_RSRC_W3);
-    const uint32_t nbytes = nvalid * 768u;
-    __builtin_amdgcn_wave_barrier();
-#pragma unroll
-    for (int k = 0; k < 8; k++) {
-      const uint32_t ob = 1024u * k + 16u * lane;
-      const uint4 v = *reinterpret_cast<const uint4 *>(lds + (ob >> 7) * LVL_STRIDE + (ob & 127));
-      typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-      u32x4 d;
-      d[0] = v.x;
-      d[1] = v.y;
-      d[2] = v.z;
-      d[3] = v.w;
-#if defined(PROBE_NOCOEF)  // development probes: drop one output stream (the work stays)
-      __builtin_amdgcn_raw_buffer_store_b128(d, coef, BUF_OOB, 0, 0);
-#else
-      __builtin_amdgcn_raw_buffer_store_b128(d, coef, ob < nbytes ? gmb0 * 768u + ob : BUF_OOB, 0, 0);
-#endif
-    }
-    __builtin_amdgcn_wave_barrier();
-  }
-#endif
-  const __amdgpu_buffer_rsrc_t rec =
-      __builtin_amdgcn_make_buffer_rsrc((void *)a.recon, (short)0, (int)(nfr * a.frame_stride), BUF_RSRC_W3);
-#pragma unroll
-  for (int k = 0; k < 8; k++) {
-    typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
-    u32x2 d;
-    d[0] = o.rec[k].x;
-    d[1] = o.rec[k].y;
-#if defined(PROBE_NOREC)
-    __builtin_amdgcn_raw_buffer_store_b64(d, rec, BUF_OOB, 0, 0);
-#else
-    __builtin_amdgcn_raw_buffer_store_b64(d, rec, o.rec_off + (uint32_t)mul24(k, o.pw), 0, 0);
-#endif
-  }
-  // the MB's record and LastIntra (p64.c:909-910: MTYPE 0, CBP 0x3f) from
-  // lane b = 0 of each MB
+  // the MB's record and LastIntra (p64.c:909-910: MTYPE 0, CBP 0x3f, LastIntra
+  // reset) from lane b = 0 of each MB
   const bool rl = l % 6 == 0 && lane < 6 * MBS_PER_WAVE && gmb0 + (unsigned)(l / 6) < nmbs;
-  const __amdgpu_buffer_rsrc_t mbr =
-      __builtin_amdgcn_make_buffer_rsrc((void *)a.mb, (short)0, (int)(nmbs * 4u), BUF_RSRC_W3);
-  const __amdgpu_buffer_rsrc_t lir =
-      __builtin_amdgcn_make_buffer_rsrc((void *)a.last_intra, (short)0, (int)nmbs, BUF_RSRC_W3);
-  __builtin_amdgcn_raw_buffer_store_b32(0x3f00u, mbr, rl ? 4u * gmb : BUF_OOB, 0, 0);
-  __builtin_amdgcn_raw_buffer_store_b8((uint8_t)0, lir, rl ? gmb : BUF_OOB, 0, 0);
+#if !INTRA_HALF
+  mbg_store(a, lds, lane, nmbs, gmb0, nvalid, o.rec_off, o.pw, o.rec, rl, gmb, 0x3f00u, 0);
+#else
+  mbg_store(a, lds, lane, nmbs, gmb0, 0, o.rec_off, o.pw, o.rec, rl, gmb, 0x3f00u, 0);  // levels already out
+#endif
 }
 // one launch covers at most 2 GiB of pictures and of levels (the host splits
 // larger batches), so 32-bit offsets address both
@@ -2672,8 +2686,15 @@ __global__ __launch_bounds__(256) INTER_OCC void k_inter_mbg(p64gpu_encode_args 
   m.sad0 = (int)__builtin_amdgcn_raw_buffer_load_b32(mer, mo + 12, 0, 0);
   m.var = (int)__builtin_amdgcn_raw_buffer_load_b32(mer, mo + 16, 0, 0);
   m.varor = (int)__builtin_amdgcn_raw_buffer_load_b32(mer, mo + 20, 0, 0);
-  const int li = a.last_intra[gmb];
-  const int ov = a.mtype_override ? (int)a.mtype_override[gmb] : -1;
+  // LastIntra and the -o override by buffer loads (an absent override array
+  // reads as out of range: no branch around a load)
+  const __amdgpu_buffer_rsrc_t lir =
+      __builtin_amdgcn_make_buffer_rsrc((void *)a.last_intra, (short)0, (int)nmbs, BUF_RSRC_W3);
+  const __amdgpu_buffer_rsrc_t ovr = __builtin_amdgcn_make_buffer_rsrc(
+      (void *)a.mtype_override, (short)0, a.mtype_override ? (int)nmbs : 0, BUF_RSRC_W3);
+  const int li = __builtin_amdgcn_raw_buffer_load_b8(lir, gmb, 0, 0);
+  const int ovl = (int)(int8_t)__builtin_amdgcn_raw_buffer_load_b8(ovr, a.mtype_override ? gmb : BUF_OOB, 0, 0);
+  const int ov = a.mtype_override ? ovl : -1;
 
   // MTYPE (p64.c:734-772): the decision, the -o override, the intra refresh
   MeOut mo_;
@@ -2770,21 +2791,15 @@ __global__ __launch_bounds__(256) INTER_OCC void k_inter_mbg(p64gpu_encode_args 
   // (late, so its registers do not overlap the block's)
   if (repred) inter_pred(B, w, h, stride, pos, mt, mvx, mvy, prow);
   const uint32_t nvalid = min((unsigned)MBS_PER_WAVE, nmbs - gmb0);
-  flush_levels_run(lds, lane, gmb0 * 768u, nvalid * 768u, reinterpret_cast<uint8_t *>(a.coef));
   const int pw = pos.plane ? w >> 1 : w;
   const uint32_t ro = (uint32_t)((int64_t)pos.fi * stride) + (uint32_t)plane_offset(pos.plane, w, h) +
                       (uint32_t)mul24(pos.y, pw) + (uint32_t)pos.x;
-#pragma unroll
-  for (int k = 0; k < 8; k++) st_out(reinterpret_cast<uint2 *>(a.recon + ro + (uint32_t)mul24(k, pw)), prow[k]);
-  if (b == 0 && lane < 6 * MBS_PER_WAVE && gmb0 + (unsigned)(l / 6) < nmbs) {
-    p64_mb_rec r;  // p64.c:909-910
-    r.mtype = (int8_t)mt;
-    r.cbp = (int8_t)cbp;
-    r.mvx = (int8_t)(mt_mf(mt) ? mvx : 0);
-    r.mvy = (int8_t)(mt_mf(mt) ? mvy : 0);
-    a.mb[gmb] = r;
-    a.last_intra[gmb] = mt_intra(mt) ? 0 : (uint8_t)(li + 1);
-  }
+  // p64.c:909-910: the record (transmitted vector only for MC types) and LastIntra
+  const bool rl = b == 0 && lane < 6 * MBS_PER_WAVE && gmb0 + (unsigned)(l / 6) < nmbs;
+  const uint32_t mbw = (uint32_t)(mt & 0xff) | ((uint32_t)(cbp & 0xff) << 8) |
+                       (mt_mf(mt) ? ((uint32_t)(mvx & 0xff) << 16) | ((uint32_t)(mvy & 0xff) << 24) : 0u);
+  mbg_store(a, lds, lane, nmbs, gmb0, nvalid, ro, pw, prow, rl, gmb, mbw,
+            mt_intra(mt) ? (uint8_t)0 : (uint8_t)(li + 1));
 }
 
 // batched 8x8 block operations (one thread per block; shares the device
