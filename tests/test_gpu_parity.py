@@ -261,6 +261,55 @@ def test_batched_streams_vs_oracle(p64, oracle_mod, torch_dev, w, h, me_mode, sl
             np.testing.assert_array_equal(g[3][s], recon, err_msg=f"recon s{s} t{t}")
 
 
+def test_split_encoder_without_me_output_and_in_graph(p64, torch_dev):
+    """Inter pictures without an ME-record output run k_motion into the
+    library's scratch buffer: same levels, records and reconstruction as with
+    the output; and the same again when the launches are captured into a HIP
+    graph after one eager call (the scratch then exists outside the capture)."""
+    torch = torch_dev
+    w, h, S, T = 352, 288, 3, 3
+    nmb, pic = (w // 16) * (h // 16), w * h * 3 // 2
+    frames = np.stack([[p64.synth_frame(11 + s, t, w, h) for s in range(S)] for t in range(T)])
+
+    def run(want_me, graph=False):
+        li = torch.zeros(S * nmb, dtype=torch.uint8, device="cuda")
+        bufs = [torch.zeros(S * pic, dtype=torch.uint8, device="cuda") for _ in range(2)]
+        cur = [dev(torch, frames[t]) for t in range(T)]
+        outs = [p64.FrameBatchOut(coef=torch.empty((S, nmb, 6, 64), dtype=torch.int16, device="cuda"),
+                                  mb=torch.empty((S, nmb, 4), dtype=torch.int8, device="cuda"),
+                                  me=torch.empty((S, nmb, 7), dtype=torch.int32, device="cuda")
+                                  if want_me else None) for _ in range(T)]
+
+        def step(t):
+            p64.encode_frames(cur[t], bufs[(t + 1) % 2], bufs[t % 2], li, width=w, height=h,
+                              intra=(t == 0), quant=8, me_mode=p64.ME_FULL, search_limit=31,
+                              out=outs[t])
+        step(0)
+        if graph:
+            step(1)  # eager inter call: the scratch is allocated here
+            li.zero_()
+            step(0)
+            torch.cuda.synchronize()
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                for t in range(1, T):
+                    step(t)
+            g.replay()
+        else:
+            for t in range(1, T):
+                step(t)
+        torch.cuda.synchronize()
+        return [(host(o.coef), host(o.mb)) for o in outs], host(bufs[(T - 1) % 2])
+
+    ref_outs, ref_rec = run(True)
+    for graph in (False, True):
+        outs, rec = run(False, graph)
+        for t in range(T):
+            np.testing.assert_array_equal(outs[t][0], ref_outs[t][0], err_msg=f"coef t{t} graph={graph}")
+            np.testing.assert_array_equal(outs[t][1], ref_outs[t][1], err_msg=f"mb t{t} graph={graph}")
+        np.testing.assert_array_equal(rec, ref_rec)
+
+
 def test_intra_refresh_and_override(p64, oracle_mod, torch_dev):
     """LastIntra > 131 forces MTYPE 0 (p64.c:772); -o overrides (p64.c:761-768),
     including MC types without coefficients (4, 7) and MQUANT types."""
