@@ -2631,6 +2631,7 @@ __device__ __forceinline__ void inter_pred(const RecBufs &B, int w, int h, int64
   A.q = 0;
   A.coded = 1;
   const RecStageB S = rec_stage_b<false>(B, w, h, stride, A);  // source OOB (zeros) if intra
+  PRIO_LOW();  // the loads are out: the loop filter at normal priority
   pred_rows(S.pred, S.filter, prow);
 }
 // the prediction as packed rows (all zero when the source was not loaded)
@@ -2710,8 +2711,7 @@ __global__ __launch_bounds__(256) INTER_OCC void k_inter_mbg(p64gpu_encode_args 
   if (li > 131) mt = 0;
   const int mvx = m.mx, mvy = m.my;
   uint2 prow[8];
-  inter_pred(B, w, h, stride, pos, mt, mvx, mvy, prow);
-  PRIO_LOW();
+  inter_pred(B, w, h, stride, pos, mt, mvx, mvy, prow);  // (drops the priority)
 
   const bool intra = mt_intra(mt), tc = mt_tcoeff(mt);
   const int q = f.q;
