@@ -1625,31 +1625,8 @@ __device__ __forceinline__ void store_block(uint8_t *dst, int pw, const int v[64
 }
 
 // ChenDct (chendct.c:97-206) on a register block given as its 8 packed pixel
-// rows: column pass (pixels unpacked per column, so the packed rows and the
-// unpacked block are never live together), then row pass; leaves the raw
-// (pre-/8) coefficients in v
-__device__ __forceinline__ void fdct_block(const uint2 rows[8], int v[64]) {
-#pragma unroll
-  for (int c = 0; c < 8; c++) {
-    int x[8], o[8];
-#pragma unroll
-    for (int k = 0; k < 8; k++) x[k] = (int)(((c < 4 ? rows[k].x : rows[k].y) >> (8 * (c & 3))) & 255);
-    fwd_col<true>(x, o);
-#pragma unroll
-    for (int k = 0; k < 8; k++) v[8 * k + c] = o[k];
-    SCHED_FENCE();
-  }
-#pragma unroll
-  for (int r = 0; r < 8; r++) {
-    int o[8];
-    fwd_row<true>(v + 8 * r, o);
-#pragma unroll
-    for (int k = 0; k < 8; k++) v[8 * r + k] = opaque(o[k]);  // see fdct_block_pk
-    SCHED_FENCE();
-  }
-}
-// The same ChenDct with the row pass in packed 16-bit arithmetic: the column
-// pass (scalar) leaves each row as four (column 2j, 2j+1) int16 pairs -- its
+// rows (or the residual rows - prow), the row pass in packed 16-bit
+// arithmetic: the column pass (scalar) leaves each row as four (column 2j, 2j+1) int16 pairs -- its
 // outputs stay within +-5,800 for pixel or +-255 residual input -- and the
 // row pass runs the butterfly of fwd8 on pairs: v_pk_add/sub/ashr for the
 // sums, and every product pair C_a x + C_b y as ONE v_dot2_i32_i16 with the
@@ -1845,27 +1822,6 @@ __device__ __forceinline__ void iq_idct_intra_rec(int v[64], int q, uint2 rec[8]
     SCHED_FENCE();
   }
 }
-// the same ChenIDct followed by BoundIDctMatrix with nothing added (intra
-// blocks of an intra picture): packed reconstructed rows
-__device__ __forceinline__ void idct_block_rec(int v[64], uint2 rec[8]) {
-#pragma unroll
-  for (int c = 0; c < 8; c++) {
-    int x[8], o[8];
-#pragma unroll
-    for (int k = 0; k < 8; k++) x[k] = v[8 * k + c];
-    inv8<true, 4>(x, o);
-#pragma unroll
-    for (int k = 0; k < 8; k++) v[8 * k + c] = o[k];
-    SCHED_FENCE();
-  }
-#pragma unroll
-  for (int r = 0; r < 8; r++) {
-    int o[8];
-    inv8<true>(v + 8 * r, o);
-    rec[r] = final_clamp_pack8(o);
-    SCHED_FENCE();
-  }
-}
 
 // intra picture (p64.c:635, 770-771: every MB is MTYPE 0, CBP 0x3f), block
 // layout: load -> ChenDct -> BoundDct + CCITTFlatQuantize + FlatBound ->
@@ -1881,72 +1837,12 @@ __device__ __forceinline__ void idct_block_rec(int v[64], uint2 rec[8]) {
 // load/store-only version of the intra kernel needed).  Each wave writes its
 // 64 blocks' levels to its own LDS slot, then store instruction k writes
 // blocks 8k..8k+7 with 8 lanes per block: whole 128-byte lines.
-// output stores of the block-layout kernels (-DBLK_NT: non-temporal, probe)
-template <typename T>
-__device__ __forceinline__ void st_out(T *p, const T &v) {
-#if defined(BLK_NT)
-  typedef unsigned int u32 __attribute__((ext_vector_type(sizeof(T) / 4)));
-  __builtin_nontemporal_store(__builtin_bit_cast(u32, v), reinterpret_cast<u32 *>(p));
-#else
-  *p = v;
-#endif
-}
 constexpr int LVL_STRIDE = 144;  // bytes per lane: 128 + 16 pad, conflict-free ds_write_b128
 constexpr int LVL_WAVE = 64 * LVL_STRIDE;
 __device__ __forceinline__ void put_levels(uint8_t *lds, int lane, int k, uint4 v) {
   *reinterpret_cast<uint4 *>(lds + lane * LVL_STRIDE + k * 16) = v;
 }
-// my_off: byte offset of the lane's own block in the level array
-__device__ __forceinline__ void flush_levels(const uint8_t *lds, int lane, uint32_t my_off, uint8_t *coef) {
-  __builtin_amdgcn_wave_barrier();
-#pragma unroll
-  for (int k = 0; k < 8; k++) {
-    const int blk = 8 * k + (lane >> 3), ch = lane & 7;
-    const uint32_t off = (uint32_t)__shfl((int)my_off, blk);
-    const uint4 v = *reinterpret_cast<const uint4 *>(lds + blk * LVL_STRIDE + ch * 16);
-    st_out(reinterpret_cast<uint4 *>(coef + off + ch * 16), v);
-  }
-  __builtin_amdgcn_wave_barrier();
-}
 
-// MB-grouped waves: the wave's levels are `nbytes` contiguous bytes at
-// coef + off (uniform); store k writes bytes 1024k .. 1024k+1023 of them,
-// 16 per lane, from the staging slot of the lane that owns them
-__device__ __forceinline__ void flush_levels_run(const uint8_t *lds, int lane, uint32_t off, uint32_t nbytes,
-                                                 uint8_t *coef) {
-  __builtin_amdgcn_wave_barrier();
-#pragma unroll
-  for (int k = 0; k < 8; k++) {
-    const uint32_t o = 1024u * k + 16u * lane;
-    if (o < nbytes) {
-      const uint4 v = *reinterpret_cast<const uint4 *>(lds + (o >> 7) * LVL_STRIDE + (o & 127));
-      st_out(reinterpret_cast<uint4 *>(coef + off + o), v);
-    }
-  }
-  __builtin_amdgcn_wave_barrier();
-}
-
-// Half staging (k_intra_mbg): scan positions 0..31 of every lane, flushed,
-// then 32..63 -- 80 bytes per lane (64 + 16 pad, conflict-free for
-// ds_write_b128 at 16 lanes per cycle: starting banks 20·lane mod 64 are
-// distinct), 5 KB per wave, which lets 5 waves per SIMD fit the LDS.  A half
-// is 64 bytes of each block's 128: the run flush writes them as 16-byte
-// pieces (4 per block), consecutive lanes consecutive pieces.
-constexpr int LVLH_STRIDE = 80;
-constexpr int LVLH_WAVE = 64 * LVLH_STRIDE;
-__device__ __forceinline__ void flush_levels_half(const uint8_t *lds, int lane, uint32_t off, uint32_t nblk,
-                                                  int half, uint8_t *coef) {
-  __builtin_amdgcn_wave_barrier();
-#pragma unroll
-  for (int i = 0; i < 4; i++) {
-    const uint32_t pc = 64u * i + (uint32_t)lane, blk = pc >> 2, sub = pc & 3;
-    if (blk < nblk) {
-      const uint4 v = *reinterpret_cast<const uint4 *>(lds + blk * LVLH_STRIDE + sub * 16);
-      st_out(reinterpret_cast<uint4 *>(coef + off + blk * 128 + half * 64 + sub * 16), v);
-    }
-  }
-  __builtin_amdgcn_wave_barrier();
-}
 
 // dword 3 of a raw buffer resource on gfx9-family parts (CDNA): 32-bit data format
 constexpr int BUF_RSRC_W3 = 0x00020000;
@@ -1981,67 +1877,27 @@ __device__ __forceinline__ IntraFetch intra_fetch_at(const p64gpu_encode_args &a
   f.q = QMB ? a.quant_mb[f.p.fi * nmb + f.p.mb] : a.quant;
   return f;
 }
-template <bool QMB>
-__device__ __forceinline__ IntraFetch intra_fetch(const p64gpu_encode_args &a, const BlkDiv &kd,
-                                                  unsigned t) {
-  return intra_fetch_at<QMB>(a, blk_pos(t, a.width, a.height, kd));
-}
-// A block's outputs between its computation and its stores: the persistent
-// kernel stores block i in the middle of block i+1's computation (after its
-// forward transform), so the waves' stores drain while they compute instead of
-// in one burst at the end of every block.
+// A block's outputs between its computation and its stores
 struct IntraOut {
   uint2 rec[8];     // reconstructed rows
   uint32_t rec_off; // byte offset of the block's first row from a.recon
-  uint32_t lvl_off; // byte offset of its levels from a.coef
-  uint32_t gmb;     // its macroblock in the launch
   int pw;           // its plane's width
 };
-__device__ __forceinline__ void intra_store(const p64gpu_encode_args &a, const IntraOut &o, const uint8_t *lds,
-                                            int lane) {
-  flush_levels(lds, lane, o.lvl_off, reinterpret_cast<uint8_t *>(a.coef));
-#pragma unroll
-  for (int k = 0; k < 8; k++)
-    st_out(reinterpret_cast<uint2 *>(a.recon + o.rec_off + (uint32_t)mul24(k, o.pw)), o.rec[k]);
-  // the MB's record and LastIntra (p64.c:909-910) from all six of its lanes
-  // (identical bytes): no branch around a store, so the wait counts of the
-  // persistent loop stay exact
-  p64_mb_rec r;
-  r.mtype = 0;
-  r.cbp = 0x3f;
-  r.mvx = 0;
-  r.mvy = 0;
-  a.mb[o.gmb] = r;
-  a.last_intra[o.gmb] = 0;
-}
-// one block: ChenDct, [the previous block's stores], quantise + zigzag into
-// the LDS staging, dequantise, ChenIDct, reconstruction into `out`
-// HALF: half staging (flush_levels_half) of a run of run_blk blocks at
-// coef + run_off, flushed from here
-template <bool PENDING, bool HALF = false>
+// one block: ChenDct, quantise + zigzag into the LDS staging, dequantise,
+// ChenIDct, reconstruction into `out`
 __device__ __forceinline__ void intra_block(const p64gpu_encode_args &a, const IntraFetch &f, uint8_t *lds,
-                                            int lane, IntraOut &out, uint32_t run_off = 0, uint32_t run_blk = 0) {
-  const int w = a.width, h = a.height, nmb = (w >> 4) * (h >> 4);
+                                            int lane, IntraOut &out) {
+  const int w = a.width, h = a.height;
   const BlkPos &p = f.p;
-  const uint32_t gmb = (uint32_t)(p.fi * nmb + p.mb);
   const int q = f.q;
   // c_qrecip.r[q] computed in place (no dependent table load in the loop)
   const float rq = __builtin_bit_cast(float, __builtin_bit_cast(uint32_t, 1.0f / (float)(2 * q)) + 1u);
   const float rqe = (q & 1) ? 0.0f : rq;
   const int qb = quant_bound(q);
-#if defined(INTRA_SCALAR_IQ)
-  const int q2 = 2 * q, qq = q - (int)!(q & 1);
-#endif
   int v[64];
-#if defined(BLK_SCALAR_FDCT)
-  fdct_block(f.rows, v);
-#else
   fdct_block_pk(f.rows, v);
-#endif
-  if (PENDING) intra_store(a, out, lds, lane);
   // in scan order: quantise (BoundDct + CCITTFlatQuantize + FlatBound), pack
-  // the level pair, dequantise (ICCITTFlatQuantize) in place; 16 bytes of
-  // levels at a time into the wave's LDS staging
+  // the level pair; 16 bytes of levels at a time into the wave's LDS staging
 #pragma unroll
   for (int k = 0; k < 8; k++) {
     uint32_t pk[4];
@@ -2053,39 +1909,18 @@ __device__ __forceinline__ void intra_block(const p64gpu_encode_args &a, const I
         const int e = k_zz.inv[8 * k + 2 * j + i];
         const bool dc = e == 0;
         l2[i] = quantise<true, true>(v[e], dc ? -0x7fffffff : -qb, dc ? 2047 : qb, dc, rq, rqe);
-#if defined(INTRA_SCALAR_IQ)
-        v[e] = dequantise<true, true>(l2[i], dc, q2, qq);
-#else
         v[e] = l2[i];  // dequantised in pairs by iq_idct_intra_rec
-#endif
       }
       pk[j] = __builtin_amdgcn_perm((uint32_t)l2[1], (uint32_t)l2[0], 0x05040100u);
     }
-    if (HALF) {
-      *reinterpret_cast<uint4 *>(lds + lane * LVLH_STRIDE + (k & 3) * 16) = make_uint4(pk[0], pk[1], pk[2], pk[3]);
-      if ((k & 3) == 3) flush_levels_half(lds, lane, run_off, run_blk, k >> 2, reinterpret_cast<uint8_t *>(a.coef));
-    } else {
-      put_levels(lds, lane, k, make_uint4(pk[0], pk[1], pk[2], pk[3]));
-    }
+    put_levels(lds, lane, k, make_uint4(pk[0], pk[1], pk[2], pk[3]));
     SCHED_FENCE();
   }
-#if defined(INTRA_SCALAR_IQ)
-  idct_block_rec(v, out.rec);  // + BoundIDctMatrix
-#else
-  iq_idct_intra_rec(v, q, out.rec);
-#endif
+  iq_idct_intra_rec(v, q, out.rec);  // ICCITTFlatQuantize + ChenIDct + BoundIDctMatrix
   out.pw = p.plane ? w >> 1 : w;
   out.rec_off = (uint32_t)((int64_t)p.fi * a.frame_stride) + (uint32_t)plane_offset(p.plane, w, h) +
                 (uint32_t)mul24(p.y, out.pw) + (uint32_t)p.x;
-  out.lvl_off = (gmb * 6 + (uint32_t)p.b) * 128;
-  out.gmb = gmb;
 }
-// -DBLK_PERSIST=1: a persistent grid with the next block's fetch in flight
-// (measured slower: 66 vs 61 us per CIF S=256 launch; the persistent grid fits
-// only 2 waves per SIMD, the one-block-per-lane grid 3)
-#ifndef BLK_PERSIST
-#define BLK_PERSIST 0
-#endif
 // the stores of an MB-grouped wave (k_intra_mbg, k_inter_mbg), all buffer
 // stores with out-of-range offsets instead of branches: the wave's levels run
 // (nvalid MBs x 768 bytes at coef + gmb0 x 768) from the LDS staging, the
@@ -2142,14 +1977,10 @@ __device__ __forceinline__ void mbg_store(const p64gpu_encode_args &a, const uin
 // intra picture, MB-grouped block layout (blk_pos_mb): one wave = 10 MBs, a
 // lane per block; levels leave as one contiguous 7,680-byte run per wave
 template <bool QMB>
-#ifndef INTRA_HALF
-#define INTRA_HALF 0
-#endif
 __global__ __launch_bounds__(256) BLK_OCC void k_intra_mbg(p64gpu_encode_args a, BlkDiv kd, unsigned nmbs) {
-  constexpr int LW = INTRA_HALF ? LVLH_WAVE : LVL_WAVE;
-  __shared__ __align__(16) uint8_t lvl[4 * LW];
+  __shared__ __align__(16) uint8_t lvl[4 * LVL_WAVE];
   const int lane = threadIdx.x & 63;
-  uint8_t *lds = lvl + (threadIdx.x >> 6) * LW;
+  uint8_t *lds = lvl + (threadIdx.x >> 6) * LVL_WAVE;
   const unsigned gmb0 = (blockIdx.x * 4u + (threadIdx.x >> 6)) * MBS_PER_WAVE;
   if (gmb0 >= nmbs) return;  // whole wave
   PRIO_HIGH();
@@ -2159,99 +1990,12 @@ __global__ __launch_bounds__(256) BLK_OCC void k_intra_mbg(p64gpu_encode_args a,
   PRIO_LOW();
   IntraOut o;
   const uint32_t nvalid = min((unsigned)MBS_PER_WAVE, nmbs - gmb0);
-  intra_block<false, (bool)INTRA_HALF>(a, f, lds, lane, o, gmb0 * 768u, 6 * nvalid);
+  intra_block(a, f, lds, lane, o);
   PRIO_ST();
   // the MB's record and LastIntra (p64.c:909-910: MTYPE 0, CBP 0x3f, LastIntra
   // reset) from lane b = 0 of each MB
   const bool rl = l % 6 == 0 && lane < 6 * MBS_PER_WAVE && gmb0 + (unsigned)(l / 6) < nmbs;
-#if !INTRA_HALF
   mbg_store(a, lds, lane, nmbs, gmb0, nvalid, o.rec_off, o.pw, o.rec, rl, gmb, 0x3f00u, 0);
-#else
-  mbg_store(a, lds, lane, nmbs, gmb0, 0, o.rec_off, o.pw, o.rec, rl, gmb, 0x3f00u, 0);  // levels already out
-#endif
-}
-// one launch covers at most 2 GiB of pictures and of levels (the host splits
-// larger batches), so 32-bit offsets address both
-template <bool QMB>
-__global__ __launch_bounds__(256) BLK_OCC void k_intra_blk(p64gpu_encode_args a, BlkDiv kd, unsigned total,
-                                                           unsigned stride) {
-  __shared__ __align__(16) uint8_t lvl[4 * LVL_WAVE];
-  const int lane = threadIdx.x & 63;
-  uint8_t *lds = lvl + (threadIdx.x >> 6) * LVL_WAVE;
-  // lanes past the end redo the last block (identical stores): every lane of
-  // a wave takes part in the level staging, every wave walks its blocks with
-  // a wave-uniform trip count
-  unsigned t = blockIdx.x * 256u + (threadIdx.x & ~63u);  // the wave's first block
-  if (t >= total) return;
-  const unsigned last = total - 1;
-#if defined(P64_TIMING)  // development probe: each wave's start/end shader and real clocks
-  const uint64_t clk0 = __builtin_amdgcn_s_memtime(), rt0 = __builtin_amdgcn_s_memrealtime();
-  uint64_t rtl = 0, rtc = 0;
-#define CLOCK_END()                                                                        \
-  do {                                                                                     \
-    const uint64_t c1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime(); \
-    if (lane == 0 && g_phase_buf) {                                                        \
-      uint32_t *o = g_phase_buf + (size_t)((blockIdx.x * 256u + threadIdx.x) >> 6) * 8;   \
-      o[0] = (uint32_t)rt0;                                                                \
-      o[1] = (uint32_t)r1;                                                                 \
-      o[2] = (uint32_t)(c1 - clk0);                                                        \
-      o[3] = (uint32_t)rtl;                                                                \
-      o[4] = (uint32_t)rtc;                                                                \
-    }                                                                                      \
-  } while (0)
-#define CLOCK_MARK(v) v = __builtin_amdgcn_s_memrealtime()
-#else
-#define CLOCK_END()
-#define CLOCK_MARK(v)
-#endif
-  IntraFetch f = intra_fetch<QMB>(a, kd, min(t + lane, last));
-  IntraOut o;
-  if (!BLK_PERSIST) {
-#if defined(P64_TIMING)
-    __builtin_amdgcn_s_waitcnt(0);
-#endif
-    CLOCK_MARK(rtl);
-    intra_block<false>(a, f, lds, lane, o);
-    CLOCK_MARK(rtc);
-    intra_store(a, o, lds, lane);
-    CLOCK_END();
-    return;
-  }
-  // drain the first fetch here: entering the loop with nothing pending keeps
-  // hipcc's wait counts inside it exact (otherwise it merges the pending
-  // first fetch into the loop header and waits for every store each block)
-  __builtin_amdgcn_s_waitcnt(0);
-#if defined(BLK_STAGGER)
-  if (blockIdx.x & 1)  // development probe: odd workgroups start later
-    for (int i = 0; i < BLK_STAGGER; i++) __builtin_amdgcn_s_sleep(127);
-#endif
-#if defined(BLK_PERSIST_DEFER)
-  // the next block's fetch is always in flight; two fetch slots alternate
-  // (unrolled by two) so no loop-carried copy waits for a fetch; each block's
-  // stores are issued inside the next block's computation
-  IntraFetch g = intra_fetch<QMB>(a, kd, min(t + stride + lane, last));
-  intra_block<false>(a, f, lds, lane, o);
-  for (t += stride; t < total; t += stride) {
-    f = intra_fetch<QMB>(a, kd, min(t + stride + lane, last));
-    intra_block<true>(a, g, lds, lane, o);
-    t += stride;
-    if (t >= total) break;
-    g = intra_fetch<QMB>(a, kd, min(t + stride + lane, last));
-    intra_block<true>(a, f, lds, lane, o);
-  }
-#else
-  // the next block's fetch is in flight while this one is transformed
-  for (;;) {
-    const IntraFetch fn = intra_fetch<QMB>(a, kd, min(t + stride + lane, last));
-    intra_block<false>(a, f, lds, lane, o);
-    t += stride;
-    if (t >= total) break;
-    intra_store(a, o, lds, lane);
-    f = fn;
-  }
-#endif
-  intra_store(a, o, lds, lane);
-  CLOCK_END();
 }
 
 // The source of an 8x8 prediction at (x, y) of a plane (any byte alignment):
@@ -3184,8 +2928,6 @@ static int encode_launch(const p64gpu_encode_args *a, const int32_t *mb_list, in
       c.quant_mb = a->quant_mb ? a->quant_mb + m0 : nullptr;
       c.coef = a->coef + m0 * 384;
       c.mb = a->mb + m0;
-      const int64_t nblk = (int64_t)c.nframes * nmb * 6;
-#if !defined(BLK_MBMAP) || BLK_MBMAP
       const int64_t nm = (int64_t)c.nframes * nmb, waves = (nm + MBS_PER_WAVE - 1) / MBS_PER_WAVE;
       if (c.quant_mb)
         hipLaunchKernelGGL(k_intra_mbg<true>, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, st, c,
@@ -3193,20 +2935,6 @@ static int encode_launch(const p64gpu_encode_args *a, const int32_t *mb_list, in
       else
         hipLaunchKernelGGL(k_intra_mbg<false>, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, st, c,
                            blk_div(a->width, a->height), (unsigned)nm);
-      (void)nblk;
-#else
-      unsigned wg;
-      const void *kfn = c.quant_mb ? (const void *)k_intra_blk<true> : (const void *)k_intra_blk<false>;
-      int s2 = persistent_grid(kfn, nblk, &wg);
-      if (s2) return s2;
-      if (!BLK_PERSIST) wg = (unsigned)((nblk + 255) / 256);
-      if (c.quant_mb)
-        hipLaunchKernelGGL(k_intra_blk<true>, dim3(wg), dim3(256), 0, st, c, blk_div(a->width, a->height),
-                           (unsigned)nblk, wg * 256u);
-      else
-        hipLaunchKernelGGL(k_intra_blk<false>, dim3(wg), dim3(256), 0, st, c, blk_div(a->width, a->height),
-                           (unsigned)nblk, wg * 256u);
-#endif
       HIP_TRY(hipGetLastError());
     }
     return P64GPU_OK;

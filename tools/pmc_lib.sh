@@ -13,4 +13,4 @@ for grp in "$@"; do
   i=$((i+1))
 done
 python3 $R/tools/pmc_summary.py $OUT > $OUT/summary.txt
-grep -E "k_intra_blk|k_recon_blk|k_encode<0>|k_decode_recon" $OUT/summary.txt
+grep -E "k_intra_mbg|k_recon_mbg|k_inter_mbg|k_motion|k_encode" $OUT/summary.txt
