@@ -2274,31 +2274,17 @@ __device__ __forceinline__ void rec_block_pk(int w, int h, int64_t stride, __amd
 // decoder reconstruction, MB-grouped block layout (blk_pos_mb), one block per
 // lane and no loop: 10 MBs per wave, each lane loads its MB's record, then its
 // levels and prediction, reconstructs and stores.  Without the persistent
-// kernel's in-flight registers it fits 4 waves per SIMD, and those waves hide
-// each other's two dependent load latencies (measured faster than
+// kernel's in-flight registers it fits 3 waves per SIMD (139 VGPRs), and those
+// waves hide each other's two dependent load latencies (measured faster than
 // k_recon_blk, whose 237 VGPRs allow 2).  Lanes past the batch (and lanes
 // 60..63) get coded = 0: every load and store of theirs is out of range.
 __global__ __launch_bounds__(256) RECON_OCC void k_recon_mbg(int w, int h, int64_t stride, const uint8_t *refp,
                                                            uint8_t *recp, const int16_t *coef,
                                                            const p64_mb_rec *mbr, const uint8_t *quant_mb,
                                                            const uint8_t *coded_mask, BlkDiv kd, unsigned nmbs) {
-#if defined(RECON_LDS_LEVELS)
-  __shared__ __align__(16) uint8_t lvl[4 * LVL_WAVE];
-  uint8_t *lds = lvl + (threadIdx.x >> 6) * LVL_WAVE;
-#endif
   const int lane = threadIdx.x & 63;
   const unsigned gmb0 = (blockIdx.x * 4u + (threadIdx.x >> 6)) * MBS_PER_WAVE;
   if (gmb0 >= nmbs) return;  // whole wave
-#if defined(RECON_STAGGER)  // experiment: de-phase the first round of workgroups
-  if (blockIdx.x < 768u) {
-    const unsigned k = blockIdx.x >> 8;
-    if (k == 1) __builtin_amdgcn_s_sleep(RECON_STAGGER);
-    if (k == 2) {
-      __builtin_amdgcn_s_sleep(RECON_STAGGER);
-      __builtin_amdgcn_s_sleep(RECON_STAGGER);
-    }
-  }
-#endif
   const int nmb = (w >> 4) * (h >> 4), nfr = (int)(nmbs / (unsigned)nmb);
   RecBufs B;
   B.ref = __builtin_amdgcn_make_buffer_rsrc((void *)refp, (short)0, (int)(nfr * stride), BUF_RSRC_W3);
@@ -2318,36 +2304,8 @@ __global__ __launch_bounds__(256) RECON_OCC void k_recon_mbg(int w, int h, int64
   A.m = __builtin_amdgcn_raw_buffer_load_b32(B.mb, 4 * gmb, 0, 0);
   A.q = __builtin_amdgcn_raw_buffer_load_b8(B.q, gmb, 0, 0);
   A.coded = __builtin_amdgcn_raw_buffer_load_b8(B.mask, valid ? gmb : BUF_OOB, 0, 0);
-#if !defined(RECON_LDS_LEVELS)
   const RecStageB S = rec_stage_b(B, w, h, stride, A);
   PRIO_LOW();
-#else
-  // -DRECON_LDS_LEVELS (measured slower, 42.3 vs 38.3 us): the wave's levels
-  // are one contiguous run of 7,680 bytes: read it with whole-line loads (16
-  // bytes per lane, consecutive lanes consecutive) into the LDS staging, 144
-  // bytes per block, skipping the chunks of blocks that carry no levels
-  // (their offsets out of range: zeros, no traffic); a lane then takes its
-  // block's 128 bytes from LDS.
-  RecStageB S = rec_stage_b<false>(B, w, h, stride, A);
-  const uint64_t ckm = __ballot(S.ck);
-#pragma unroll
-  for (int k = 0; k < 8; k++) {
-    const int c = lane + 64 * k, j = c >> 3;  // 16-byte chunk, its block (lane)
-    const bool on = c < 8 * 6 * MBS_PER_WAVE && ((ckm >> j) & 1);
-    const auto v = __builtin_amdgcn_raw_buffer_load_b128(B.coef, on ? gmb0 * 768u + 16u * c : BUF_OOB, 0, 0);
-    if (c < 8 * 6 * MBS_PER_WAVE)
-      *reinterpret_cast<uint4 *>(lds + j * LVL_STRIDE + (c & 7) * 16) = make_uint4(v[0], v[1], v[2], v[3]);
-  }
-  __builtin_amdgcn_wave_barrier();
-#pragma unroll
-  for (int k = 0; k < 8; k++) {
-    const uint4 v = *reinterpret_cast<const uint4 *>(lds + lane * LVL_STRIDE + k * 16);
-    S.lq[k][0] = v.x;
-    S.lq[k][1] = v.y;
-    S.lq[k][2] = v.z;
-    S.lq[k][3] = v.w;
-  }
-#endif
   rec_block_pk(w, h, stride, rec, A, S);
 }
 
