@@ -2378,7 +2378,8 @@ __global__ __launch_bounds__(256) INTER_OCC void k_inter_mbg(p64gpu_encode_args 
   const int l = min(lane, 6 * MBS_PER_WAVE - 1), b = l % 6;
   const unsigned gmb = min(gmb0 + (unsigned)(l / 6), nmbs - 1);  // tail lanes repeat the last MB
   const BlkPos pos = blk_pos_mb(gmb, b, w, h, kd);
-  const IntraFetch f = intra_fetch_at<QMB>(a, pos);  // current rows, q
+  // the ME record, LastIntra and override first: the prediction loads wait
+  // on them (wait counts are in issue order), the current rows only later
   const __amdgpu_buffer_rsrc_t mer =
       __builtin_amdgcn_make_buffer_rsrc((void *)me, (short)0, (int)(nmbs * sizeof(p64_me_rec)), BUF_RSRC_W3);
   const uint32_t mo = gmb * (uint32_t)sizeof(p64_me_rec);
@@ -2398,6 +2399,7 @@ __global__ __launch_bounds__(256) INTER_OCC void k_inter_mbg(p64gpu_encode_args 
   const int li = __builtin_amdgcn_raw_buffer_load_b8(lir, gmb, 0, 0);
   const int ovl = (int)(int8_t)__builtin_amdgcn_raw_buffer_load_b8(ovr, a.mtype_override ? gmb : BUF_OOB, 0, 0);
   const int ov = a.mtype_override ? ovl : -1;
+  const IntraFetch f = intra_fetch_at<QMB>(a, pos);  // current rows, q
 
   // MTYPE (p64.c:734-772): the decision, the -o override, the intra refresh
   MeOut mo_;
