@@ -2104,17 +2104,6 @@ __device__ __forceinline__ RecStageB rec_stage_b(const RecBufs &B, int w, int h,
   S.ck = rec_block_coded(A);
   S.inter = A.coded && !mt_intra(mt);
   S.filter = mt_filter(mt);
-  if (LEVELS) {
-    const uint32_t co = S.ck ? (uint32_t)(((p.fi * nmb + p.mb) * 6 + p.b) * 128) : BUF_OOB;
-#pragma unroll
-    for (int k = 0; k < 8; k++) {
-      const auto v = __builtin_amdgcn_raw_buffer_load_b128(B.coef, co + 16 * k, 0, 0);
-      S.lq[k][0] = v[0];
-      S.lq[k][1] = v[1];
-      S.lq[k][2] = v[2];
-      S.lq[k][3] = v[3];
-    }
-  }
   const int pw = p.plane ? w >> 1 : w, ph = p.plane ? h >> 1 : h;
   int dx = 0, dy = 0;
   if (mt_mf(mt)) {  // chroma MV/2 with C truncation (io.c:268-270)
@@ -2136,6 +2125,19 @@ __device__ __forceinline__ RecStageB rec_stage_b(const RecBufs &B, int w, int h,
     S.pred.d[k][0] = v[0];
     S.pred.d[k][1] = v[1];
     S.pred.d[k][2] = __builtin_amdgcn_raw_buffer_load_b32(B.ref, po3 + (uint32_t)mul24(k, pw), 0, 0);
+  }
+  // the levels after the prediction source: the prediction is formed first,
+  // and wait counts are in issue order
+  if (LEVELS) {
+    const uint32_t co = S.ck ? (uint32_t)(((p.fi * nmb + p.mb) * 6 + p.b) * 128) : BUF_OOB;
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      const auto v = __builtin_amdgcn_raw_buffer_load_b128(B.coef, co + 16 * k, 0, 0);
+      S.lq[k][0] = v[0];
+      S.lq[k][1] = v[1];
+      S.lq[k][2] = v[2];
+      S.lq[k][3] = v[3];
+    }
   }
   return S;
 }
