@@ -33,6 +33,8 @@ def main():
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--width", type=int, default=352)
     ap.add_argument("--height", type=int, default=288)
+    ap.add_argument("--skew", type=int, default=0,
+                    help="bytes between the two reconstruction buffers' placements (16-aligned)")
     a = ap.parse_args()
     w, h, S = a.width, a.height, a.streams
     nmb = (w // 16) * (h // 16)
@@ -40,7 +42,10 @@ def main():
     fr = p64_amd.synth_frames_device(w, h, 1, S, 0, 8)  # 8 slots: 311 MB > the 256 MB MALL
     li = torch.zeros(S * nmb, dtype=torch.uint8, device="cuda")
     r0 = torch.zeros(S * pic, dtype=torch.uint8, device="cuda")
-    r1 = torch.zeros_like(r0)
+    if a.skew:  # the second buffer `skew` bytes into a larger allocation
+        r1 = torch.zeros(S * pic + a.skew, dtype=torch.uint8, device="cuda")[a.skew:]
+    else:
+        r1 = torch.zeros_like(r0)
     out = p64_amd.FrameBatchOut(coef=torch.empty((S, nmb, 6, 64), dtype=torch.int16, device="cuda"),
                                 mb=torch.empty((S, nmb, 4), dtype=torch.int8, device="cuda"),
                                 me=torch.empty((S, nmb, 7), dtype=torch.int32, device="cuda"))
