@@ -747,6 +747,7 @@ def run_intra(args, torch, dist, np, p64_amd, world, frames, S, nmb, pic, nslots
             "roofline": roofline(mbs * INTRA_BYTES_PER_MB, kavg, "k_intra_mbg<false>",
                                  load_pmc(args.pmc_json, key),
                                  algorithmic_bytes_per_mb=INTRA_BYTES_PER_MB, timing=timing_note(args)),
+            "valu_busy": (load_pmc(args.pmc_json, key) or {}).get("valu_busy"),
             "verified_vs_oracle": verified}
 
 
@@ -809,6 +810,7 @@ def run_decode(args, torch, dist, np, p64_amd, world, enc, S, nmb, pic):
                        "macroblocks_per_step_per_gpu": mbs},
             "roofline": roofline(bpl, kavg, "k_recon_mbg", load_pmc(args.pmc_json, key),
                                  algorithmic_bytes_per_mb=round(bpl / mbs, 1), timing=timing_note(args)),
+            "valu_busy": (load_pmc(args.pmc_json, key) or {}).get("valu_busy"),
             "verified_vs_encoder": {"ok": ok, "note": "last decoded picture == encoder "
                                                       "reconstruction, all sequences"}}
 
