@@ -2708,6 +2708,20 @@ static p64_me_rec *me_scratch(size_t n, hipStream_t st) {
   return g_me_buf;
 }
 
+// pictures per launch of the block-layout kernels: every buffer of a launch
+// within the 2 GiB of a 32-bit buffer offset (per = the larger of a picture's
+// bytes and its levels' bytes).  P64GPU_CHUNK_BYTES lowers the limit (tests
+// exercise the split launches with it); read on every call.
+int pictures_per_launch(int64_t per) {
+  int64_t lim = ((int64_t)1 << 31) - 1;
+  const char *e = getenv("P64GPU_CHUNK_BYTES");
+  if (e && *e) {
+    const long long v = atoll(e);
+    if (v > 0 && v < lim) lim = v;
+  }
+  const int64_t n = lim / per;
+  return n < 1 ? 1 : (int)n;
+}
 // P64GPU_RECON_PERSISTENT=1: the persistent pipelined decoder k_recon_blk
 // instead of k_recon_mbg (kept for A/B measurements)
 bool recon_persistent() {
@@ -2879,7 +2893,7 @@ static int encode_launch(const p64gpu_encode_args *a, const int32_t *mb_list, in
     // pictures per launch: pictures and levels of a launch within 2 GiB
     const int nmb = (a->width / 16) * (a->height / 16);
     const int64_t per = (int64_t)nmb * 768 > a->frame_stride ? (int64_t)nmb * 768 : a->frame_stride;
-    const int chunk = (int)((((int64_t)1 << 31) - 1) / per);
+    const int chunk = pictures_per_launch(per);
     for (int f0 = 0; f0 < a->nframes; f0 += chunk) {
       p64gpu_encode_args c = *a;
       c.nframes = a->nframes - f0 < chunk ? a->nframes - f0 : chunk;
@@ -2914,7 +2928,7 @@ static int encode_launch(const p64gpu_encode_args *a, const int32_t *mb_list, in
                            a->ref, a->cur, a->search_limit, me, kd);
       HIP_TRY(hipGetLastError());
       const int64_t per = (int64_t)nmb * 768 > a->frame_stride ? (int64_t)nmb * 768 : a->frame_stride;
-      const int chunk = (int)((((int64_t)1 << 31) - 1) / per);
+      const int chunk = pictures_per_launch(per);
       for (int f0 = 0; f0 < a->nframes; f0 += chunk) {
         p64gpu_encode_args c = *a;
         c.nframes = a->nframes - f0 < chunk ? a->nframes - f0 : chunk;
@@ -2965,7 +2979,7 @@ int p64gpu_decode_recon(int w, int h, int nframes, int64_t stride, const uint8_t
     // pictures per launch: every buffer of a launch within the 2 GiB range
     // of the block kernels' 32-bit buffer offsets
     const int64_t per = (int64_t)nmb * 768 > stride ? (int64_t)nmb * 768 : stride;
-    const int chunk = (int)((((int64_t)1 << 31) - 1) / per);
+    const int chunk = pictures_per_launch(per);
     for (int f0 = 0; f0 < nframes; f0 += chunk) {
       const int nf = nframes - f0 < chunk ? nframes - f0 : chunk;
       const int64_t blocks = (int64_t)nf * nmb * 6;

@@ -310,6 +310,37 @@ def test_split_encoder_without_me_output_and_in_graph(p64, torch_dev):
         np.testing.assert_array_equal(rec, ref_rec)
 
 
+def test_split_launches_match_single_launch(p64, torch_dev, monkeypatch):
+    """Batches larger than one launch's 2 GiB of 32-bit buffer offsets are cut
+    into several launches (intra, inter block kernel, decoder).  A lowered
+    limit (P64GPU_CHUNK_BYTES: one picture per launch) gives the same levels,
+    records and reconstructions as one launch."""
+    torch = torch_dev
+    w, h, S = 352, 288, 3
+    nmb, pic = (w // 16) * (h // 16), w * h * 3 // 2
+    frames = [dev(torch, np.stack([p64.synth_frame(31 + s, t, w, h) for s in range(S)])) for t in range(2)]
+
+    def run():
+        li = torch.zeros(S * nmb, dtype=torch.uint8, device="cuda")
+        r0 = torch.zeros(S * pic, dtype=torch.uint8, device="cuda")
+        r1 = torch.zeros_like(r0)
+        o0 = p64.encode_frames(frames[0], None, r0, li, width=w, height=h, intra=True, quant=5)
+        o1 = p64.encode_frames(frames[1], r0, r1, li, width=w, height=h, intra=False, quant=5,
+                               me_mode=p64.ME_FULL, search_limit=31)
+        qmb = torch.full((S * nmb,), 5, dtype=torch.uint8, device="cuda")
+        d1 = torch.zeros_like(r0)
+        p64.decode_recon(r0, d1, o1.coef, o1.mb, qmb, torch.ones_like(qmb), width=w, height=h)
+        torch.cuda.synchronize()
+        return [host(t) for t in (o0.coef, o0.mb, r0, o1.coef, o1.mb, r1, d1, li)]
+
+    whole = run()
+    monkeypatch.setenv("P64GPU_CHUNK_BYTES", "200000")
+    split = run()
+    for a, b in zip(whole, split):
+        np.testing.assert_array_equal(a, b)
+    np.testing.assert_array_equal(whole[6], whole[5])  # decoder == encoder reconstruction
+
+
 def test_intra_refresh_and_override(p64, oracle_mod, torch_dev):
     """LastIntra > 131 forces MTYPE 0 (p64.c:772); -o overrides (p64.c:761-768),
     including MC types without coefficients (4, 7) and MQUANT types."""
