@@ -2204,7 +2204,7 @@ __global__ __launch_bounds__(256) BLK_OCC void k_recon_blk(int w, int h, int64_t
   RecStageA A1 = rec_stage_a(B, w, h, kd, min(t + gstride, last));
   RecStageB S0 = rec_stage_b(B, w, h, stride, A0);
   // drain the pipeline fill: entering the loop with nothing pending keeps
-  // hipcc's wait counts inside it exact (see k_intra_blk)
+  // hipcc's wait counts inside it exact
   __builtin_amdgcn_s_waitcnt(0);
   // unrolled by two so the stage-B registers alternate between S0 and S1
   // instead of being copied (and waited for) at the back-edge
