@@ -341,6 +341,46 @@ def test_split_launches_match_single_launch(p64, torch_dev, monkeypatch):
     np.testing.assert_array_equal(whole[6], whole[5])  # decoder == encoder reconstruction
 
 
+@pytest.mark.parametrize("content,mode", [("pan15", 1), ("noise", 1), ("flat", 1), ("pan15", 0)])
+def test_stress_contents_vs_oracle(p64, oracle_mod, torch_dev, content, mode):
+    """The bench's stress inputs (+-15-px pans, uniform noise,
+    constant planes) through the split encoder, checked picture by picture
+    against the oracle; the decoder reproduces the encoder's reconstruction."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(os.path.dirname(GOLDEN), "..", "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    torch = torch_dev
+    w, h, S, T = 352, 288, 2, 3
+    nmb, pic = (w // 16) * (h // 16), w * h * 3 // 2
+    frames = bench.make_inputs(torch, p64, content, w, h, 5, S, T)  # [T][S][pic] on the device
+    li = torch.zeros(S * nmb, dtype=torch.uint8, device="cuda")
+    bufs = [torch.zeros(S * pic, dtype=torch.uint8, device="cuda") for _ in range(2)]
+    got = []
+    for t in range(T):
+        ref, rec = bufs[(t + 1) % 2], bufs[t % 2]
+        o = p64.encode_frames(frames[t].reshape(-1), ref, rec, li, width=w, height=h, intra=(t == 0),
+                              quant=8, me_mode=mode, search_limit=31)
+        got.append((host(o.coef), host(o.mb), host(rec).reshape(S, pic)))
+        if t > 0:  # decode the inter picture from its records and levels
+            qmb = torch.full((S * nmb,), 8, dtype=torch.uint8, device="cuda")
+            d = torch.zeros_like(rec)
+            p64.decode_recon(ref, d, o.coef, o.mb, qmb, torch.ones_like(qmb), width=w, height=h)
+            assert torch.equal(d, rec), f"decoder != encoder reconstruction at t{t}"
+    fr = host(frames)
+    for s in range(S):
+        li_o = np.zeros(nmb, np.uint8)
+        ref = None
+        for t in range(T):
+            coef, mb, _, recon = oracle_mod.encode_frame(w, h, fr[t][s], ref, li_o, intra=(t == 0), quant=8,
+                                                         me_mode=mode, search_limit=31)
+            ref = recon
+            np.testing.assert_array_equal(got[t][0][s], coef, err_msg=f"{content} coef s{s} t{t}")
+            np.testing.assert_array_equal(got[t][1][s].view(p64.MB_DTYPE).reshape(nmb), mb,
+                                          err_msg=f"{content} mb s{s} t{t}")
+            np.testing.assert_array_equal(got[t][2][s], recon, err_msg=f"{content} recon s{s} t{t}")
+
+
 def test_intra_refresh_and_override(p64, oracle_mod, torch_dev):
     """LastIntra > 131 forces MTYPE 0 (p64.c:772); -o overrides (p64.c:761-768),
     including MC types without coefficients (4, 7) and MQUANT types."""
