@@ -2228,6 +2228,25 @@ __global__ __launch_bounds__(256) BLK_OCC void k_recon_blk(int w, int h, int64_t
 // rows (16 registers instead of the 24-dword source), the dequantisation and
 // IDCT run unconditionally (an uncoded block's levels were read as zeros and
 // give a zero residual), so the register peak is the IDCT's
+// one reconstructed row: residual v[0..7] (after idct_final) + prediction
+// row pr (packed bytes), clamped to 0..255 (BoundIDctMatrix), packed -- in
+// 16-bit pairs: v_cvt_pk_i16_i32 (saturating), the prediction bytes widened by
+// v_perm, v_pk_add_i16 with clamp, v_sat_pk_u8_i16.  Saturating the residual
+// to +-32767 first changes nothing: the prediction is 0..255.
+__device__ __forceinline__ uint2 recon_row(const int v[8], uint2 pr) {
+  uint32_t o2[4];
+#pragma unroll
+  for (int j = 0; j < 4; j++) {
+    uint32_t rp, sum, sat;
+    asm("v_cvt_pk_i16_i32 %0, %1, %2" : "=v"(rp) : "v"(v[2 * j]), "v"(v[2 * j + 1]));
+    const uint32_t pd = j < 2 ? pr.x : pr.y;
+    const uint32_t pp = __builtin_amdgcn_perm(0u, pd, (j & 1) ? 0x0c030c02u : 0x0c010c00u);
+    asm("v_pk_add_i16 %0, %1, %2 clamp" : "=v"(sum) : "v"(pp), "v"(rp));
+    asm("v_sat_pk_u8_i16 %0, %1" : "=v"(sat) : "v"(sum));
+    o2[j] = sat;
+  }
+  return make_uint2(__builtin_amdgcn_perm(o2[1], o2[0], 0x05040100u), __builtin_amdgcn_perm(o2[3], o2[2], 0x05040100u));
+}
 __device__ __forceinline__ void pred_rows(const PredSrc &P, bool filter, uint2 prow[8]);
 __device__ __forceinline__ void rec_block_pk(int w, int h, int64_t stride, __amdgpu_buffer_rsrc_t rec,
                                              const RecStageA &A, const RecStageB &S) {
@@ -2252,12 +2271,7 @@ __device__ __forceinline__ void rec_block_pk(int w, int h, int64_t stride, __amd
                               : BUF_OOB;
 #pragma unroll
   for (int k = 0; k < 8; k++) {
-#pragma unroll
-    for (int c = 0; c < 8; c++) {
-      const uint32_t pd = c < 4 ? prow[k].x : prow[k].y;
-      v[8 * k + c] = clampi(v[8 * k + c] + (int)((pd >> (8 * (c & 3))) & 255), 0, 255);  // BoundIDctMatrix
-    }
-    const uint2 r = pack8(v + 8 * k);
+    const uint2 r = recon_row(v + 8 * k, prow[k]);  // + prediction, BoundIDctMatrix
     typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
     u32x2 d;
     d[0] = r.x;
@@ -2485,14 +2499,7 @@ __global__ __launch_bounds__(256) INTER_OCC void k_inter_mbg(p64gpu_encode_args 
   iq_idct_cols([&](int e, int f) { return pk2(v[e], v[f]); }, q2, qq, intra, v[0] * 8, v);
   idct_rows(v);
 #pragma unroll
-  for (int k = 0; k < 8; k++) {
-#pragma unroll
-    for (int c = 0; c < 8; c++) {
-      const uint32_t pd = c < 4 ? prow[k].x : prow[k].y;
-      v[8 * k + c] = clampi(v[8 * k + c] + (int)((pd >> (8 * (c & 3))) & 255), 0, 255);
-    }
-    prow[k] = pack8(v + 8 * k);  // now the reconstructed rows
-  }
+  for (int k = 0; k < 8; k++) prow[k] = recon_row(v + 8 * k, prow[k]);  // now the reconstructed rows
   // no levels at all in the MB: the reconstruction is the new prediction
   // (late, so its registers do not overlap the block's)
   if (repred) inter_pred(B, w, h, stride, pos, mt, mvx, mvy, prow);
