@@ -381,6 +381,26 @@ def test_stress_contents_vs_oracle(p64, oracle_mod, torch_dev, content, mode):
             np.testing.assert_array_equal(got[t][2][s], recon, err_msg=f"{content} recon s{s} t{t}")
 
 
+def test_env_switches_same_bytes(torch_dev):
+    """The A/B switches select other kernels, never other
+    bytes: the fused encoder, the one-wave-per-MB intra/decoder kernels and
+    the persistent decoder give the default path's outputs exactly."""
+    import subprocess
+    import sys
+    probe = os.path.join(os.path.dirname(os.path.abspath(__file__)), "switch_probe.py")
+
+    def digest(extra):
+        env = dict(os.environ)
+        env.update(extra)
+        r = subprocess.run([sys.executable, probe], env=env, capture_output=True, text=True, timeout=150)
+        assert r.returncode == 0, r.stderr[-2000:]
+        return r.stdout.strip().splitlines()[-1]
+
+    ref = digest({})
+    for sw in ({"P64GPU_FUSED": "1"}, {"P64GPU_MB_LAYOUT": "1"}, {"P64GPU_RECON_PERSISTENT": "1"}):
+        assert digest(sw) == ref, sw
+
+
 def test_intra_refresh_and_override(p64, oracle_mod, torch_dev):
     """LastIntra > 131 forces MTYPE 0 (p64.c:772); -o overrides (p64.c:761-768),
     including MC types without coefficients (4, 7) and MQUANT types."""
