@@ -172,7 +172,10 @@ int p64gpu_encode_mb_list(const p64gpu_encode_args *args, const int32_t *mb_list
  * (p64DecodeGOB leaves untransmitted MBs untouched); coded_mask
  * ([nmb] bytes, nonzero = MB present in the stream) selects the MBs written.
  * mb[].mtype/cbp/mvx/mvy and quant_mb (UseQuant per MB) come from the host
- * VLC decoder.  Pictures are independent within the call (nframes >= 1). */
+ * VLC decoder.  Pictures are independent within the call (nframes >= 1).
+ * Levels are what H.261 syntax can carry (|AC level| <= 127, intra DC
+ * 1..254): the dequantiser works in packed 16-bit arithmetic, exact for
+ * |level| <= 528. */
 int p64gpu_decode_recon(int width, int height, int nframes, int64_t frame_stride,
                         const uint8_t *ref, uint8_t *recon, const int16_t *coef,
                         const p64_mb_rec *mb, const uint8_t *quant_mb,
