@@ -18,7 +18,13 @@ all: $(LIB) p64_amd/p64gpu oracle
 p64_amd/csrc/synth.o: p64_amd/csrc/synth.c include/p64gpu.h
 	$(CC) -O2 -fPIC -Wall -c $< -o $@
 
-p64_amd/csrc/p64gpu.o: p64_amd/csrc/p64gpu.hip include/p64gpu.h
+KERNEL_DEPS := include/p64gpu.h p64_amd/csrc/common.h p64_amd/csrc/launch.h
+GPU_OBJS := p64_amd/csrc/k_search.o p64_amd/csrc/k_block.o p64_amd/csrc/k_aux.o p64_amd/csrc/p64gpu_abi.o
+
+p64_amd/csrc/k_aux.o: p64_amd/csrc/k_aux.hip $(KERNEL_DEPS) p64_amd/csrc/synth_impl.h
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+p64_amd/csrc/%.o: p64_amd/csrc/%.hip $(KERNEL_DEPS)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
 p64_amd/csrc/p64stream.o: p64_amd/csrc/p64stream.c include/p64stream.h include/p64gpu.h
@@ -34,7 +40,7 @@ p64_amd/csrc/p64prog.o: p64_amd/csrc/p64prog.c include/p64prog.h include/p64gpu.
 p64_amd/csrc/p64vlc.o: p64_amd/csrc/p64vlc.hip include/p64gpu.h include/p64stream.h
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-$(LIB): p64_amd/csrc/p64gpu.o p64_amd/csrc/synth.o p64_amd/csrc/p64stream.o p64_amd/csrc/p64seq.o \
+$(LIB): $(GPU_OBJS) p64_amd/csrc/synth.o p64_amd/csrc/p64stream.o p64_amd/csrc/p64seq.o \
         p64_amd/csrc/p64prog.o p64_amd/csrc/p64vlc.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $^
 
@@ -48,8 +54,10 @@ ref:
 	$(MAKE) -C oracle ref
 
 # ISA listing of the kernels for inspection (not part of the build)
-asm: p64_amd/csrc/p64gpu.hip
-	$(HIPCC) $(HIPFLAGS) --offload-arch=$(ARCH) -S --cuda-device-only -o build/p64gpu.s $<
+asm: p64_amd/csrc/k_search.hip p64_amd/csrc/k_block.hip
+	mkdir -p build
+	for k in k_search k_block; do \
+	  $(HIPCC) $(HIPFLAGS) -S --cuda-device-only -o build/$$k.s p64_amd/csrc/$$k.hip || exit 1; done
 
 clean:
 	rm -f p64_amd/csrc/*.o $(LIB) p64_amd/p64gpu_enc

@@ -74,7 +74,10 @@ SAD_PEAK = 256 * 4 * 16 * 4 * 2.4e9
 #          384 prediction source if not intra, 384 recon write (counted exactly
 #          from the records of each launch, see decode_bytes)
 BYTES_PER_MB = 384 + 384 + 1 + 768 + 384 + 4 + 28 + 1
+READ_BYTES_PER_MB = 384 + 384 + 1
 INTRA_BYTES_PER_MB = 384 + 768 + 384 + 4 + 1
+# rocprofv3 --kernel-trace --stats summary of the default bench command (this round)
+PROFILE_STATS = "profiles/r03_kernel_stats.csv"
 MAX_SLOTS = 256  # distinct input pictures per sequence kept resident (~10 GB at S=256 CIF)
 
 
@@ -223,23 +226,47 @@ def write_y4m(path, frames, w, h):
             f.write(fr.tobytes())
 
 
-def _cpu_run(refbin, env, fmt, procs, nfr, td, args):
-    cmds = [[refbin, fmt, "-y4m", "-a", "0", "-b", str(nfr - 1), "-q", str(args.quant),
-             "-i", str(args.search_limit), os.path.join(td, f"s{k}"), "-z", ".y4m",
-             "-s", os.path.join(td, f"s{k}.p64")] for k in range(procs)]
+def _cpu_procs(cmds, env, stdin_path=None):
+    """Run the commands as concurrent processes; wall seconds."""
     t0 = time.perf_counter()
-    ps = [subprocess.Popen(c, env=env, stdout=subprocess.DEVNULL) for c in cmds]
+    ins = [open(stdin_path) if stdin_path else subprocess.DEVNULL for _ in cmds]
+    ps = [subprocess.Popen(c, env=env, stdin=i, stdout=subprocess.DEVNULL) for c, i in zip(cmds, ins)]
     rc = [p.wait() for p in ps]
     dt = time.perf_counter() - t0
+    for i in ins:
+        if stdin_path:
+            i.close()
     if any(rc):
-        raise RuntimeError(f"reference encoder failed: {rc}")
+        raise RuntimeError(f"reference run failed: {rc}")
     return dt
 
 
-def cpu_baseline(args):
-    """The reference encoder itself (oracle/_ref/p64hook: the unmodified
-    reference objects, FastBME via the MotionEstimation wrap) on y4m files of
-    the same generator: one process, then one per core of the box's share."""
+def _cpu_leg(run, nprocs, units_per_proc, sample, extra=""):
+    """One CPU-baseline leg: `run(k)` -> wall seconds of k concurrent processes,
+    first 1 process, then nprocs (this box's CPU share)."""
+    dt1 = run(1)
+    dtn = run(nprocs) if nprocs > 1 else dt1
+    return {"value": round(nprocs * units_per_proc / dtn, 1), "unit": "macroblocks/s", "cores": nprocs,
+            "kind": "reference",
+            "single_process": {"value": round(units_per_proc / dt1, 1), "cores": 1, "seconds": round(dt1, 2)},
+            "sample": f"{sample}; {nprocs} concurrent processes (this box's CPU share), "
+                      f"{nprocs * units_per_proc} MBs in {dtn:.2f} s wall; single_process: "
+                      f"{units_per_proc} MBs in {dt1:.2f} s{extra}"}
+
+
+def cpu_baselines(args, legs):
+    """The reference itself (oracle/_ref: the unmodified reference objects;
+    p64hook adds only the link-time wraps of oracle/ref_hooks.c), timed on this
+    box's host cores before the GPU is touched, per leg:
+      inter   the encoder on y4m files of the same generator (FastBME SL via
+              P64REF_ME=full, or the shipped StepBME for --mode tss)
+      intra   the encoder under `-o` with program tests/golden/progs/intra_only
+              (MTYPE 0 everywhere, p64.c:761-768) and P64REF_ME=none (no search:
+              the records are unused), i.e. ChenDct + quantisation + VLC + IQ/IDCT
+      decode  `p64 -d` (p64DecodeSequence p64.c:1022) of the reference's own
+              encoding of those files, y4m output
+    Returns {leg: cpu_baseline object}; a leg without a reference path (4CIF:
+    p64.c:1477-1520 and me.c:49-58 stop at CIF) times the clean-room port."""
     import p64_amd  # host-only synth (no GPU use)
 
     w, h = args.width, args.height
@@ -248,44 +275,68 @@ def cpu_baseline(args):
     cores = box_cores()
     procs = max(1, min(args.cpu_procs or cores, cores))
     nfr = args.cpu_frames
-    refbin = os.path.join(REPO, "oracle", "_ref", "p64hook")
-    me = "FastBME SL=%d" % args.search_limit if args.mode == "full" else "StepBME (TSS)"
+    hook = os.path.join(REPO, "oracle", "_ref", "p64hook")
+    out = {}
+    if not fmt or not os.access(hook, os.X_OK):
+        return {leg: cpu_port(args, p64_amd, w, h, nmb) for leg in legs if leg in ("inter", "4cif")}
     with tempfile.TemporaryDirectory() as td:
         for k in range(procs):
             frames = [p64_amd.synth_frame(1 + k, t, w, h) for t in range(nfr)]
             write_y4m(os.path.join(td, f"s{k}.y4m"), frames, w, h)
-        if fmt and os.access(refbin, os.X_OK):
-            env = dict(os.environ)
-            if args.mode == "full":
-                env["P64REF_ME"] = "full"
-            env.pop("P64REF_DUMP", None)
-            dt1 = _cpu_run(refbin, env, fmt, 1, nfr, td, args)
-            dtn = _cpu_run(refbin, env, fmt, procs, nfr, td, args) if procs > 1 else dt1
-            mbs1, mbsn = nfr * nmb, procs * nfr * nmb
-            return {"value": round(mbsn / dtn, 1), "unit": "macroblocks/s", "cores": procs,
-                    "kind": "reference",
-                    "single_process": {"value": round(mbs1 / dt1, 1), "cores": 1,
-                                       "seconds": round(dt1, 2)},
-                    "sample": f"reference encoder (oracle/_ref/p64hook, unmodified reference "
-                              f"objects, {me}), {procs} concurrent processes (this box's CPU "
-                              f"share) each encoding its own {nfr}-picture {w}x{h} y4m sequence "
-                              f"(first picture intra), q={args.quant}; {mbsn} MBs in {dtn:.2f} s "
-                              f"wall; single_process: 1 process, {mbs1} MBs in {dt1:.2f} s; "
-                              f"includes the reference's VLC and file I/O (compare with_vlc)"}
-        # fallback: the clean-room port (single core)
-        sys.path.insert(0, os.path.join(REPO, "oracle"))
-        import oracle
+        env = dict(os.environ)
+        env.pop("P64REF_DUMP", None)
 
-        frames = [p64_amd.synth_frame(1, t, w, h) for t in range(min(nfr, 12))]
-        t0 = time.perf_counter()
-        oracle.encode_sequence(frames, w, h, quant=args.quant,
-                               me_mode=1 if args.mode == "full" else 0,
-                               search_limit=args.search_limit)
-        dt = time.perf_counter() - t0
-        mbs = len(frames) * nmb
-        return {"value": round(mbs / dt, 1), "unit": "macroblocks/s", "cores": 1, "kind": "port",
-                "sample": f"oracle/p64_oracle.c (scalar, no early exit) on {len(frames)} pictures "
-                          f"of one {w}x{h} sequence; {mbs} MBs in {dt:.2f} s"}
+        def enc_cmds(n, extra=()):
+            return [[hook, fmt, "-y4m", "-a", "0", "-b", str(nfr - 1), "-q", str(args.quant),
+                     "-i", str(args.search_limit), *extra, os.path.join(td, f"s{k}"), "-z", ".y4m",
+                     "-s", os.path.join(td, f"s{k}.p64")] for k in range(n)]
+        desc = f"{nfr}-picture {w}x{h} y4m sequence per process (same generator), q={args.quant}"
+        if "inter" in legs or "decode" in legs:
+            me = "FastBME SL=%d" % args.search_limit if args.mode == "full" else "StepBME (TSS)"
+            env_i = dict(env, P64REF_ME="full") if args.mode == "full" else env
+            leg = _cpu_leg(lambda n: _cpu_procs(enc_cmds(n), env_i), procs, nfr * nmb,
+                           f"reference encoder (oracle/_ref/p64hook, {me}), {desc} (first picture intra)",
+                           "; includes the reference's VLC and file I/O (compare with_vlc)")
+            if "inter" in legs:
+                out["inter"] = leg
+        if "decode" in legs:  # the streams the inter leg wrote (s0..s{procs-1}.p64)
+            def dec_cmds(n):
+                return [[hook, "-d", "-y4m", "-s", os.path.join(td, f"s{k}.p64"),
+                         os.path.join(td, f"d{k}")] for k in range(n)]
+            out["decode"] = _cpu_leg(lambda n: _cpu_procs(dec_cmds(n), env), procs, nfr * nmb,
+                                     f"reference decoder (p64 -d, p64DecodeSequence p64.c:1022) of the "
+                                     f"reference's own encoding ({args.mode.upper()}) of a {desc}, "
+                                     f"y4m output", "; includes VLC parsing and file I/O")
+        if "intra" in legs:
+            prog = os.path.join(REPO, "tests", "golden", "progs", "intra_only.prog")
+            env_n = dict(env, P64REF_ME="none")
+            out["intra"] = _cpu_leg(lambda n: _cpu_procs(enc_cmds(n, ("-o",)), env_n, prog), procs,
+                                    nfr * nmb,
+                                    f"reference encoder under -o intra_only.prog (every MB MTYPE 0, "
+                                    f"p64.c:761-768) with the search hooked out (P64REF_ME=none), {desc}",
+                                    "; includes the interpreter call per MB, VLC and file I/O")
+    return out
+
+
+def cpu_port(args, p64_amd, w, h, nmb):
+    """The clean-room port (scalar, one core) where the reference has no path."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle
+
+    n = min(args.cpu_frames, 12 if nmb <= 396 else 4)
+    frames = [p64_amd.synth_frame(1, t, w, h) for t in range(n)]
+    t0 = time.perf_counter()
+    oracle.encode_sequence(frames, w, h, quant=args.quant, me_mode=1 if args.mode == "full" else 0,
+                           search_limit=args.search_limit)
+    dt = time.perf_counter() - t0
+    mbs = len(frames) * nmb
+    note = ("no reference path: the reference cannot encode 4CIF (p64.c:1477-1520 formats; "
+            "me.c:49-58 records sized for CIF), so the clean-room port stands in; "
+            if (w, h) == (704, 576) else "")
+    return {"value": round(mbs / dt, 1), "unit": "macroblocks/s", "cores": 1, "kind": "port",
+            "single_process": {"value": round(mbs / dt, 1), "cores": 1, "seconds": round(dt, 2)},
+            "sample": f"{note}oracle/p64_oracle.c (scalar, exhaustive search, no early exit) on "
+                      f"{len(frames)} pictures of one {w}x{h} sequence; {mbs} MBs in {dt:.2f} s"}
 
 
 # ---------------------------------------------------------------------------
@@ -431,10 +482,12 @@ def main(argv=None):
     if args.dry:
         return dry_main(args, rank, world)
 
-    cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu and args.content == "synth" and \
-            args.config in ("inter", "4cif"):
-        cpu = cpu_baseline(args)
+    cpus = {}
+    if rank == 0 and world == 1 and not args.no_cpu and args.content == "synth":
+        legs = {"inter": ["inter"] + ([] if args.no_extra else ["intra", "decode"]),
+                "4cif": ["inter"], "intra": ["intra"], "decode": ["decode"]}[args.config]
+        cpus = cpu_baselines(args, legs)
+    cpu = cpus.get(args.config if args.config in ("intra", "decode") else "inter")
 
     import numpy as np
     import torch
@@ -558,6 +611,8 @@ def main(argv=None):
                                          nslots)),
                 "decode": strip(run_decode(args, torch, dist, np, p64_amd, world, enc, S, nmb, pic)),
             }
+            for leg in ("intra", "decode"):
+                extra[leg]["cpu_baseline"] = cpus.get(leg)
 
         with_vlc = None
         if not args.no_vlc:
@@ -580,13 +635,13 @@ def main(argv=None):
         pmc_me, pmc_in = load_pmc(args.pmc_json, key + "_me"), load_pmc(args.pmc_json, key + "_inter")
         if os.environ.get("P64GPU_FUSED", "0") in ("", "0"):  # split: k_motion, k_inter_mbg
             kernel = f"{kme} + {kin} (one step)"
-            prof = os.path.join(REPO, "profiles", "r02_kernel_stats.csv")
+            prof = os.path.join(REPO, PROFILE_STATS)
             split = {"dominant": kme,
                      "dominant_note": "k_motion is VALU-bound (roofline_sad, valu_busy); the HBM "
                                       "roofline is taken over the whole step, both kernels",
                      "kernels_us_rocprof": rocprof_avg_us(prof, (kme, kin)) if key.endswith(
                          "S256") else None,
-                     "kernels_us_source": "profiles/r02_kernel_stats.csv (rocprofv3 --kernel-trace "
+                     "kernels_us_source": f"{PROFILE_STATS} (rocprofv3 --kernel-trace "
                                           "--stats of this default bench command)"}
             pmc = None  # (an entry under `key` would be the fused kernel's)
             if pmc_me and pmc_in:
@@ -611,6 +666,14 @@ def main(argv=None):
             "roofline": roofline(mbs_launch * BYTES_PER_MB, kavg, kernel, pmc,
                                  algorithmic_bytes_per_mb=BYTES_PER_MB, timing=timing_note(args, root),
                                  **split),
+            "roofline_hbm_read": {
+                "bound": "hbm", "achieved": round(mbs_launch * READ_BYTES_PER_MB / kavg / 1e9, 1),
+                "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(mbs_launch * READ_BYTES_PER_MB / kavg / 1e9 / HBM_PEAK_GBS, 5),
+                "algorithmic_read_bytes_per_mb": READ_BYTES_PER_MB,
+                "note": "the north_star's HBM-read roofline: the bytes a step must read (current "
+                        "picture 384 + previous reconstruction 384 + LastIntra 1 per MB) over the "
+                        "step time"},
             "roofline_sad": {"bound": "valu", "achieved": round(sad_rate / 1e12, 3),
                              "peak": round(SAD_PEAK / 1e12, 3), "unit": "T byte-absdiff/s",
                              "frac": round(sad_rate / SAD_PEAK, 4), "candidates_per_mb": cand,

@@ -158,6 +158,12 @@ typedef struct {
   p64_me_rec *me;         /* NULL or [nframes][nmb], written (inter only)    */
 } p64gpu_encode_args;
 
+/* Alignment: cur, ref, recon and coef 16 bytes; mb and me 4 bytes (the
+ * kernels use 16-byte vector and dword record accesses); frame_stride a
+ * multiple of 16.  Otherwise P64GPU_E_INVALID.
+ * Inter pictures with args->me == NULL keep their ME records in a library
+ * scratch buffer private to the (device, stream) of the call; see
+ * p64gpu_release_scratch. */
 int p64gpu_encode_frames(const p64gpu_encode_args *args, void *stream);
 /* The same for one picture (args->nframes == 1) restricted to the count
  * macroblocks listed in mb_list (device array of raster indices; entries out
@@ -167,6 +173,13 @@ int p64gpu_encode_frames(const p64gpu_encode_args *args, void *stream);
 int p64gpu_encode_mb_list(const p64gpu_encode_args *args, const int32_t *mb_list, int count,
                           void *stream);
 
+/* Frees the ME-record scratch buffers the library allocated for inter encodes
+ * without args->me (one per device and stream; outgrown ones are kept until
+ * this call, because a HIP graph captured earlier may still reference them).
+ * Call only when no such encode is in flight and no graph that captured one
+ * will be replayed. */
+int p64gpu_release_scratch(void);
+
 /* ---- decoder-side reconstruction (device pointers) ---------------------- */
 /* recon must already hold the previous picture where MBs are not coded
  * (p64DecodeGOB leaves untransmitted MBs untouched); coded_mask
@@ -175,7 +188,7 @@ int p64gpu_encode_mb_list(const p64gpu_encode_args *args, const int32_t *mb_list
  * VLC decoder.  Pictures are independent within the call (nframes >= 1).
  * Levels are what H.261 syntax can carry (|AC level| <= 127, intra DC
  * 1..254): the dequantiser works in packed 16-bit arithmetic, exact for
- * |level| <= 528. */
+ * |level| <= 528.  ref, recon and coef 16-byte aligned, mb 4-byte aligned. */
 int p64gpu_decode_recon(int width, int height, int nframes, int64_t frame_stride,
                         const uint8_t *ref, uint8_t *recon, const int16_t *coef,
                         const p64_mb_rec *mb, const uint8_t *quant_mb,

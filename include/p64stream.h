@@ -103,7 +103,8 @@ void p64s_reader_close(p64s_reader *r);
 /* -c ForceCIF (p64.c:308-310, 1071-1072): decode every picture with CIF
  * geometry and GOB numbering whatever its PTYPE says (a QCIF or NTSC stream
  * lands in the CIF frame; GOBs it does not send stay as they were).  Call
- * right after p64s_reader_open. */
+ * right after p64s_reader_open: once p64s_read_picture has run it fails with
+ * P64GPU_E_INVALID (the caller's arrays are sized for the old geometry). */
 int p64s_reader_force_cif(p64s_reader *r);
 /* Geometry of the stream (from its first picture header, or CIF when forced). */
 int p64s_reader_info(const p64s_reader *r, p64s_picture_info *info);

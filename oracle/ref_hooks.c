@@ -10,6 +10,9 @@
  *       P64REF_ME=full  : run the dormant brute-force FastBME (me.c:187-246)
  *                         for every MB instead of the shipped StepBME (me.c:352),
  *                         i.e. the one-line swap SURVEY.md 0.2 describes.
+ *       P64REF_ME=none  : no search, zero records (CPU-baseline timing of the
+ *                         reference's intra coding under `-o` with a program
+ *                         that keeps every MB intra: the records are unused).
  *       otherwise       : call the real MotionEstimation (TSS, me.c:255-330).
  *       Either way, dump the Me* record arrays (me.c:49-60).
  *   --wrap=WriteMBHeader     (caller p64.c:930 WriteMDU -> marker.c:288)
@@ -84,6 +87,10 @@ void __wrap_MotionEstimation(MEM *pmem, MEM *fmem) {
         MeOVal[MeN] = OMV;
         MeN++;
       }
+  } else if (mode && !strcmp(mode, "none")) {
+    const int n = (fmem->width / 16) * (fmem->height / 16);
+    for (MeN = 0; MeN < n; MeN++)
+      MeX[MeN] = MeY[MeN] = MeVal[MeN] = MeOVal[MeN] = MeVAR[MeN] = MeVAROR[MeN] = MeMWOR[MeN] = 0;
   } else {
     __real_MotionEstimation(pmem, fmem);
   }

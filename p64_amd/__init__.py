@@ -112,6 +112,7 @@ def lib() -> ctypes.CDLL:
     L.p64gpu_motion_estimation.argtypes = [i32, i32, i32, i64, vp, vp, i32, i32, vp, vp]
     L.p64gpu_encode_frames.argtypes = [ctypes.POINTER(EncodeArgs), vp]
     L.p64gpu_decode_recon.argtypes = [i32, i32, i32, i64, vp, vp, vp, vp, vp, vp, vp]
+    L.p64gpu_release_scratch.argtypes = []
     L.p64gpu_encoder_open.argtypes = [i32, i32, i32, i32, i32, ctypes.POINTER(vp)]
     L.p64gpu_encoder_frame.argtypes = [vp, vp, i32, i32, vp, vp, vp, vp, vp]
     L.p64gpu_encoder_close.argtypes = [vp]
@@ -371,6 +372,12 @@ def encode_frames(cur, ref, recon, last_intra, *, width: int, height: int, intra
             _dev_check(out.me, torch.int32, "out.me")
             if out.me.numel() < nmb_all * 7:
                 raise P64GpuError("out.me smaller than nframes x nmb records")
+    # inter pictures always hand the library an ME-record buffer: a torch
+    # allocation is stream- and graph-safe (the caching allocator), so the
+    # library's own per-stream scratch is never needed from Python
+    me = out.me
+    if me is None and not intra:
+        me = torch.empty((nframes, nmb, 7), dtype=torch.int32, device=dev)
     a = EncodeArgs(width=width, height=height, nframes=nframes, intra=int(bool(intra)),
                    quant=quant, me_mode=me_mode, search_limit=search_limit, reserved=0,
                    frame_stride=stride, cur=cur.data_ptr(),
@@ -379,7 +386,7 @@ def encode_frames(cur, ref, recon, last_intra, *, width: int, height: int, intra
                    quant_mb=(quant_mb.data_ptr() if quant_mb is not None else None),
                    mtype_override=(mtype_override.data_ptr() if mtype_override is not None else None),
                    coef=out.coef.data_ptr(), mb=out.mb.data_ptr(),
-                   me=(out.me.data_ptr() if out.me is not None else None))
+                   me=(me.data_ptr() if me is not None else None))
     _check(lib().p64gpu_encode_frames(ctypes.byref(a), _stream(torch)))
     return out
 

@@ -1,0 +1,136 @@
+// k_aux.hip -- batched reference block routines (one thread per 8x8 block,
+// full 32-bit arithmetic for arbitrary int32 input: the p64gpu_block_op API)
+// and the device generator of the synthetic pictures.
+
+#include "common.h"
+#include "launch.h"
+
+#define SYNTH_FN __host__ __device__ static inline
+#include "synth_impl.h"
+
+namespace {
+
+// batched 8x8 block operations (one thread per block; shares the device
+// functions of the fused kernels, full 32-bit arithmetic for arbitrary input)
+__global__ void k_block_op(int op, const int32_t *in, int32_t *out, int64_t nblocks, int dcq,
+                           int acq) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nblocks) return;
+  int m[64], t[64];
+  const int32_t *src = in + i * 64;
+  int32_t *dst = out + i * 64;
+  for (int n = 0; n < 64; n++) m[n] = src[n];
+  switch (op) {
+    case P64GPU_OP_DCT: {
+      int x[8], o[8];
+      for (int c = 0; c < 8; c++) {
+        for (int k = 0; k < 8; k++) x[k] = m[8 * k + c];
+        fwd_col<false>(x, o);
+        for (int k = 0; k < 8; k++) t[8 * k + c] = o[k];
+      }
+      for (int rr = 0; rr < 8; rr++) {
+        for (int k = 0; k < 8; k++) x[k] = t[8 * rr + k];
+        fwd_row<false>(x, o);
+        for (int k = 0; k < 8; k++) m[8 * rr + k] = dct_final(o[k]);
+      }
+      break;
+    }
+    case P64GPU_OP_IDCT: {
+      int x[8], o[8];
+      for (int c = 0; c < 8; c++) {
+        for (int k = 0; k < 8; k++) x[k] = m[8 * k + c] << 2;
+        inv8<false>(x, o);
+        for (int k = 0; k < 8; k++) t[8 * k + c] = o[k];
+      }
+      for (int rr = 0; rr < 8; rr++) {
+        for (int k = 0; k < 8; k++) x[k] = t[8 * rr + k];
+        inv8<false>(x, o);
+        for (int k = 0; k < 8; k++) m[8 * rr + k] = idct_final(o[k]);
+      }
+      break;
+    }
+    case P64GPU_OP_QUANT_INTRA:
+      m[0] = qdc_intra(m[0], dcq);
+      for (int n = 1; n < 64; n++) m[n] = qlevel(m[n], acq);
+      break;
+    case P64GPU_OP_QUANT_INTER:
+      m[0] = qlevel(m[0], dcq);
+      for (int n = 1; n < 64; n++) m[n] = qlevel(m[n], acq);
+      break;
+    case P64GPU_OP_IQUANT_INTRA:
+      m[0] = m[0] * dcq;
+      for (int n = 1; n < 64; n++) m[n] = rlevel<false>(m[n], acq);
+      break;
+    case P64GPU_OP_IQUANT_INTER:
+      m[0] = rlevel<false>(m[0], dcq);
+      for (int n = 1; n < 64; n++) m[n] = rlevel<false>(m[n], acq);
+      break;
+    case P64GPU_OP_BOUND_DCT:
+      m[0] = min(m[0], 2047);
+      for (int n = 1; n < 64; n++) m[n] = clampi(m[n], -1023, 1023);
+      break;
+    case P64GPU_OP_BOUND_IDCT:
+      for (int n = 0; n < 64; n++) m[n] = clampi(m[n], 0, 255);
+      break;
+    case P64GPU_OP_BOUND_QFLAT:
+      m[0] = clampi(m[0], 1, 254);
+      for (int n = 1; n < 64; n++) m[n] = clampi(m[n], -127, 127);
+      break;
+    case P64GPU_OP_BOUND_QUANT:
+      for (int n = 0; n < 64; n++) m[n] = clampi(m[n], -127, 127);
+      break;
+    case P64GPU_OP_ZIGZAG:
+      for (int n = 0; n < 64; n++) t[c_zz.pos[n]] = m[n];
+      for (int n = 0; n < 64; n++) m[n] = t[n];
+      break;
+    case P64GPU_OP_IZIGZAG:
+      for (int n = 0; n < 64; n++) t[n] = m[c_zz.pos[n]];
+      for (int n = 0; n < 64; n++) m[n] = t[n];
+      break;
+    default:
+      break;
+  }
+  for (int n = 0; n < 64; n++) dst[n] = m[n];
+}
+
+// deterministic synthetic pictures on the device (same bytes as synth.c):
+// picture (t, s) = stream seed0+s, frame frame0+t, at out + (t*nseeds+s)*stride
+__global__ __launch_bounds__(256) void k_synth(int w, int h, uint32_t seed0, int nseeds,
+                                               int frame0, int64_t stride, uint8_t *out) {
+  const int pic = blockIdx.y;
+  const int t = pic / nseeds, sidx = pic - t * nseeds;
+  const uint32_t seed = seed0 + (uint32_t)sidx;
+  const int frame = frame0 + t;
+  uint8_t *y = out + (size_t)pic * stride;
+  uint8_t *u = y + (size_t)w * h, *v = u + (size_t)(w / 2) * (h / 2);
+  const int nl = w * h, nc = (w / 2) * (h / 2);
+  for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < nl + nc; k += gridDim.x * blockDim.x) {
+    if (k < nl) {
+      y[k] = p64s_luma(seed, frame, k % w, k / w);
+    } else {
+      const int c = k - nl;
+      p64s_chroma(seed, frame, c % (w / 2), c / (w / 2), &u[c], &v[c]);
+    }
+  }
+}
+
+}  // namespace
+
+namespace p64k {
+
+hipError_t block_op(int op, const int32_t *in, int32_t *out, int64_t nblocks, int dcq, int acq,
+                    hipStream_t st) {
+  const int threads = 64;
+  const int64_t grid = (nblocks + threads - 1) / threads;
+  hipLaunchKernelGGL(k_block_op, dim3((unsigned)grid), dim3(threads), 0, st, op, in, out, nblocks, dcq, acq);
+  return hipGetLastError();
+}
+
+hipError_t synth(int w, int h, uint32_t seed0, int nseeds, int frame0, int nslots, int64_t stride,
+                 uint8_t *out, hipStream_t st) {
+  hipLaunchKernelGGL(k_synth, dim3(64, (unsigned)(nseeds * nslots)), dim3(256), 0, st, w, h, seed0, nseeds,
+                     frame0, stride, out);
+  return hipGetLastError();
+}
+
+}  // namespace p64k

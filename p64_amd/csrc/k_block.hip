@@ -1,0 +1,857 @@
+// k_block.hip -- the block-layout kernels: one LANE per 8x8 block, the whole
+// block in registers, a wave = 10 consecutive macroblocks (lane 6m + b).
+//
+//   k_intra_mbg  intra pictures: ChenDct, CCITTFlatQuantize, zigzag, ICCITT-
+//                FlatQuantize, ChenIDct, reconstruction (p64.c:823-1013)
+//   k_inter_mbg  inter pictures after k_motion: MTYPE decision from the ME
+//                record, prediction + loop filter (io.c:142-496), residual
+//                ChenDct, quantisers, CBP (p64.c:887-908), IQ/IDCT, recon
+//   k_recon_mbg  decoder reconstruction (DecompressMDU p64.c:1179 +
+//                DecodeSaveMDU p64.c:971)
+//
+// No LDS exchange between the transform passes; levels leave through a
+// per-wave LDS staging area as whole 1-KB stores; every load and store is a
+// buffer access whose out-of-range offset replaces a branch.
+
+#include "common.h"
+#include "launch.h"
+
+namespace {
+
+// ---------------------------------------------------------------------------
+// Block layout: one LANE per 8x8 block, the whole block in 64 VGPRs.  For the
+// two HBM-bound paths (intra pictures, decoder reconstruction) this removes
+// every lane exchange: the Chen column and row passes, the zigzag (a register
+// renaming) and the quantisers run in registers, with no LDS and no barrier,
+// and no lane idles (the row layout of k_encode leaves 16 of 64 lanes idle).
+// Thread t of a launch maps to picture t / (6 nmb) and, inside the picture,
+// first the luma blocks in raster order of the 8x8 block grid, then the U and
+// the V blocks in raster order: a wave's 64 lanes read and write 64 adjacent
+// 8-byte row segments (512 contiguous bytes per row instruction), and each
+// lane writes its block's 128 bytes of levels as whole cache lines.
+
+constexpr ZigZag k_zz = make_zigzag();  // compile-time copy for register renaming
+
+// keeps the machine scheduler from interleaving the 8 lines of a pass (it
+// would trade registers for ILP the block layout does not need: other waves
+// hide latency)
+#define SCHED_FENCE() __builtin_amdgcn_sched_barrier(0)
+
+// A wave issues its loads at raised priority, so a freshly launched wave gets
+// its requests out ahead of the older waves' arithmetic
+#define PRIO_HIGH() __builtin_amdgcn_s_setprio(3)
+#define PRIO_LOW() __builtin_amdgcn_s_setprio(0)
+
+struct BlkPos {
+  int fi;     // picture in the launch
+  int mb;     // raster macroblock
+  int b;      // block c = 0..5 of the MB (p64.c:77-79)
+  int plane;  // 0 Y, 1 U, 2 V
+  int x, y;   // block origin in its plane
+};
+// MB-grouped block layout: wave w takes macroblocks 10w .. 10w+9 of the
+// launch, lane 6m + b block b of its m-th MB (lanes 60..63 repeat lane 59).
+// A wave's levels are then 7,680 contiguous bytes and its pixel rows and
+// records contiguous runs per plane: its HBM traffic is a few long runs
+// instead of 64 blocks scattered over a block row.  (MBS_PER_WAVE: common.h)
+__device__ __forceinline__ BlkPos blk_pos_mb(unsigned gmb, int b, int w, int h, const BlkDiv &k) {
+  const int mbw = w >> 4;
+  BlkPos p;
+  p.fi = (int)mdiv(gmb, k.mn, k.sn);
+  p.mb = (int)(gmb - (unsigned)p.fi * (unsigned)(mbw * (h >> 4)));
+  const int mby = (int)mdiv((unsigned)p.mb, k.mw, k.sw), mbx = p.mb - mby * mbw;
+  p.b = b;
+  p.plane = b < 4 ? 0 : b - 3;
+  p.x = b < 4 ? 16 * mbx + 8 * (b & 1) : 8 * mbx;
+  p.y = b < 4 ? 16 * mby + 8 * (b >> 1) : 8 * mby;
+  return p;
+}
+// ChenDct (chendct.c:97-206) on a register block given as its 8 packed pixel
+// rows (or the residual rows - prow), the row pass in packed 16-bit
+// arithmetic: the column pass (scalar) leaves each row as four (column 2j, 2j+1) int16 pairs -- its
+// outputs stay within +-5,800 for pixel or +-255 residual input -- and the
+// row pass runs the butterfly of fwd8 on pairs: v_pk_add/sub/ashr for the
+// sums, and every product pair C_a x + C_b y as ONE v_dot2_i32_i16 with the
+// constant pair as its literal (the two products and their sum exact in
+// 32 bits, the same ms9 rounding after).  Row-pass intermediates stay below
+// 2^15: sums <= 11,600, u = d + r <= 14,000.  Half the registers of the
+// scalar form between the passes.
+typedef short s16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ s16x2 pk16(int lo, int hi) {  // two values that fit int16
+  return __builtin_bit_cast(s16x2, (uint32_t)(lo & 0xffff) | ((uint32_t)hi << 16));
+}
+__device__ __forceinline__ int dot2(s16x2 a, short ca, short cb) {
+  // VOP3P with the constant pair in an SGPR and an inline-0 accumulator: the
+  // builtin becomes v_mov 0 + v_dot2c (6 clocks per wave instead of 4)
+  const uint32_t c = (uint32_t)(uint16_t)ca | ((uint32_t)(uint16_t)cb << 16);
+  int r;
+  asm("v_dot2_i32_i16 %0, %1, %2, 0" : "=v"(r) : "v"(a), "s"(c));
+  return r;
+}
+// row pass of one row given as (x0,x1), (x2,x3), (x4,x5), (x6,x7)
+__device__ __forceinline__ void fwd_row_pk(const s16x2 p[4], int o[8]) {
+  const s16x2 s01 = (p[0] + p[3].yx) >> 1, s23 = (p[1] + p[2].yx) >> 1;  // (s0,s1) (s2,s3)
+  const s16x2 d01 = (p[0] - p[3].yx) >> 1, d23 = (p[1] - p[2].yx) >> 1;  // (d0,d1) (d2,d3)
+  const s16x2 e01 = s01 + s23.yx, e32 = s01 - s23.yx;                    // (e0,e1) (e3,e2)
+  o[0] = ms9(dot2(e01, C1D4, C1D4));
+  o[4] = ms9(dot2(e01, C1D4, -C1D4));
+  o[2] = ms9(dot2(e32, C1D8, C3D8));   // C3D8 e2 + C1D8 e3
+  o[6] = ms9(dot2(e32, C3D8, -C1D8));  // C3D8 e3 - C1D8 e2
+  const s16x2 q = __builtin_shufflevector(d01, d23, 1, 2);   // (d1, d2)
+  const int r1 = ms9(dot2(q, C1D4, C1D4)), r0 = ms9(dot2(q, C1D4, -C1D4));
+  const s16x2 dd = __builtin_shufflevector(d23, d01, 1, 2);  // (d3, d0)
+  const s16x2 rr = pk16(r0, r1);
+  const s16x2 u03 = dd + rr, u12 = dd - rr;                   // (u0,u3) (u1,u2)
+  o[1] = ms9(dot2(u03, C7D16, C1D16));
+  o[7] = ms9(dot2(u03, -C1D16, C7D16));
+  o[3] = ms9(dot2(u12, -C5D16, C3D16));
+  o[5] = ms9(dot2(u12, C3D16, C5D16));
+}
+// (the final rounding dct_final(v) reads the sign of v = X >> 9; hipcc then
+// takes it from X itself and keeps all 64 pre-shift sums alive next to the
+// shifted coefficients until quantisation -- 64 extra VGPRs.  The opaque copy
+// ends X's life at the shift.)
+// RES: the input is the residual rows - prow (both packed pixel rows)
+template <bool RES = false>
+__device__ __forceinline__ void fdct_block_pk(const uint2 rows[8], int v[64], const uint2 *prow = nullptr) {
+  s16x2 p[8][4];  // [row][column pair]
+#pragma unroll
+  for (int c = 0; c < 8; c += 2) {
+    int x[8], y[8], o[8], u[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      const uint32_t wd = c < 4 ? rows[k].x : rows[k].y;
+      x[k] = (int)((wd >> (8 * (c & 3))) & 255);
+      y[k] = (int)((wd >> (8 * ((c + 1) & 3))) & 255);
+      if (RES) {
+        const uint32_t pd = c < 4 ? prow[k].x : prow[k].y;
+        x[k] -= (int)((pd >> (8 * (c & 3))) & 255);
+        y[k] -= (int)((pd >> (8 * ((c + 1) & 3))) & 255);
+      }
+    }
+    fwd_col<true>(x, o);
+    fwd_col<true>(y, u);
+#pragma unroll
+    for (int k = 0; k < 8; k++) p[k][c >> 1] = pk16(o[k], u[k]);
+    SCHED_FENCE();
+  }
+#pragma unroll
+  for (int r = 0; r < 8; r++) {
+    fwd_row_pk(p[r], v + 8 * r);
+#pragma unroll
+    for (int k = 0; k < 8; k++) v[8 * r + k] = opaque(v[8 * r + k]);
+    SCHED_FENCE();
+  }
+}
+
+// 8 IDCT row outputs o (before the final rounding) -> BoundIDct(idct_final(o))
+// as 8 packed bytes.  For o < 0 idct_final(o) <= 0 and (o + 8) >> 4 <= 0 alike,
+// so after the clamp to 0..255 the final rounding's sign term drops out:
+// clamp((o + 8) >> 4).  The clamp + pack is v_cvt_pk_i16_i32 (saturating) +
+// v_sat_pk_u8_i16 per pair and one v_perm per 4 pixels (inline asm: hipcc's
+// own clamp+pack fusion is the miscompiled v_ashr_pk_u8_i32 form, see pack8).
+__device__ __forceinline__ uint32_t sat4(const int x[4]) {
+  uint32_t p01, p23, s01, s23;
+  asm("v_cvt_pk_i16_i32 %0, %1, %2" : "=v"(p01) : "v"(x[0]), "v"(x[1]));
+  asm("v_cvt_pk_i16_i32 %0, %1, %2" : "=v"(p23) : "v"(x[2]), "v"(x[3]));
+  asm("v_sat_pk_u8_i16 %0, %1" : "=v"(s01) : "v"(p01));
+  asm("v_sat_pk_u8_i16 %0, %1" : "=v"(s23) : "v"(p23));
+  return __builtin_amdgcn_perm(s23, s01, 0x05040100u);
+}
+__device__ __forceinline__ uint2 final_clamp_pack8(const int o[8]) {
+  int x[8];
+#pragma unroll
+  for (int k = 0; k < 8; k++) x[k] = (o[k] + 8) >> 4;
+  return make_uint2(sat4(x), sat4(x + 4));
+}
+// ChenIDct (chendct.c:217-375) on a register block: column pass (inputs <<2,
+// folded into the constants), row pass, final rounding
+__device__ __forceinline__ void idct_block(int v[64]) {
+#pragma unroll
+  for (int c = 0; c < 8; c++) {
+    int x[8], o[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) x[k] = v[8 * k + c];
+    inv8<true, 4>(x, o);
+#pragma unroll
+    for (int k = 0; k < 8; k++) v[8 * k + c] = o[k];
+    SCHED_FENCE();
+  }
+#pragma unroll
+  for (int r = 0; r < 8; r++) {
+    int o[8];
+    inv8<true>(v + 8 * r, o);
+#pragma unroll
+    for (int k = 0; k < 8; k++) v[8 * r + k] = idct_final(o[k]);
+    SCHED_FENCE();
+  }
+}
+// ICCITTFlatQuantize + ChenIDct + BoundIDctMatrix of an intra block from its
+// levels (natural order in v; the DC dequantised as DC x 8): the dequantiser
+// runs on natural level pairs (x_k, x_k') of a column in packed 16-bit
+// arithmetic (dequantise_pk; |value| <= 7,905) and the column pass takes
+// every product pair C_a x_k + C_b x_k' as one v_dot2_i32_i16 on those pairs
+// (the <<2 input scale folded into the constants, <= 2,008: products and sums
+// exact in 32 bits); row pass and final stage as idct_block_rec
+__device__ __forceinline__ uint32_t pk2(int lo, int hi) { return __builtin_amdgcn_perm((uint32_t)hi, (uint32_t)lo, 0x05040100u); }
+// the column pass of that from natural level pairs: pair(e, e') returns the
+// levels of natural positions e (low half) and e' (high half) packed; q2/qq
+// packed per lane (0 for a block without coefficients); dcfix: the DC is
+// the intra DC (dequantised as dc8 = DC x 8)
+template <class PairFn>
+__device__ __forceinline__ void iq_idct_cols(PairFn pair, uint32_t q2, uint32_t qq, bool dcfix, int dc8,
+                                             int v[64]) {
+#pragma unroll
+  for (int c = 0; c < 8; c++) {
+    uint32_t p04 = dequantise_pk(pair(c, 32 + c), q2, qq);
+    if (c == 0) p04 = dcfix ? __builtin_amdgcn_perm(p04, (uint32_t)dc8, 0x07060100u) : p04;  // (DC x 8, x4)
+    const s16x2 a04 = __builtin_bit_cast(s16x2, p04);
+    const s16x2 a17 = __builtin_bit_cast(s16x2, dequantise_pk(pair(8 + c, 56 + c), q2, qq));
+    const s16x2 a53 = __builtin_bit_cast(s16x2, dequantise_pk(pair(40 + c, 24 + c), q2, qq));
+    const s16x2 a26 = __builtin_bit_cast(s16x2, dequantise_pk(pair(16 + c, 48 + c), q2, qq));
+    const int p0 = ms9(dot2(a17, 4 * C7D16, -4 * C1D16)), p3 = ms9(dot2(a17, 4 * C1D16, 4 * C7D16));
+    const int p1 = ms9(dot2(a53, 4 * C3D16, -4 * C5D16)), p2 = ms9(dot2(a53, 4 * C5D16, 4 * C3D16));
+    const int q0 = ms9(dot2(a04, 4 * C1D4, 4 * C1D4)), q1 = ms9(dot2(a04, 4 * C1D4, -4 * C1D4));
+    const int q2_ = ms9(dot2(a26, 4 * C3D8, -4 * C1D8)), q3 = ms9(dot2(a26, 4 * C1D8, 4 * C3D8));
+    const int e0 = q0 + q3, e1 = q1 + q2_, e2 = q1 - q2_, e3 = q0 - q3;
+    const int f0 = p0 + p1, f1 = p0 - p1, f2 = p3 - p2, f3 = p3 + p2;
+    const int g1 = ms9(kmul<true>(C1D4, f2 - f1)), g2 = ms9(kmul<true>(C1D4, f2 + f1));
+    v[c] = e0 + f3;
+    v[8 + c] = e1 + g2;
+    v[16 + c] = e2 + g1;
+    v[24 + c] = e3 + f0;
+    v[32 + c] = e3 - f0;
+    v[40 + c] = e2 - g1;
+    v[48 + c] = e1 - g2;
+    v[56 + c] = e0 - f3;
+    SCHED_FENCE();
+  }
+}
+// row pass + idct_final (the residual, to be added to a prediction)
+__device__ __forceinline__ void idct_rows(int v[64]) {
+#pragma unroll
+  for (int r = 0; r < 8; r++) {
+    int o[8];
+    inv8<true>(v + 8 * r, o);
+#pragma unroll
+    for (int k = 0; k < 8; k++) v[8 * r + k] = idct_final(o[k]);
+    SCHED_FENCE();
+  }
+}
+// levels (ints, natural order) in v -> reconstructed rows of an intra block.
+// The row pass takes its product pairs by v_dot2 too: in an intra picture
+// the dequantised inputs are bounded by the quantiser (|AC| <= 1,023 + q <=
+// 1,054, DC <= 254 x 8 = 2,032), which bounds the column-pass outputs by
+// 25,062 (every sign pattern at those magnitudes) < 2^15; a decoder or an
+// inter residual may exceed that (up to 167,072), so only here.
+__device__ __forceinline__ void iq_idct_intra_rec(int v[64], int q, uint2 rec[8]) {
+  const uint32_t q2 = 0x20002u * (uint32_t)q, qq = 0x10001u * (uint32_t)(q - (int)!(q & 1));
+  iq_idct_cols([&](int e, int f) { return pk2(v[e], v[f]); }, q2, qq, true, v[0] * 8, v);
+#pragma unroll
+  for (int r = 0; r < 8; r++) {
+    const int *x = v + 8 * r;
+    const s16x2 a04 = __builtin_bit_cast(s16x2, pk2(x[0], x[4])), a17 = __builtin_bit_cast(s16x2, pk2(x[1], x[7]));
+    const s16x2 a53 = __builtin_bit_cast(s16x2, pk2(x[5], x[3])), a26 = __builtin_bit_cast(s16x2, pk2(x[2], x[6]));
+    const int p0 = ms9(dot2(a17, C7D16, -C1D16)), p3 = ms9(dot2(a17, C1D16, C7D16));
+    const int p1 = ms9(dot2(a53, C3D16, -C5D16)), p2 = ms9(dot2(a53, C5D16, C3D16));
+    const int q0 = ms9(dot2(a04, C1D4, C1D4)), q1 = ms9(dot2(a04, C1D4, -C1D4));
+    const int q2_ = ms9(dot2(a26, C3D8, -C1D8)), q3 = ms9(dot2(a26, C1D8, C3D8));
+    const int e0 = q0 + q3, e1 = q1 + q2_, e2 = q1 - q2_, e3 = q0 - q3;
+    const int f0 = p0 + p1, f1 = p0 - p1, f2 = p3 - p2, f3 = p3 + p2;
+    const int g1 = ms9(kmul<true>(C1D4, f2 - f1)), g2 = ms9(kmul<true>(C1D4, f2 + f1));
+    const int o[8] = {e0 + f3, e1 + g2, e2 + g1, e3 + f0, e3 - f0, e2 - g1, e1 - g2, e0 - f3};
+    rec[r] = final_clamp_pack8(o);
+    SCHED_FENCE();
+  }
+}
+
+// intra picture (p64.c:635, 770-771: every MB is MTYPE 0, CBP 0x3f), block
+// layout: load -> ChenDct -> BoundDct + CCITTFlatQuantize + FlatBound ->
+// zigzag store -> ICCITTFlatQuantize -> ChenIDct -> BoundIDct -> recon.
+// Persistent: a lane walks blocks t, t + stride, ... and issues the loads of
+// its next block before transforming the current one, so every wave keeps
+// HBM reads in flight under its own VALU work (without it the waves of a round
+// load, compute and store in lock step and the memory system idles while they
+// compute).
+// Levels leave through LDS: a lane's block is 128 bytes of levels, and 64
+// lanes storing their own 16-byte pieces touch 64 cache lines per store
+// instruction (measured: the level stores alone took 44 us of the 63 us a
+// load/store-only version of the intra kernel needed).  Each wave writes its
+// 64 blocks' levels to its own LDS slot, then store instruction k writes
+// blocks 8k..8k+7 with 8 lanes per block: whole 128-byte lines.
+constexpr int LVL_STRIDE = 144;  // bytes per lane: 128 + 16 pad, conflict-free ds_write_b128
+constexpr int LVL_WAVE = 64 * LVL_STRIDE;
+__device__ __forceinline__ void put_levels(uint8_t *lds, int lane, int k, uint4 v) {
+  *reinterpret_cast<uint4 *>(lds + lane * LVL_STRIDE + k * 16) = v;
+}
+
+// dword 3 of a raw buffer resource on gfx9-family parts (CDNA): 32-bit data format
+constexpr int BUF_RSRC_W3 = 0x00020000;
+constexpr uint32_t BUF_OOB = 0x80000000u;  // >= every buffer's num_records: loads 0, stores dropped
+
+struct IntraFetch {
+  BlkPos p;
+  uint2 rows[8];  // the block's pixels
+  int q;          // UseQuant
+};
+// QMB: a per-MB UseQuant array is given (else a.quant, uniform, no load)
+template <bool QMB>
+__device__ __forceinline__ IntraFetch intra_fetch_at(const p64gpu_encode_args &a, const BlkPos &pos) {
+  const int w = a.width, h = a.height, nmb = (w >> 4) * (h >> 4);
+  IntraFetch f;
+  f.p = pos;
+  const int pw = f.p.plane ? w >> 1 : w;
+  // buffer loads: 32-bit offsets (a launch covers < 2 GiB of pictures), no
+  // 64-bit address arithmetic per row
+  const __amdgpu_buffer_rsrc_t cur = __builtin_amdgcn_make_buffer_rsrc(
+      (void *)a.cur, (short)0, (int)((int64_t)a.nframes * a.frame_stride), BUF_RSRC_W3);
+  const uint32_t o = (uint32_t)((int64_t)f.p.fi * a.frame_stride) +
+                     (uint32_t)(plane_offset(f.p.plane, w, h) + mul24(f.p.y, pw) + f.p.x);
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    const auto v = __builtin_amdgcn_raw_buffer_load_b64(cur, o + (uint32_t)mul24(k, pw), 0, 0);
+    f.rows[k] = make_uint2(v[0], v[1]);
+  }
+  f.q = QMB ? a.quant_mb[f.p.fi * nmb + f.p.mb] : a.quant;
+  return f;
+}
+// A block's outputs between its computation and its stores
+struct IntraOut {
+  uint2 rec[8];     // reconstructed rows
+  uint32_t rec_off; // byte offset of the block's first row from a.recon
+  int pw;           // its plane's width
+};
+// one block: ChenDct, quantise + zigzag into the LDS staging, dequantise,
+// ChenIDct, reconstruction into `out`
+__device__ __forceinline__ void intra_block(const p64gpu_encode_args &a, const IntraFetch &f, uint8_t *lds,
+                                            int lane, IntraOut &out) {
+  const int w = a.width, h = a.height;
+  const BlkPos &p = f.p;
+  const int q = f.q;
+  // c_qrecip.r[q] computed in place (no dependent table load in the loop)
+  const float rq = __builtin_bit_cast(float, __builtin_bit_cast(uint32_t, 1.0f / (float)(2 * q)) + 1u);
+  const float rqe = (q & 1) ? 0.0f : rq;
+  const int qb = quant_bound(q);
+  int v[64];
+  fdct_block_pk(f.rows, v);
+  // in scan order: quantise (BoundDct + CCITTFlatQuantize + FlatBound), pack
+  // the level pair; 16 bytes of levels at a time into the wave's LDS staging
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    uint32_t pk[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      int l2[2];
+#pragma unroll
+      for (int i = 0; i < 2; i++) {
+        const int e = k_zz.inv[8 * k + 2 * j + i];
+        const bool dc = e == 0;
+        l2[i] = quantise<true, true>(v[e], dc ? -0x7fffffff : -qb, dc ? 2047 : qb, dc, rq, rqe);
+        v[e] = l2[i];  // dequantised in pairs by iq_idct_intra_rec
+      }
+      pk[j] = __builtin_amdgcn_perm((uint32_t)l2[1], (uint32_t)l2[0], 0x05040100u);
+    }
+    put_levels(lds, lane, k, make_uint4(pk[0], pk[1], pk[2], pk[3]));
+    SCHED_FENCE();
+  }
+  iq_idct_intra_rec(v, q, out.rec);  // ICCITTFlatQuantize + ChenIDct + BoundIDctMatrix
+  out.pw = p.plane ? w >> 1 : w;
+  out.rec_off = (uint32_t)((int64_t)p.fi * a.frame_stride) + (uint32_t)plane_offset(p.plane, w, h) +
+                (uint32_t)mul24(p.y, out.pw) + (uint32_t)p.x;
+}
+// the stores of an MB-grouped wave (k_intra_mbg, k_inter_mbg), all buffer
+// stores with out-of-range offsets instead of branches: the wave's levels run
+// (nvalid MBs x 768 bytes at coef + gmb0 x 768) from the LDS staging, the
+// lane's 8 reconstructed rows (rec_off, plane width pw), and from the record
+// lanes (rl) the MB record dword and the LastIntra byte of MB gmb
+__device__ __forceinline__ void mbg_store(const p64gpu_encode_args &a, const uint8_t *lds, int lane,
+                                          unsigned nmbs, unsigned gmb0, uint32_t nvalid, uint32_t rec_off,
+                                          int pw, const uint2 rows[8], bool rl, unsigned gmb, uint32_t mbw,
+                                          uint8_t li) {
+  const int nfr = (int)(nmbs / (unsigned)((a.width >> 4) * (a.height >> 4)));
+  const __amdgpu_buffer_rsrc_t coef =
+      __builtin_amdgcn_make_buffer_rsrc((void *)a.coef, (short)0, (int)(nmbs * 768u), BUF_RSRC_W3);
+  const uint32_t nbytes = nvalid * 768u;
+  __builtin_amdgcn_wave_barrier();
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    const uint32_t ob = 1024u * k + 16u * lane;
+    const uint4 v = *reinterpret_cast<const uint4 *>(lds + (ob >> 7) * LVL_STRIDE + (ob & 127));
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    u32x4 d;
+    d[0] = v.x;
+    d[1] = v.y;
+    d[2] = v.z;
+    d[3] = v.w;
+    __builtin_amdgcn_raw_buffer_store_b128(d, coef, ob < nbytes ? gmb0 * 768u + ob : BUF_OOB, 0, 0);
+  }
+  __builtin_amdgcn_wave_barrier();
+  const __amdgpu_buffer_rsrc_t rec =
+      __builtin_amdgcn_make_buffer_rsrc((void *)a.recon, (short)0, (int)(nfr * a.frame_stride), BUF_RSRC_W3);
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+    u32x2 d;
+    d[0] = rows[k].x;
+    d[1] = rows[k].y;
+    __builtin_amdgcn_raw_buffer_store_b64(d, rec, rec_off + (uint32_t)mul24(k, pw), 0, 0);
+  }
+  const __amdgpu_buffer_rsrc_t mbr =
+      __builtin_amdgcn_make_buffer_rsrc((void *)a.mb, (short)0, (int)(nmbs * 4u), BUF_RSRC_W3);
+  const __amdgpu_buffer_rsrc_t lir =
+      __builtin_amdgcn_make_buffer_rsrc((void *)a.last_intra, (short)0, (int)nmbs, BUF_RSRC_W3);
+  __builtin_amdgcn_raw_buffer_store_b32(mbw, mbr, rl ? 4u * gmb : BUF_OOB, 0, 0);
+  __builtin_amdgcn_raw_buffer_store_b8(li, lir, rl ? gmb : BUF_OOB, 0, 0);
+}
+
+// intra picture, MB-grouped block layout (blk_pos_mb): one wave = 10 MBs, a
+// lane per block; levels leave as one contiguous 7,680-byte run per wave
+template <bool QMB>
+__global__ __launch_bounds__(256) void k_intra_mbg(p64gpu_encode_args a, BlkDiv kd, unsigned nmbs) {
+  __shared__ __align__(16) uint8_t lvl[4 * LVL_WAVE];
+  const int lane = threadIdx.x & 63;
+  uint8_t *lds = lvl + (threadIdx.x >> 6) * LVL_WAVE;
+  const unsigned gmb0 = (blockIdx.x * 4u + (threadIdx.x >> 6)) * MBS_PER_WAVE;
+  if (gmb0 >= nmbs) return;  // whole wave
+  PRIO_HIGH();
+  const int l = min(lane, 6 * MBS_PER_WAVE - 1);
+  const unsigned gmb = min(gmb0 + (unsigned)(l / 6), nmbs - 1);  // tail lanes repeat the last MB
+  const IntraFetch f = intra_fetch_at<QMB>(a, blk_pos_mb(gmb, l % 6, a.width, a.height, kd));
+  PRIO_LOW();
+  IntraOut o;
+  const uint32_t nvalid = min((unsigned)MBS_PER_WAVE, nmbs - gmb0);
+  intra_block(a, f, lds, lane, o);
+  // the MB's record and LastIntra (p64.c:909-910: MTYPE 0, CBP 0x3f, LastIntra
+  // reset) from lane b = 0 of each MB
+  const bool rl = l % 6 == 0 && lane < 6 * MBS_PER_WAVE && gmb0 + (unsigned)(l / 6) < nmbs;
+  mbg_store(a, lds, lane, nmbs, gmb0, nvalid, o.rec_off, o.pw, o.rec, rl, gmb, 0x3f00u, 0);
+}
+// The source of an 8x8 prediction at (x, y) of a plane (any byte alignment):
+// three aligned dwords per row (the third only matters when the row is
+// misaligned)
+struct PredSrc {
+  uint32_t d[8][3];
+  int sh;
+};
+__device__ __forceinline__ void pred_row(const PredSrc &p, int r, int s[8]) {
+  unpack8(align4(p.d[r][1], p.d[r][0], p.sh), align4(p.d[r][2], p.d[r][1], p.sh), s);
+}
+// horizontal taps of the H.261 loop filter: [1 2 1], edge columns x4
+__device__ __forceinline__ void hz_row(const PredSrc &p, int r, int hz[8]) {
+  int s[8];
+  pred_row(p, r, s);
+  hz[0] = s[0] << 2;
+#pragma unroll
+  for (int k = 1; k < 7; k++) hz[k] = s[k - 1] + 2 * s[k] + s[k + 1];
+  hz[7] = s[7] << 2;
+}
+// decoder reconstruction (DecompressMDU p64.c:1179-1237 + DecodeSaveMDU
+// p64.c:971-1013), block layout, persistent, as a two-stage load pipeline:
+// while block i is transformed, the levels and prediction source of block
+// i+1 (whose record arrived during block i-1) and the record of block i+2 are
+// in flight.  Every load is a buffer load: where a block needs no levels
+// (uncoded) or no prediction (intra MB) its offset is out of range, which
+// reads zeros without touching memory -- no branch around any load, so the
+// wait counts stay exact and only the algorithmic bytes move.
+// MBs whose coded_mask is 0 are left alone.  Motion vectors are clamped so a
+// block's source stays inside its plane: a conforming stream never needs it
+// (H.261 vectors point inside the picture; the reader rejects others) and a
+// corrupt one cannot make the kernel read outside the picture.
+// One launch covers at most 2 GiB of levels and of pictures (the host splits
+// larger batches), so every offset fits the 32-bit buffer range.
+
+struct RecBufs {
+  __amdgpu_buffer_rsrc_t ref, coef, mb, q, mask;
+};
+struct RecStageA {  // the block and its MB's record
+  BlkPos p;
+  uint32_t m;  // p64_mb_rec as one dword
+  int q, coded;
+};
+struct RecStageB {  // what the block's reconstruction reads
+  uint32_t lq[8][4];  // zigzag levels, 8 x 16 bytes (zeros if not coded)
+  PredSrc pred;       // prediction source (zeros if intra)
+  bool ck, inter, filter;
+};
+// does block p.b of the MB carry levels (MTYPE with TCOEFF, CBP bit; p64.c:1200)
+__device__ __forceinline__ bool rec_block_coded(const RecStageA &A) {
+  const int mt = (int)(int8_t)(A.m & 0xff);
+  const int cbp = mt_cbp(mt) ? (int)((A.m >> 8) & 0x3f) : 0x3f;
+  return A.coded && mt_tcoeff(mt) && ((cbp >> (5 - A.p.b)) & 1);
+}
+// LEVELS: load the block's levels into S.lq (else the caller fills them)
+template <bool LEVELS = true>
+__device__ __forceinline__ RecStageB rec_stage_b(const RecBufs &B, int w, int h, int64_t stride,
+                                                 const RecStageA &A) {
+  const int nmb = (w >> 4) * (h >> 4);
+  const BlkPos &p = A.p;
+  const int mt = (int)(int8_t)(A.m & 0xff);
+  RecStageB S;
+  S.ck = rec_block_coded(A);
+  S.inter = A.coded && !mt_intra(mt);
+  S.filter = mt_filter(mt);
+  const int pw = p.plane ? w >> 1 : w, ph = p.plane ? h >> 1 : h;
+  int dx = 0, dy = 0;
+  if (mt_mf(mt)) {  // chroma MV/2 with C truncation (io.c:268-270)
+    const int mvx = (int)(int8_t)((A.m >> 16) & 0xff), mvy = (int)(int8_t)(A.m >> 24);
+    dx = p.plane ? mvx / 2 : mvx;
+    dy = p.plane ? mvy / 2 : mvy;
+  }
+  const int sx = clampi(p.x + dx, 0, pw - 8), sy = clampi(p.y + dy, 0, ph - 8);
+  S.pred.sh = sx & 3;
+  const uint32_t po = S.inter ? (uint32_t)((int64_t)p.fi * stride) + (uint32_t)plane_offset(p.plane, w, h) +
+                                    (uint32_t)(mul24(sy, pw) + (sx & ~3))
+                              : BUF_OOB;
+  // the third dword only when the row is misaligned (then it lies inside the
+  // row: sx <= pw - 9); an aligned row at the plane's end would reach past it
+  const uint32_t po3 = S.pred.sh ? po + 8 : BUF_OOB;
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    const auto v = __builtin_amdgcn_raw_buffer_load_b64(B.ref, po + (uint32_t)mul24(k, pw), 0, 0);
+    S.pred.d[k][0] = v[0];
+    S.pred.d[k][1] = v[1];
+    S.pred.d[k][2] = __builtin_amdgcn_raw_buffer_load_b32(B.ref, po3 + (uint32_t)mul24(k, pw), 0, 0);
+  }
+  // the levels after the prediction source: the prediction is formed first,
+  // and wait counts are in issue order
+  if (LEVELS) {
+    const uint32_t co = S.ck ? (uint32_t)(((p.fi * nmb + p.mb) * 6 + p.b) * 128) : BUF_OOB;
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      const auto v = __builtin_amdgcn_raw_buffer_load_b128(B.coef, co + 16 * k, 0, 0);
+      S.lq[k][0] = v[0];
+      S.lq[k][1] = v[1];
+      S.lq[k][2] = v[2];
+      S.lq[k][3] = v[3];
+    }
+  }
+  return S;
+}
+// pred_rows (below) + dequantise + ChenIDct + reconstruction for the
+// non-persistent decoder: the prediction is formed first and kept as 8 packed
+// rows (16 registers instead of the 24-dword source), the dequantisation and
+// IDCT run unconditionally (an uncoded block's levels were read as zeros and
+// give a zero residual), so the register peak is the IDCT's
+// one reconstructed row: residual v[0..7] (after idct_final) + prediction
+// row pr (packed bytes), clamped to 0..255 (BoundIDctMatrix), packed -- in
+// 16-bit pairs: v_cvt_pk_i16_i32 (saturating), the prediction bytes widened by
+// v_perm, v_pk_add_i16 with clamp, v_sat_pk_u8_i16.  Saturating the residual
+// to +-32767 first changes nothing: the prediction is 0..255.
+__device__ __forceinline__ uint2 recon_row(const int v[8], uint2 pr) {
+  uint32_t o2[4];
+#pragma unroll
+  for (int j = 0; j < 4; j++) {
+    uint32_t rp, sum, sat;
+    asm("v_cvt_pk_i16_i32 %0, %1, %2" : "=v"(rp) : "v"(v[2 * j]), "v"(v[2 * j + 1]));
+    const uint32_t pd = j < 2 ? pr.x : pr.y;
+    const uint32_t pp = __builtin_amdgcn_perm(0u, pd, (j & 1) ? 0x0c030c02u : 0x0c010c00u);
+    asm("v_pk_add_i16 %0, %1, %2 clamp" : "=v"(sum) : "v"(pp), "v"(rp));
+    asm("v_sat_pk_u8_i16 %0, %1" : "=v"(sat) : "v"(sum));
+    o2[j] = sat;
+  }
+  return make_uint2(__builtin_amdgcn_perm(o2[1], o2[0], 0x05040100u), __builtin_amdgcn_perm(o2[3], o2[2], 0x05040100u));
+}
+__device__ __forceinline__ void pred_rows(const PredSrc &P, bool filter, uint2 prow[8]);
+__device__ __forceinline__ void rec_block_pk(int w, int h, int64_t stride, __amdgpu_buffer_rsrc_t rec,
+                                             const RecStageA &A, const RecStageB &S) {
+  const BlkPos &p = A.p;
+  uint2 prow[8];
+  pred_rows(S.pred, S.filter && S.inter, prow);  // zeros for intra (source not loaded)
+  int v[64];
+  const int q = A.q;
+  const uint32_t q2 = 0x20002u * (uint32_t)q, qq = 0x10001u * (uint32_t)(q - (int)!(q & 1));
+  // natural level pairs straight from the packed zigzag words (one v_perm each)
+  auto pair = [&](int e, int f) {
+    const int s1 = k_zz.pos[e], s2 = k_zz.pos[f];
+    const uint32_t sel = ((s1 & 1) ? 0x0302u : 0x0100u) | (((s2 & 1) ? 0x0706u : 0x0504u) << 16);
+    return __builtin_amdgcn_perm(S.lq[s2 >> 3][(s2 >> 1) & 3], S.lq[s1 >> 3][(s1 >> 1) & 3], sel);
+  };
+  iq_idct_cols(pair, q2, qq, !S.inter, (int)(int16_t)(S.lq[0][0] & 0xffff) * 8, v);
+  idct_rows(v);
+  const int pw = p.plane ? w >> 1 : w;
+  const uint32_t ro = A.coded ? (uint32_t)((int64_t)p.fi * stride) + (uint32_t)plane_offset(p.plane, w, h) +
+                                    (uint32_t)(mul24(p.y, pw) + p.x)
+                              : BUF_OOB;
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    const uint2 r = recon_row(v + 8 * k, prow[k]);  // + prediction, BoundIDctMatrix
+    typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+    u32x2 d;
+    d[0] = r.x;
+    d[1] = r.y;
+    __builtin_amdgcn_raw_buffer_store_b64(d, rec, ro + (uint32_t)mul24(k, pw), 0, 0);
+  }
+}
+// occupancy targets: k_inter_mbg 4 waves per SIMD (<= 128 VGPRs), the decoder
+// 3 (its 139 VGPRs spill at 4)
+#define INTER_OCC __attribute__((amdgpu_waves_per_eu(4)))
+#define RECON_OCC __attribute__((amdgpu_waves_per_eu(3)))
+// decoder reconstruction, MB-grouped block layout (blk_pos_mb), one block per
+// lane and no loop: 10 MBs per wave, each lane loads its MB's record, then its
+// levels and prediction, reconstructs and stores.  Without the persistent
+// kernel's in-flight registers it fits 3 waves per SIMD (139 VGPRs), and those
+// waves hide each other's two dependent load latencies (measured faster than
+// k_recon_blk, whose 237 VGPRs allow 2).  Lanes past the batch (and lanes
+// 60..63) get coded = 0: every load and store of theirs is out of range.
+__global__ __launch_bounds__(256) RECON_OCC void k_recon_mbg(int w, int h, int64_t stride, const uint8_t *refp,
+                                                           uint8_t *recp, const int16_t *coef,
+                                                           const p64_mb_rec *mbr, const uint8_t *quant_mb,
+                                                           const uint8_t *coded_mask, BlkDiv kd, unsigned nmbs) {
+  const int lane = threadIdx.x & 63;
+  const unsigned gmb0 = (blockIdx.x * 4u + (threadIdx.x >> 6)) * MBS_PER_WAVE;
+  if (gmb0 >= nmbs) return;  // whole wave
+  const int nmb = (w >> 4) * (h >> 4), nfr = (int)(nmbs / (unsigned)nmb);
+  RecBufs B;
+  B.ref = __builtin_amdgcn_make_buffer_rsrc((void *)refp, (short)0, (int)(nfr * stride), BUF_RSRC_W3);
+  B.coef = __builtin_amdgcn_make_buffer_rsrc((void *)coef, (short)0, nfr * nmb * 768, BUF_RSRC_W3);
+  B.mb = __builtin_amdgcn_make_buffer_rsrc((void *)mbr, (short)0, nfr * nmb * 4, BUF_RSRC_W3);
+  B.q = __builtin_amdgcn_make_buffer_rsrc((void *)quant_mb, (short)0, nfr * nmb, BUF_RSRC_W3);
+  B.mask = __builtin_amdgcn_make_buffer_rsrc((void *)coded_mask, (short)0, nfr * nmb, BUF_RSRC_W3);
+  const __amdgpu_buffer_rsrc_t rec =
+      __builtin_amdgcn_make_buffer_rsrc((void *)recp, (short)0, (int)(nfr * stride), BUF_RSRC_W3);
+  PRIO_HIGH();
+  const int l = min(lane, 6 * MBS_PER_WAVE - 1);
+  const unsigned g = gmb0 + (unsigned)(l / 6);
+  const bool valid = lane < 6 * MBS_PER_WAVE && g < nmbs;
+  const unsigned gmb = min(g, nmbs - 1);
+  RecStageA A;
+  A.p = blk_pos_mb(gmb, l % 6, w, h, kd);
+  A.m = __builtin_amdgcn_raw_buffer_load_b32(B.mb, 4 * gmb, 0, 0);
+  A.q = __builtin_amdgcn_raw_buffer_load_b8(B.q, gmb, 0, 0);
+  A.coded = __builtin_amdgcn_raw_buffer_load_b8(B.mask, valid ? gmb : BUF_OOB, 0, 0);
+  const RecStageB S = rec_stage_b(B, w, h, stride, A);
+  PRIO_LOW();
+  rec_block_pk(w, h, stride, rec, A, S);
+}
+
+// ---------------------------------------------------------------------------
+// inter picture, second stage of the split encoder: k_motion writes every
+// MB's ME record, then this block-layout kernel does the rest of
+// ReadCompressMDU / CompressMDU (p64.c:734-1013) with one lane per 8x8 block
+// (10 MBs per wave, lane = 6m + b, as k_intra_mbg): MTYPE decision from the
+// ME record, prediction (MC, loop filter), ChenDct of the residual,
+// quantisation, the CBP decision across the MB's six lanes (wave ballots),
+// zigzag levels through the LDS staging, dequantisation, ChenIDct and the
+// reconstruction.  The fused one-wave-per-MB k_encode spends 40% of its time
+// in this half with 48 of 64 lanes busy on LDS-exchanged row passes; here
+// every lane holds its block in registers.
+__device__ __forceinline__ void pred_rows(const PredSrc &P, bool filter, uint2 prow[8]);
+struct InterMe {  // the fields of p64_me_rec the decision needs
+  int mx, my, sad, sad0, var, varor;
+};
+// prediction of the lane's block for MTYPE mt / vector (mvx, mvy), packed rows
+__device__ __forceinline__ void inter_pred(const RecBufs &B, int w, int h, int64_t stride, const BlkPos &p,
+                                           int mt, int mvx, int mvy, uint2 prow[8]) {
+  RecStageA A;
+  A.p = p;
+  A.m = (uint32_t)(mt & 0xff) | ((uint32_t)(mvx & 0xff) << 16) | ((uint32_t)(mvy & 0xff) << 24);
+  A.q = 0;
+  A.coded = 1;
+  const RecStageB S = rec_stage_b<false>(B, w, h, stride, A);  // source OOB (zeros) if intra
+  PRIO_LOW();  // the loads are out: the loop filter at normal priority
+  pred_rows(S.pred, S.filter, prow);
+}
+// the prediction as packed rows (all zero when the source was not loaded)
+__device__ __forceinline__ void pred_rows(const PredSrc &P, bool filter, uint2 prow[8]) {
+  if (filter) {  // add_pred's loop filter, one packed row at a time
+    int hp[8], hc[8], hn[8];
+    hz_row(P, 0, hc);
+    hz_row(P, 1, hn);
+#pragma unroll
+    for (int r = 0; r < 8; r++) {
+      int o[8];
+#pragma unroll
+      for (int k = 0; k < 8; k++)
+        o[k] = (r == 0 || r == 7) ? ((hc[k] << 2) + 8) >> 4 : (hp[k] + 2 * hc[k] + hn[k] + 8) >> 4;
+      prow[r] = pack8(o);
+#pragma unroll
+      for (int k = 0; k < 8; k++) {
+        hp[k] = hc[k];
+        hc[k] = hn[k];
+      }
+      if (r + 2 < 8) hz_row(P, r + 2, hn);
+    }
+  } else {  // the source rows as they are
+#pragma unroll
+    for (int r = 0; r < 8; r++)
+      prow[r] = make_uint2(align4(P.d[r][1], P.d[r][0], P.sh), align4(P.d[r][2], P.d[r][1], P.sh));
+  }
+}
+template <bool QMB>
+__global__ __launch_bounds__(256) INTER_OCC void k_inter_mbg(p64gpu_encode_args a, BlkDiv kd, unsigned nmbs,
+                                                             const p64_me_rec *me) {
+  __shared__ __align__(16) uint8_t lvl[4 * LVL_WAVE];
+  const int lane = threadIdx.x & 63;
+  uint8_t *lds = lvl + (threadIdx.x >> 6) * LVL_WAVE;
+  const unsigned gmb0 = (blockIdx.x * 4u + (threadIdx.x >> 6)) * MBS_PER_WAVE;
+  if (gmb0 >= nmbs) return;  // whole wave
+  const int w = a.width, h = a.height, nmb = (w >> 4) * (h >> 4), nfr = (int)(nmbs / (unsigned)nmb);
+  const int64_t stride = a.frame_stride;
+  RecBufs B;
+  B.ref = __builtin_amdgcn_make_buffer_rsrc((void *)a.ref, (short)0, (int)(nfr * stride), BUF_RSRC_W3);
+  PRIO_HIGH();
+  const int l = min(lane, 6 * MBS_PER_WAVE - 1), b = l % 6;
+  const unsigned gmb = min(gmb0 + (unsigned)(l / 6), nmbs - 1);  // tail lanes repeat the last MB
+  const BlkPos pos = blk_pos_mb(gmb, b, w, h, kd);
+  // the ME record, LastIntra and override first: the prediction loads wait
+  // on them (wait counts are in issue order), the current rows only later
+  const __amdgpu_buffer_rsrc_t mer =
+      __builtin_amdgcn_make_buffer_rsrc((void *)me, (short)0, (int)(nmbs * sizeof(p64_me_rec)), BUF_RSRC_W3);
+  const uint32_t mo = gmb * (uint32_t)sizeof(p64_me_rec);
+  InterMe m;
+  m.mx = (int)__builtin_amdgcn_raw_buffer_load_b32(mer, mo + 0, 0, 0);
+  m.my = (int)__builtin_amdgcn_raw_buffer_load_b32(mer, mo + 4, 0, 0);
+  m.sad = (int)__builtin_amdgcn_raw_buffer_load_b32(mer, mo + 8, 0, 0);
+  m.sad0 = (int)__builtin_amdgcn_raw_buffer_load_b32(mer, mo + 12, 0, 0);
+  m.var = (int)__builtin_amdgcn_raw_buffer_load_b32(mer, mo + 16, 0, 0);
+  m.varor = (int)__builtin_amdgcn_raw_buffer_load_b32(mer, mo + 20, 0, 0);
+  // LastIntra and the -o override by buffer loads (an absent override array
+  // reads as out of range: no branch around a load)
+  const __amdgpu_buffer_rsrc_t lir =
+      __builtin_amdgcn_make_buffer_rsrc((void *)a.last_intra, (short)0, (int)nmbs, BUF_RSRC_W3);
+  const __amdgpu_buffer_rsrc_t ovr = __builtin_amdgcn_make_buffer_rsrc(
+      (void *)a.mtype_override, (short)0, a.mtype_override ? (int)nmbs : 0, BUF_RSRC_W3);
+  const int li = __builtin_amdgcn_raw_buffer_load_b8(lir, gmb, 0, 0);
+  const int ovl = (int)(int8_t)__builtin_amdgcn_raw_buffer_load_b8(ovr, a.mtype_override ? gmb : BUF_OOB, 0, 0);
+  const int ov = a.mtype_override ? ovl : -1;
+  const IntraFetch f = intra_fetch_at<QMB>(a, pos);  // current rows, q
+
+  // MTYPE (p64.c:734-772): the decision, the -o override, the intra refresh
+  MeOut mo_;
+  mo_.mx = m.mx;
+  mo_.my = m.my;
+  mo_.sad = m.sad;
+  mo_.sad0 = m.sad0;
+  mo_.var = m.var;
+  mo_.varor = m.varor;
+  mo_.mwor = 0;
+  int mt = decide_mtype(mo_);
+  if (ov >= 0) mt = ov;
+  if (li > 131) mt = 0;
+  const int mvx = m.mx, mvy = m.my;
+  uint2 prow[8];
+  inter_pred(B, w, h, stride, pos, mt, mvx, mvy, prow);  // (drops the priority)
+
+  const bool intra = mt_intra(mt), tc = mt_tcoeff(mt);
+  const int q = f.q;
+  const float rq = __builtin_bit_cast(float, __builtin_bit_cast(uint32_t, 1.0f / (float)(2 * q)) + 1u);
+  const float rqe = (q & 1) ? 0.0f : rq;
+  const int qe = (int)!(q & 1), qbr = 256 * q - 1 - qe, qb = min(1023, qbr);
+  // levels & tcm: 0 when the MB type carries no coefficients (through an
+  // opaque mask: as a select hipcc branches around every quantisation)
+  const int tcm = opaque(tc ? -1 : 0);
+  int v[64];
+  fdct_block_pk<true>(f.rows, v, prow);
+  // quantise in scan order into the LDS staging (levels of a block whose MB
+  // type carries no coefficients are 0); Σ l^2 for the CBP decision:
+  // Σ|l| > 1 <=> Σ l^2 > 1 and Σ|l| > 0 <=> Σ l^2 > 0 for integers
+  int ss = 0;
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    uint32_t pk[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      int l2[2];
+#pragma unroll
+      for (int i = 0; i < 2; i++) {
+        const int e = k_zz.inv[8 * k + 2 * j + i];
+        if (e == 0) {  // DC: intra (DC +- 4) / 8 in 1..254, inter as AC with DC bounds
+          const int c = dct_final(v[0]);
+          int vi;
+          asm("v_med3_i32 %0, %1, %2, %3" : "=v"(vi) : "v"(c), "v"(-qbr), "v"(min(2047, qbr)));
+          const float x = (float)vi;
+          const int li_ = (int)__builtin_fmaf(x, rq, __builtin_copysignf(rqe, x));
+          const int ld = clampi(dct_final(min(c, 2047)), 1, 254);
+          l2[i] = intra ? ld : li_;
+        } else {
+          l2[i] = quantise<false, true>(v[e], -qb, qb, false, rq, rqe);
+        }
+        l2[i] &= tcm;
+      }
+      pk[j] = __builtin_amdgcn_perm((uint32_t)l2[1], (uint32_t)l2[0], 0x05040100u);
+      ss = __builtin_amdgcn_sdot2(__builtin_bit_cast(s16x2, pk[j]), __builtin_bit_cast(s16x2, pk[j]), ss, false);
+      v[k_zz.inv[8 * k + 2 * j]] = l2[0];
+      v[k_zz.inv[8 * k + 2 * j + 1]] = l2[1];
+    }
+    put_levels(lds, lane, k, make_uint4(pk[0], pk[1], pk[2], pk[3]));
+    SCHED_FENCE();
+  }
+  // CBP (p64.c:887-908): block coded if Σ|l| > 1; none such -> the first
+  // block with a nonzero level; no nonzero level at all -> MC without
+  // coefficients (MTYPE 4 / 7), vector kept, CBP 0x3f
+  const int sh = 6 * (l / 6);
+  const uint32_t big = (uint32_t)(__ballot(ss > 1) >> sh) & 63u, any = (uint32_t)(__ballot(ss > 0) >> sh) & 63u;
+  int cbp = 0x3f;
+  bool repred = false;  // 2/3 -> 4 switches from the zero vector to the ME vector
+  if (mt_cbp(mt)) {
+    if (any == 0) {
+      repred = !mt_mf(mt);
+      mt = mt_filter(mt) ? 7 : 4;
+    } else {
+      const uint32_t sel = big ? big : (any & (0u - any));  // lane-bit b = block b
+      cbp = (int)(__builtin_bitreverse32(sel) >> 26);           // block b -> bit 5 - b
+    }
+  }
+  const bool ck = mt_tcoeff(mt) && ((cbp >> (5 - b)) & 1);
+  const uint32_t q2 = ck ? 0x20002u * (uint32_t)q : 0u, qq = ck ? 0x10001u * (uint32_t)(q - qe) : 0u;
+  // IQ in level pairs + ChenIDct (all-zero levels / q2 = qq = 0 give zero)
+  iq_idct_cols([&](int e, int f) { return pk2(v[e], v[f]); }, q2, qq, intra, v[0] * 8, v);
+  idct_rows(v);
+#pragma unroll
+  for (int k = 0; k < 8; k++) prow[k] = recon_row(v + 8 * k, prow[k]);  // now the reconstructed rows
+  // no levels at all in the MB: the reconstruction is the new prediction
+  // (late, so its registers do not overlap the block's)
+  if (repred) inter_pred(B, w, h, stride, pos, mt, mvx, mvy, prow);
+  const uint32_t nvalid = min((unsigned)MBS_PER_WAVE, nmbs - gmb0);
+  const int pw = pos.plane ? w >> 1 : w;
+  const uint32_t ro = (uint32_t)((int64_t)pos.fi * stride) + (uint32_t)plane_offset(pos.plane, w, h) +
+                      (uint32_t)mul24(pos.y, pw) + (uint32_t)pos.x;
+  // p64.c:909-910: the record (transmitted vector only for MC types) and LastIntra
+  const bool rl = b == 0 && lane < 6 * MBS_PER_WAVE && gmb0 + (unsigned)(l / 6) < nmbs;
+  const uint32_t mbw = (uint32_t)(mt & 0xff) | ((uint32_t)(cbp & 0xff) << 8) |
+                       (mt_mf(mt) ? ((uint32_t)(mvx & 0xff) << 16) | ((uint32_t)(mvy & 0xff) << 24) : 0u);
+  mbg_store(a, lds, lane, nmbs, gmb0, nvalid, ro, pw, prow, rl, gmb, mbw,
+            mt_intra(mt) ? (uint8_t)0 : (uint8_t)(li + 1));
+}
+
+}  // namespace
+
+namespace p64k {
+
+static unsigned mbg_workgroups(unsigned nmbs) {
+  const unsigned waves = (nmbs + MBS_PER_WAVE - 1) / MBS_PER_WAVE;
+  return (waves + 3) / 4;
+}
+
+hipError_t intra_mbg(const p64gpu_encode_args &a, hipStream_t st) {
+  const unsigned nm = (unsigned)((int64_t)a.nframes * (a.width / 16) * (a.height / 16));
+  if (a.quant_mb)
+    hipLaunchKernelGGL(k_intra_mbg<true>, dim3(mbg_workgroups(nm)), dim3(256), 0, st, a,
+                       blk_div(a.width, a.height), nm);
+  else
+    hipLaunchKernelGGL(k_intra_mbg<false>, dim3(mbg_workgroups(nm)), dim3(256), 0, st, a,
+                       blk_div(a.width, a.height), nm);
+  return hipGetLastError();
+}
+
+hipError_t inter_mbg(const p64gpu_encode_args &a, const p64_me_rec *me, hipStream_t st) {
+  const unsigned nm = (unsigned)((int64_t)a.nframes * (a.width / 16) * (a.height / 16));
+  if (a.quant_mb)
+    hipLaunchKernelGGL(k_inter_mbg<true>, dim3(mbg_workgroups(nm)), dim3(256), 0, st, a,
+                       blk_div(a.width, a.height), nm, me);
+  else
+    hipLaunchKernelGGL(k_inter_mbg<false>, dim3(mbg_workgroups(nm)), dim3(256), 0, st, a,
+                       blk_div(a.width, a.height), nm, me);
+  return hipGetLastError();
+}
+
+hipError_t recon_mbg(int w, int h, int nframes, int64_t stride, const uint8_t *ref, uint8_t *recon,
+                     const int16_t *coef, const p64_mb_rec *mb, const uint8_t *quant_mb,
+                     const uint8_t *coded_mask, hipStream_t st) {
+  const unsigned nm = (unsigned)((int64_t)nframes * (w / 16) * (h / 16));
+  hipLaunchKernelGGL(k_recon_mbg, dim3(mbg_workgroups(nm)), dim3(256), 0, st, w, h, stride, ref, recon,
+                     coef, mb, quant_mb, coded_mask, blk_div(w, h), nm);
+  return hipGetLastError();
+}
+
+}  // namespace p64k

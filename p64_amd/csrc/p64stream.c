@@ -529,6 +529,7 @@ struct p64s_reader {
   int ended, end_tr, last_tr;
   int mt, mvx, mvy; /* ReadMBHeader's persistent MType / MVDH / MVDV */
   int force_cif;    /* -c: CIF geometry whatever PTYPE says (p64.c:1071-1072) */
+  int started;      /* p64s_read_picture has been called */
 };
 
 /* n <= 25 bits at the current position without consuming them; bytes past
@@ -599,6 +600,9 @@ void p64s_reader_close(p64s_reader *r) { free(r); }
 
 int p64s_reader_force_cif(p64s_reader *r) {
   if (!r) return fail(P64GPU_E_INVALID, "reader_force_cif: NULL reader");
+  /* the caller sized its arrays from the geometry reader_info gave: changing
+   * it once pictures are being read would overrun them */
+  if (r->started) return fail(P64GPU_E_INVALID, "reader_force_cif: pictures already read");
   r->force_cif = 1;
   r->first.format = P64S_CIF;
   p64s_geometry(P64S_CIF, &r->first.width, &r->first.height, &r->first.ngob);
@@ -660,6 +664,7 @@ int p64s_read_picture(p64s_reader *r, p64s_picture_info *info, p64_mb_rec *mb, u
                       uint8_t *coded, int16_t *coef) {
   if (!r || !info || !mb || !quant_mb || !coded || !coef)
     return fail(P64GPU_E_INVALID, "read_picture: NULL argument");
+  r->started = 1;
   p64s_picture_info pi = r->first;
   const int nmb = pi.ngob * 33;
   memset(mb, 0, (size_t)nmb * sizeof *mb);

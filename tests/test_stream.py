@@ -322,3 +322,20 @@ def test_decode_short_p64_matches_reference_md5(p64, st, oracle_mod, force_cif):
         for c, a in zip("YUV", planes):
             key = f"{'sc' if force_cif else 'short'}{i}.{c}"
             assert hashlib.md5(a.tobytes()).hexdigest() == exp[key], key
+
+
+def test_force_cif_refused_after_first_picture(p64, st):
+    """p64s_reader_force_cif changes the geometry the caller sized its arrays
+    for: once a picture has been read it is refused, before that
+    it is accepted."""
+    import ctypes
+    data = open(os.path.join(GOLDEN, "short.p64"), "rb").read()
+    r = st.Reader(data)
+    assert r.read() is not None
+    assert p64.lib().p64s_reader_force_cif(r._h) == -1
+    assert b"already read" in p64.lib().p64gpu_last_error()
+    r2 = st.Reader(data)
+    assert p64.lib().p64s_reader_force_cif(r2._h) == 0
+    info = st._Info()
+    assert p64.lib().p64s_reader_info(r2._h, ctypes.byref(info)) == 0
+    assert (info.width, info.height) == (352, 288)

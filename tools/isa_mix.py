@@ -1,6 +1,6 @@
 """Static instruction mix of one kernel in a gfx950 ISA listing (development aid).
 
-    hipcc ... -S --cuda-device-only -o /tmp/k.s p64_amd/csrc/p64gpu.hip
+    hipcc ... -S --cuda-device-only -o /tmp/k.s p64_amd/csrc/k_search.hip
     python tools/isa_mix.py /tmp/k.s k_intra_mbg [--top 40]
 
 Counts every instruction between the kernel's symbol label and its

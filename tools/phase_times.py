@@ -1,6 +1,6 @@
 """Per-phase wall cycles of the fused FULL encode kernel (development aid).
 
-Needs a library built with -DP64_TIMING (every SECTION() of p64gpu.hip stores
+Needs a library built with -DP64_TIMING (every SECTION() of k_search.hip stores
 the wave's s_memtime offset).  Runs the kbench workload (256 CIF sequences,
 pictures 1..3 after an intra picture) and prints, per phase, the mean cycles a
 macroblock's wave spends between that SECTION and the next one it reaches:
@@ -20,7 +20,7 @@ import torch  # noqa: E402
 
 import p64_amd  # noqa: E402
 
-src = open(os.path.join(REPO, "p64_amd/csrc/p64gpu.hip")).read()
+src = open(os.path.join(REPO, "p64_amd/csrc/k_search.hip")).read()
 names = re.findall(r'^\s*SECTION\("([^"]+)"\);', src, re.M)
 names = names + ["?"] * (31 - len(names)) + ["end"]
 w, h, S = 352, 288, 256

@@ -2,7 +2,7 @@
 
     python tools/pmc_merge.py gpurun_out/pmcb /tmp/k.s [profiles/pmc_traffic.json]
 
-/tmp/k.s is the ISA listing of p64gpu.hip (make asm, or hipcc -S
+/tmp/k.s is the ISA listing of k_search.hip (make asm, or hipcc -S
 --cuda-device-only) used for each kernel's mean VALU issue cost.
 
 Per kernel and workload it records, averaged over the profiled dispatches:

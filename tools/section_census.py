@@ -15,7 +15,7 @@ kern = sys.argv[1] if len(sys.argv) > 1 else "k_motionILi2"
 out = "/tmp/p64_sections.s"
 subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-DP64_SECTIONS",
                 *sys.argv[2:], "-S", "--cuda-device-only", "-o", out,
-                os.path.join(REPO, "p64_amd/csrc/p64gpu.hip")], check=True)
+                os.path.join(REPO, "p64_amd/csrc/k_search.hip")], check=True)
 s = open(out).read()
 start = next(i for i in range(len(s)) if s.startswith("_Z", i) and kern in s[i:s.find(":", i)]
              and s[s.find(":", i) + 1:s.find(":", i) + 4].strip().startswith(";"))

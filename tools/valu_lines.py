@@ -7,7 +7,7 @@ import subprocess
 import sys
 
 R = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-src_path = os.path.join(R, "p64_amd", "csrc", "p64gpu.hip")
+src_path = os.path.join(R, "p64_amd", "csrc", "k_search.hip")
 subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-g", "-S",
                 "--cuda-device-only", "-o", "/tmp/valu_lines.s", src_path], check=True,
                stderr=subprocess.DEVNULL)
@@ -35,5 +35,5 @@ for l in body:
 print("total VALU", sum(cnt.values()))
 for (f, ln), c in cnt.most_common(int(sys.argv[2]) if len(sys.argv) > 2 else 40):
     name = files.get(f, "?")
-    s = src[ln - 1].strip()[:80] if name.endswith("p64gpu.hip") and ln else name
+    s = src[ln - 1].strip()[:80] if name.endswith("k_search.hip") and ln else name
     print(f"{c:5d} {ln:5d} {s}")
