@@ -660,3 +660,130 @@ def test_bench_scale_properties(p64, oracle_mod, torch_dev):
                                           err_msg=f"coef s{s} t{t}")
             np.testing.assert_array_equal(host(recs[t]).reshape(S, pic)[s], recon,
                                           err_msg=f"recon s{s} t{t}")
+
+
+# ---------------------------------------------------------------------------
+# the range proofs of the packed 16-bit arithmetic, pinned at
+# their edges against the oracle: extreme levels through the decoder for every
+# q, extreme residuals and pixels through the block encoders
+
+def _edge_level_blocks(rng, n):
+    """n zigzag level blocks at the H.261 extremes: all +-127 with the sign
+    patterns that maximise the IDCT sums (constant, alternating, the sign of
+    each 1-D cosine basis row/column), plus random +-127 and random levels."""
+    pos = np.zeros(64, int)  # natural index -> scan position (transform.c:67-75)
+    k = 0
+    for d in range(15):
+        rows = range(max(0, d - 7), min(d, 7) + 1)
+        for r in (rows if d % 2 else reversed(rows)):
+            pos[8 * r + d - r] = k
+            k += 1
+    cosv = np.cos((2 * np.arange(8)[:, None] + 1) * np.arange(8)[None, :] * np.pi / 16)  # [x, u]
+    pats = [np.ones(64), -np.ones(64), np.tile([1, -1], 32), np.repeat([1, -1], 32)]
+    for u in range(8):  # natural-order sign patterns: outer products of basis signs
+        for v in range(0, 8, 3):
+            s = np.sign(np.outer(cosv[u], cosv[v]) + 1e-9).reshape(64)
+            pats += [s, -s]
+    out = np.zeros((n, 64), np.int16)
+    for i in range(n):
+        k = i % (len(pats) + 2)
+        if k < len(pats):
+            nat = (127 * pats[k]).astype(np.int16)
+        elif k == len(pats):
+            nat = (127 * rng.choice([-1, 1], 64)).astype(np.int16)
+        else:
+            nat = rng.integers(-127, 128, 64).astype(np.int16)
+        out[i, pos] = nat  # zigzag order
+    return out
+
+
+def test_decoder_extreme_levels_every_q_vs_oracle(p64, oracle_mod, torch_dev):
+    """k_recon_mbg's packed dequantiser (exact for |level| <= 528) and v_dot2
+    IDCT column pass at their edges: |level| = 127 in every position with the
+    IDCT's worst sign patterns, every q = 1..31, intra (DC 1..254) and inter
+    types with and without the loop filter, against oracle.decode_mb
+    (p64.c:1179-1237 + 971-1013)."""
+    torch = torch_dev
+    w, h = 176, 144
+    mbw, nmb, pic = w // 16, 99, w * h * 3 // 2
+    rng = np.random.default_rng(127)
+    ref = rng.integers(0, 256, pic).astype(np.uint8)
+    for rnd in range(4):
+        recon0 = rng.integers(0, 256, pic).astype(np.uint8)
+        mt = rng.integers(0, 10, nmb)
+        mt[: 10] = [0, 1, 2, 3, 4, 5, 6, 7, 8, 9]
+        cbp = rng.integers(1, 64, nmb)
+        cbp[rnd::5] = 63
+        q = (np.arange(nmb) + 7 * rnd) % 31 + 1
+        mbx, mby = np.arange(nmb) % mbw, np.arange(nmb) // mbw
+        mvx = np.array([rng.integers(max(-15, -16 * x), min(15, w - 16 - 16 * x) + 1) for x in mbx])
+        mvy = np.array([rng.integers(max(-15, -16 * y), min(15, h - 16 - 16 * y) + 1) for y in mby])
+        mf = mt >= 4
+        mvx, mvy = np.where(mf, mvx, 0), np.where(mf, mvy, 0)
+        coef = _edge_level_blocks(rng, nmb * 6).reshape(nmb, 6, 64)
+        intra = mt < 2
+        coef[intra, :, 0] = rng.choice([1, 2, 127, 128, 253, 254], (intra.sum(), 6))
+        exp = recon0.copy()
+        for k in range(nmb):
+            oracle_mod.decode_mb(w, h, ref, exp, int(mbx[k]), int(mby[k]), int(mt[k]), int(cbp[k]),
+                                 int(mvx[k]), int(mvy[k]), int(q[k]), coef[k])
+        mb = np.stack([mt, cbp, mvx, mvy], 1).astype(np.int8)
+        d = dev(torch, recon0)
+        p64.decode_recon(dev(torch, ref), d, dev(torch, coef), dev(torch, mb),
+                         dev(torch, q.astype(np.uint8)), dev(torch, np.ones(nmb, np.uint8)),
+                         width=w, height=h)
+        np.testing.assert_array_equal(host(d), exp, err_msg=f"round {rnd}")
+
+
+def _edge_pictures(w, h):
+    """(cur, ref) pairs whose residuals sit at +-255 in the patterns that drive
+    the forward DCT to its extremes: 1/2/4-pixel checkerboards, stripes,
+    half-planes, and 0/255 pictures against their inverse."""
+    y, x = np.mgrid[0:h, 0:w]
+    out = []
+    for pat in ((x + y) % 2, (x // 2 + y // 2) % 2, (x // 4 + y // 4) % 2, x % 2, y % 2,
+                (x % 8) >= 4, (y % 8) >= 4, np.zeros((h, w), int)):
+        a = (255 * np.asarray(pat, np.int64)).astype(np.uint8)
+        yc, xc = np.mgrid[0:h // 2, 0:w // 2]
+        ac = (255 * ((xc + yc) % 2)).astype(np.uint8)
+        cur = np.concatenate([a.reshape(-1), ac.reshape(-1), (255 - ac).reshape(-1)])
+        out.append((cur, 255 - cur))
+    return out
+
+
+def test_block_encoders_extreme_residuals_vs_oracle(p64, oracle_mod, torch_dev):
+    """k_intra_mbg / k_inter_mbg at the edges of their 16-bit range proofs
+    (column outputs of a +-255 residual, row-pass intermediates < 2^15, the
+    intra v_dot2 IDCT row pass bound): residuals of +-255 in checkerboard and
+    stripe patterns, 0/255 intra pictures, every q = 1..31 by per-MB UseQuant,
+    through MTYPE overrides 0..9, against oracle.encode_frame."""
+    torch = torch_dev
+    w, h = 176, 144
+    nmb = 99
+    q = ((np.arange(nmb) % 31) + 1).astype(np.uint8)
+    for i, (cur, ref) in enumerate(_edge_pictures(w, h)):
+        # intra picture of cur
+        li = np.zeros(nmb, np.uint8)
+        coef, mb, _, rec = oracle_mod.encode_frame(w, h, cur, None, li, intra=True, quant=8, quant_mb=q)
+        lid = torch.zeros(nmb, dtype=torch.uint8, device="cuda")
+        rd = torch.zeros(cur.size, dtype=torch.uint8, device="cuda")
+        o = p64.encode_frames(dev(torch, cur), None, rd, lid, width=w, height=h, intra=True, quant=8,
+                              quant_mb=dev(torch, q))
+        np.testing.assert_array_equal(host(o.coef)[0], coef, err_msg=f"intra coef pattern {i}")
+        np.testing.assert_array_equal(host(rd), rec, err_msg=f"intra recon pattern {i}")
+        # inter picture cur predicted from ref, every MTYPE by override (MC
+        # types take the ME vector the search finds)
+        ov = (np.arange(nmb) % 10).astype(np.int8)
+        li = np.zeros(nmb, np.uint8)
+        coef, mb, me, rec = oracle_mod.encode_frame(w, h, cur, ref, li, intra=False, quant=8,
+                                                    me_mode=1, search_limit=31, quant_mb=q,
+                                                    mtype_override=ov)
+        lid = torch.zeros(nmb, dtype=torch.uint8, device="cuda")
+        rd = torch.zeros(cur.size, dtype=torch.uint8, device="cuda")
+        o = p64.encode_frames(dev(torch, cur), dev(torch, ref), rd, lid, width=w, height=h,
+                              intra=False, quant=8, me_mode=p64.ME_FULL, search_limit=31,
+                              quant_mb=dev(torch, q), mtype_override=dev(torch, ov))
+        np.testing.assert_array_equal(host(o.coef)[0], coef, err_msg=f"inter coef pattern {i}")
+        np.testing.assert_array_equal(host(o.mb)[0].view(p64.MB_DTYPE).reshape(nmb), mb,
+                                      err_msg=f"inter mb pattern {i}")
+        np.testing.assert_array_equal(host(rd), rec, err_msg=f"inter recon pattern {i}")
