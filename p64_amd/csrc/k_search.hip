@@ -122,6 +122,7 @@ constexpr int ME_LIST_MAX = 256;
 static_assert(ME_LIST_MAX <= SURV_LIST_MAX, "survivor list size");
 constexpr uint32_t ME_INVALID = 1u << 19;
 constexpr int ME_LOW_CONTRAST = 12;
+constexpr int ME_NOISE_SAD0 = 24 * 256;  // mean |difference| 24 at (0,0)
 constexpr int KEY_SHIFT = 10;
 constexpr unsigned KEY_ORD = (1u << KEY_SHIFT) - 1;
 // lower-bound map: 4 phase planes (x mod 4) x MAP_ROWS rows x MAP_ROW_BYTES
@@ -232,8 +233,8 @@ __device__ __forceinline__ void build_lb_map(MbLds &L, int lane) {
 }
 
 // the current block's 16 sub-block averages (same nesting as the map), row j
-// of sub-blocks as one wave-uniform dword cm[j] (byte i = sub-block (i, j));
-// returns their range (max - min)
+// of sub-blocks as one wave-uniform dword cm[j] (byte i = sub-block (i, j),
+// also left as bytes 0..15 of L.cpred); returns their range (max - min)
 __device__ __forceinline__ int cur_lb_map(MbLds &L, int lane, uint32_t cm[4]) {
   unsigned lo = 255, hi = 0;
   if (lane < 16) {
@@ -259,6 +260,31 @@ __device__ __forceinline__ int cur_lb_map(MbLds &L, int lane, uint32_t cm[4]) {
 #pragma unroll
   for (int j = 0; j < 4; j++) cm[j] = (uint32_t)uni((int)L.cpred[j]);
   return range;
+}
+
+// SAD(0,0) (OMV, me.c:203/271) and, in the same wave reduction, the current
+// block's high-frequency energy E = sum |pixel - its 4x4 sub-block average|
+// (both < 2^16: one 32-bit sum carries the two)
+__device__ __forceinline__ void sad_zero_hf(const MbLds &L, int lane, int &sad0, int &ehf) {
+  const uint32_t r = L.win[(WIN_OY + (lane >> 2)) * WIN_WORDS + WIN_OX / 4 + (lane & 3)];
+  const uint32_t c = L.cur[lane];
+  const uint32_t m = reinterpret_cast<const uint8_t *>(L.cpred)[4 * (lane >> 4) + (lane & 3)];
+  const int t = wave_sum((int)(sad4(r, c, 0u) | (sad4(c, m * 0x01010101u, 0u) << 16)));
+  sad0 = t & 0xffff;
+  ehf = (int)((unsigned)t >> 16);
+}
+
+// every byte of the window equal: then every valid candidate block equals the
+// zero-vector block, all SADs equal SAD(0,0) and (0,0) wins (it wins ties)
+__device__ __forceinline__ bool window_constant(const MbLds &L, int lane) {
+  const uint32_t v = (L.win[0] & 255u) * 0x01010101u;
+  bool diff = false;
+#pragma unroll
+  for (int k = 0; k < (WIN_ROWS * WIN_WORDS + 63) / 64; k++) {
+    const int t = lane + 64 * k;
+    if (t < WIN_ROWS * WIN_WORDS) diff |= L.win[t] != v;
+  }
+  return !__any(diff);
 }
 
 __device__ __forceinline__ void ord_pos(unsigned ord, int &cdx, int &cdy) {  // ord >= 1
@@ -331,7 +357,7 @@ __device__ __forceinline__ unsigned finish_list(const MbLds &L, int n, int lane)
 
 
 __device__ __forceinline__ void me_full(MbLds &L, const uint8_t *cur_blk, int w, int h, int x0,
-                                        int y0, int sl, int lane, int sad0, int &mx, int &my,
+                                        int y0, int sl, int lane, int &sad0_out, int &mx, int &my,
                                         int &best) {
   const int half = lane >> 5, dxi = lane & 31;
   const bool lane_ok = dxi < 30;
@@ -361,6 +387,10 @@ __device__ __forceinline__ void me_full(MbLds &L, const uint8_t *cur_blk, int w,
   SECTION("cur_map");
   uint32_t cm[4];
   const int range = uni(cur_lb_map(L, lane, cm));
+  int sad0, ehf;
+  sad_zero_hf(L, lane, sad0, ehf);
+  sad0 = uni(sad0);
+  sad0_out = sad0;
   unsigned bk = 0xFFFFFFFFu, ckey = 0xFFFFFFFFu, Ts = 0, pk = 0;
   uint32_t acc[15];
   lds_u32 *list = as_lds(L.list);  // aliases the map once the map is dead
@@ -368,7 +398,14 @@ __device__ __forceinline__ void me_full(MbLds &L, const uint8_t *cur_blk, int w,
   // Low-contrast blocks (sub-block averages within a few levels) prune almost
   // nothing: they go to the dense search straight away (speed only, the result
   // is the same; tools/me_paths.py measured 98% dense below 12, none above 15).
-  if (range >= ME_LOW_CONTRAST) {
+  // So do noise-like blocks: a large SAD(0,0) at least half of which the
+  // current block's own high-frequency energy E (what the 4x4 averages
+  // cannot see) could account for: the bound then prunes nothing anywhere
+  // (tools/noise_rule.py: every uniform-noise block, no synthetic or 15-px
+  // pan one)
+  bool lb_path = range >= ME_LOW_CONTRAST;
+  if (sad0 > ME_NOISE_SAD0 && 2 * uni(ehf) > sad0) lb_path = false;
+  if (lb_path) {
     // 1. lower bounds S
     SECTION("lb_map");
     build_lb_map(L, lane);
@@ -444,11 +481,15 @@ __device__ __forceinline__ void me_full(MbLds &L, const uint8_t *cur_blk, int w,
       bk = finish_groups<1>(L, nsurv, lane);
     else
       bk = finish_list(L, nsurv, lane);
-  } else {  // little pruned: every candidate densely, rows in two chunks
+  } else if (range < 4 && uni(window_constant(L, lane))) {
+    bk = 0xFFFFFFFFu;  // constant window (checked for nearly flat blocks): (0,0), below
+  } else {  // little pruned: every candidate densely, the current rows in SGPRs
     const uint32_t *wrow = L.win + (15 * half) * WIN_WORDS + (colb >> 2);
     const int sh = colb & 3;
     uint32_t cs[64];
     init(acc);
+    // (in two chunks of 8 rows: all 16 in SGPRs raise the kernel's SGPR
+    // count past 80 and cost every macroblock a wave slot per SIMD)
     load_cur_rows8<0>(cur_blk, w, cs);
     full_rows<0, 8, 0, 22>(wrow, sh, cs, acc);
     load_cur_rows8<8>(cur_blk, w, cs);
@@ -543,11 +584,12 @@ template <int MODE>  // 1 = TSS, 2 = FULL
 __device__ __forceinline__ MeOut motion_estimate(MbLds &L, const uint8_t *cur_y, int w, int h,
                                                  int x0, int y0, int sl, int lane) {
   MeOut o;
-  o.sad0 = uni(sad_zero(L, lane));
-  if (MODE == 2)
+  if (MODE == 2) {
     me_full(L, cur_y + (size_t)y0 * w + x0, w, h, x0, y0, sl, lane, o.sad0, o.mx, o.my, o.sad);
-  else
+  } else {
+    o.sad0 = uni(sad_zero(L, lane));
     me_tss(L, w, h, x0, y0, lane, o.sad0, o.mx, o.my, o.sad);
+  }
   o.mx = uni(o.mx);
   o.my = uni(o.my);
   o.sad = uni(o.sad);
