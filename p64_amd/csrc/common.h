@@ -67,10 +67,39 @@ __device__ __forceinline__ int kmul(int c, int v) {
 }
 __device__ __forceinline__ int ms9(int v) { return v >> 9; }  // MSCALE, arithmetic
 
+// 24-bit constant products as the instructions themselves: hipcc turns some
+// __mul24 of the forward column pass (sums of sums of bytes, <<2) into the
+// quarter-rate v_mul_lo_u32, having lost the operand range on the way
+template <int C>
+__device__ __forceinline__ int mul_c(int v) {
+  int r;
+  asm("v_mul_i32_i24 %0, %1, %2" : "=v"(r) : "i"(C), "v"(v));
+  return r;
+}
+template <int C>
+__device__ __forceinline__ int mad_c(int v, int acc) {  // C v + acc
+  int r;
+  asm("v_mad_i32_i24 %0, %1, %2, %3" : "=v"(r) : "v"(v), "s"(C), "v"(acc));
+  return r;
+}
+
 // forward butterfly on scaled sums s[k] and differences d[k] (chendct.c:135-159)
 template <bool N>
 __device__ __forceinline__ void fwd8(const int s[4], const int d[4], int o[8]) {
   const int e0 = s[0] + s[3], e1 = s[1] + s[2], e2 = s[1] - s[2], e3 = s[0] - s[3];
+  if (N) {  // operands proven < 2^23 (callers: pixels or residuals)
+    o[0] = ms9(mul_c<C1D4>(e0 + e1));
+    o[4] = ms9(mul_c<C1D4>(e0 - e1));
+    o[2] = ms9(mad_c<C3D8>(e2, mul_c<C1D8>(e3)));
+    o[6] = ms9(mad_c<C3D8>(e3, mul_c<-C1D8>(e2)));
+    const int r0 = ms9(mul_c<C1D4>(d[1] - d[2])), r1 = ms9(mul_c<C1D4>(d[1] + d[2]));
+    const int u0 = d[3] + r0, u1 = d[3] - r0, u2 = d[0] - r1, u3 = d[0] + r1;
+    o[1] = ms9(mad_c<C7D16>(u0, mul_c<C1D16>(u3)));
+    o[3] = ms9(mad_c<C3D16>(u2, mul_c<-C5D16>(u1)));
+    o[5] = ms9(mad_c<C3D16>(u1, mul_c<C5D16>(u2)));
+    o[7] = ms9(mad_c<C7D16>(u3, mul_c<-C1D16>(u0)));
+    return;
+  }
   o[0] = ms9(kmul<N>(C1D4, e0 + e1));
   o[4] = ms9(kmul<N>(C1D4, e0 - e1));
   o[2] = ms9(kmul<N>(C3D8, e2) + kmul<N>(C1D8, e3));

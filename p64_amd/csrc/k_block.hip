@@ -15,6 +15,7 @@
 
 #include "common.h"
 #include "launch.h"
+#include "quant_int.h"
 
 namespace {
 
@@ -31,6 +32,28 @@ namespace {
 // lane writes its block's 128 bytes of levels as whole cache lines.
 
 constexpr ZigZag k_zz = make_zigzag();  // compile-time copy for register renaming
+
+// The forward quantiser from the raw row-pass output (quant_int.h: final /8,
+// BoundDct, CCITT(Flat)Quantize, bound, as one clamp, one 24-bit multiply-add
+// and one shift; tests/test_quant_int.py checks every q and value).  The
+// binary32 form it replaces (quantise in common.h) spent two conversions per
+// coefficient.
+struct QIntTab {
+  p64_qint ac[32], dc[32];  // AC (intra and inter), inter DC; by q
+};
+constexpr QIntTab make_qint_tab() {
+  QIntTab t{};
+  for (int q = 1; q < 32; q++) {
+    t.ac[q] = p64_qint_make(q, 0);
+    t.dc[q] = p64_qint_make(q, 1);
+  }
+  return t;
+}
+__constant__ QIntTab c_qint = make_qint_tab();
+__device__ __forceinline__ int qlevel_int(int v, const p64_qint &t) {
+  const int vc = min(max(v, t.vlo), t.vhi);
+  return (__mul24(vc, t.m) + (vc < 0 ? t.cn : t.cp)) >> t.s;
+}
 
 // keeps the machine scheduler from interleaving the 8 lines of a pass (it
 // would trade registers for ILP the block layout does not need: other waves
@@ -332,10 +355,7 @@ __device__ __forceinline__ void intra_block(const p64gpu_encode_args &a, const I
   const int w = a.width, h = a.height;
   const BlkPos &p = f.p;
   const int q = f.q;
-  // c_qrecip.r[q] computed in place (no dependent table load in the loop)
-  const float rq = __builtin_bit_cast(float, __builtin_bit_cast(uint32_t, 1.0f / (float)(2 * q)) + 1u);
-  const float rqe = (q & 1) ? 0.0f : rq;
-  const int qb = quant_bound(q);
+  const p64_qint qt = c_qint.ac[q];
   int v[64];
   fdct_block_pk(f.rows, v);
   // in scan order: quantise (BoundDct + CCITTFlatQuantize + FlatBound), pack
@@ -349,8 +369,8 @@ __device__ __forceinline__ void intra_block(const p64gpu_encode_args &a, const I
 #pragma unroll
       for (int i = 0; i < 2; i++) {
         const int e = k_zz.inv[8 * k + 2 * j + i];
-        const bool dc = e == 0;
-        l2[i] = quantise<true, true>(v[e], dc ? -0x7fffffff : -qb, dc ? 2047 : qb, dc, rq, rqe);
+        // intra DC: ((DC +- 4) / 8) in 1..254 of the bounded DC (transform.c:321-325)
+        l2[i] = e == 0 ? clampi(dct_final(min(dct_final(v[0]), 2047)), 1, 254) : qlevel_int(v[e], qt);
         v[e] = l2[i];  // dequantised in pairs by iq_idct_intra_rec
       }
       pk[j] = __builtin_amdgcn_perm((uint32_t)l2[1], (uint32_t)l2[0], 0x05040100u);
@@ -738,9 +758,8 @@ __global__ __launch_bounds__(256) INTER_OCC void k_inter_mbg(p64gpu_encode_args 
 
   const bool intra = mt_intra(mt), tc = mt_tcoeff(mt);
   const int q = f.q;
-  const float rq = __builtin_bit_cast(float, __builtin_bit_cast(uint32_t, 1.0f / (float)(2 * q)) + 1u);
-  const float rqe = (q & 1) ? 0.0f : rq;
-  const int qe = (int)!(q & 1), qbr = 256 * q - 1 - qe, qb = min(1023, qbr);
+  const int qe = (int)!(q & 1);
+  const p64_qint qt = c_qint.ac[q], qd = c_qint.dc[q];
   // levels & tcm: 0 when the MB type carries no coefficients (through an
   // opaque mask: as a select hipcc branches around every quantisation)
   const int tcm = opaque(tc ? -1 : 0);
@@ -759,17 +778,10 @@ __global__ __launch_bounds__(256) INTER_OCC void k_inter_mbg(p64gpu_encode_args 
 #pragma unroll
       for (int i = 0; i < 2; i++) {
         const int e = k_zz.inv[8 * k + 2 * j + i];
-        if (e == 0) {  // DC: intra (DC +- 4) / 8 in 1..254, inter as AC with DC bounds
-          const int c = dct_final(v[0]);
-          int vi;
-          asm("v_med3_i32 %0, %1, %2, %3" : "=v"(vi) : "v"(c), "v"(-qbr), "v"(min(2047, qbr)));
-          const float x = (float)vi;
-          const int li_ = (int)__builtin_fmaf(x, rq, __builtin_copysignf(rqe, x));
-          const int ld = clampi(dct_final(min(c, 2047)), 1, 254);
-          l2[i] = intra ? ld : li_;
-        } else {
-          l2[i] = quantise<false, true>(v[e], -qb, qb, false, rq, rqe);
-        }
+        if (e == 0)  // DC: intra (DC +- 4) / 8 in 1..254, inter as AC with DC bounds
+          l2[i] = intra ? clampi(dct_final(min(dct_final(v[0]), 2047)), 1, 254) : qlevel_int(v[0], qd);
+        else
+          l2[i] = qlevel_int(v[e], qt);
         l2[i] &= tcm;
       }
       pk[j] = __builtin_amdgcn_perm((uint32_t)l2[1], (uint32_t)l2[0], 0x05040100u);
