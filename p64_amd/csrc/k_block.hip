@@ -225,6 +225,28 @@ __device__ __forceinline__ uint32_t pk2(int lo, int hi) { return __builtin_amdgc
 // levels of natural positions e (low half) and e' (high half) packed; q2/qq
 // packed per lane (0 for a block without coefficients); dcfix: the DC is
 // the intra DC (dequantised as dc8 = DC x 8)
+// ChenIDct column pass of column c from its dequantised natural pairs
+// (x_c, x_4c) (x_1c, x_7c) (x_5c, x_3c) (x_2c, x_6c) -- x_rc = row r
+__device__ __forceinline__ void idct_col_pairs(int c, uint32_t p04, uint32_t p17, uint32_t p53, uint32_t p26,
+                                               int v[64]) {
+  const s16x2 a04 = __builtin_bit_cast(s16x2, p04), a17 = __builtin_bit_cast(s16x2, p17);
+  const s16x2 a53 = __builtin_bit_cast(s16x2, p53), a26 = __builtin_bit_cast(s16x2, p26);
+  const int p0 = ms9(dot2(a17, 4 * C7D16, -4 * C1D16)), p3 = ms9(dot2(a17, 4 * C1D16, 4 * C7D16));
+  const int p1 = ms9(dot2(a53, 4 * C3D16, -4 * C5D16)), p2 = ms9(dot2(a53, 4 * C5D16, 4 * C3D16));
+  const int q0 = ms9(dot2(a04, 4 * C1D4, 4 * C1D4)), q1 = ms9(dot2(a04, 4 * C1D4, -4 * C1D4));
+  const int q2_ = ms9(dot2(a26, 4 * C3D8, -4 * C1D8)), q3 = ms9(dot2(a26, 4 * C1D8, 4 * C3D8));
+  const int e0 = q0 + q3, e1 = q1 + q2_, e2 = q1 - q2_, e3 = q0 - q3;
+  const int f0 = p0 + p1, f1 = p0 - p1, f2 = p3 - p2, f3 = p3 + p2;
+  const int g1 = ms9(kmul<true>(C1D4, f2 - f1)), g2 = ms9(kmul<true>(C1D4, f2 + f1));
+  v[c] = e0 + f3;
+  v[8 + c] = e1 + g2;
+  v[16 + c] = e2 + g1;
+  v[24 + c] = e3 + f0;
+  v[32 + c] = e3 - f0;
+  v[40 + c] = e2 - g1;
+  v[48 + c] = e1 - g2;
+  v[56 + c] = e0 - f3;
+}
 template <class PairFn>
 __device__ __forceinline__ void iq_idct_cols(PairFn pair, uint32_t q2, uint32_t qq, bool dcfix, int dc8,
                                              int v[64]) {
@@ -232,36 +254,8 @@ __device__ __forceinline__ void iq_idct_cols(PairFn pair, uint32_t q2, uint32_t 
   for (int c = 0; c < 8; c++) {
     uint32_t p04 = dequantise_pk(pair(c, 32 + c), q2, qq);
     if (c == 0) p04 = dcfix ? __builtin_amdgcn_perm(p04, (uint32_t)dc8, 0x07060100u) : p04;  // (DC x 8, x4)
-    const s16x2 a04 = __builtin_bit_cast(s16x2, p04);
-    const s16x2 a17 = __builtin_bit_cast(s16x2, dequantise_pk(pair(8 + c, 56 + c), q2, qq));
-    const s16x2 a53 = __builtin_bit_cast(s16x2, dequantise_pk(pair(40 + c, 24 + c), q2, qq));
-    const s16x2 a26 = __builtin_bit_cast(s16x2, dequantise_pk(pair(16 + c, 48 + c), q2, qq));
-    const int p0 = ms9(dot2(a17, 4 * C7D16, -4 * C1D16)), p3 = ms9(dot2(a17, 4 * C1D16, 4 * C7D16));
-    const int p1 = ms9(dot2(a53, 4 * C3D16, -4 * C5D16)), p2 = ms9(dot2(a53, 4 * C5D16, 4 * C3D16));
-    const int q0 = ms9(dot2(a04, 4 * C1D4, 4 * C1D4)), q1 = ms9(dot2(a04, 4 * C1D4, -4 * C1D4));
-    const int q2_ = ms9(dot2(a26, 4 * C3D8, -4 * C1D8)), q3 = ms9(dot2(a26, 4 * C1D8, 4 * C3D8));
-    const int e0 = q0 + q3, e1 = q1 + q2_, e2 = q1 - q2_, e3 = q0 - q3;
-    const int f0 = p0 + p1, f1 = p0 - p1, f2 = p3 - p2, f3 = p3 + p2;
-    const int g1 = ms9(kmul<true>(C1D4, f2 - f1)), g2 = ms9(kmul<true>(C1D4, f2 + f1));
-    v[c] = e0 + f3;
-    v[8 + c] = e1 + g2;
-    v[16 + c] = e2 + g1;
-    v[24 + c] = e3 + f0;
-    v[32 + c] = e3 - f0;
-    v[40 + c] = e2 - g1;
-    v[48 + c] = e1 - g2;
-    v[56 + c] = e0 - f3;
-    SCHED_FENCE();
-  }
-}
-// row pass + idct_final (the residual, to be added to a prediction)
-__device__ __forceinline__ void idct_rows(int v[64]) {
-#pragma unroll
-  for (int r = 0; r < 8; r++) {
-    int o[8];
-    inv8<true>(v + 8 * r, o);
-#pragma unroll
-    for (int k = 0; k < 8; k++) v[8 * r + k] = idct_final(o[k]);
+    idct_col_pairs(c, p04, dequantise_pk(pair(8 + c, 56 + c), q2, qq), dequantise_pk(pair(40 + c, 24 + c), q2, qq),
+                   dequantise_pk(pair(16 + c, 48 + c), q2, qq), v);
     SCHED_FENCE();
   }
 }
@@ -590,26 +584,49 @@ __device__ __forceinline__ void rec_block_pk(int w, int h, int64_t stride, __amd
     const uint32_t sel = ((s1 & 1) ? 0x0302u : 0x0100u) | (((s2 & 1) ? 0x0706u : 0x0504u) << 16);
     return __builtin_amdgcn_perm(S.lq[s2 >> 3][(s2 >> 1) & 3], S.lq[s1 >> 3][(s1 >> 1) & 3], sel);
   };
-  iq_idct_cols(pair, q2, qq, !S.inter, (int)(int16_t)(S.lq[0][0] & 0xffff) * 8, v);
-  idct_rows(v);
+  // every column's dequantised natural pairs first: the zigzag words die
+  // here, so the IDCT's 64 values never share the registers with them
+  // (peak 84 instead of 112 live values: 4 waves per SIMD instead of 3)
+  uint32_t np[8][4];
+#pragma unroll
+  for (int c = 0; c < 8; c++) {
+    np[c][0] = dequantise_pk(pair(c, 32 + c), q2, qq);
+    np[c][1] = dequantise_pk(pair(8 + c, 56 + c), q2, qq);
+    np[c][2] = dequantise_pk(pair(40 + c, 24 + c), q2, qq);
+    np[c][3] = dequantise_pk(pair(16 + c, 48 + c), q2, qq);
+  }
+  if (!S.inter)  // intra DC: DC x 8 (transform.c:371)
+    np[0][0] = __builtin_amdgcn_perm(np[0][0], (uint32_t)((int)(int16_t)(S.lq[0][0] & 0xffff) * 8), 0x07060100u);
+  SCHED_FENCE();
+#pragma unroll
+  for (int c = 0; c < 8; c++) {
+    idct_col_pairs(c, np[c][0], np[c][1], np[c][2], np[c][3], v);
+    SCHED_FENCE();
+  }
   const int pw = p.plane ? w >> 1 : w;
   const uint32_t ro = A.coded ? (uint32_t)((int64_t)p.fi * stride) + (uint32_t)plane_offset(p.plane, w, h) +
                                     (uint32_t)(mul24(p.y, pw) + p.x)
                               : BUF_OOB;
+  // row pass, + prediction, BoundIDctMatrix and the store, row by row: each
+  // row's values die at its store
 #pragma unroll
   for (int k = 0; k < 8; k++) {
-    const uint2 r = recon_row(v + 8 * k, prow[k]);  // + prediction, BoundIDctMatrix
+    int o[8];
+    inv8<true>(v + 8 * k, o);
+#pragma unroll
+    for (int j = 0; j < 8; j++) o[j] = idct_final(o[j]);
+    const uint2 r = recon_row(o, prow[k]);
     typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
     u32x2 d;
     d[0] = r.x;
     d[1] = r.y;
     __builtin_amdgcn_raw_buffer_store_b64(d, rec, ro + (uint32_t)mul24(k, pw), 0, 0);
+    SCHED_FENCE();
   }
 }
-// occupancy targets: k_inter_mbg 4 waves per SIMD (<= 128 VGPRs), the decoder
-// 3 (its 139 VGPRs spill at 4)
+// occupancy targets: 4 waves per SIMD (<= 128 VGPRs)
 #define INTER_OCC __attribute__((amdgpu_waves_per_eu(4)))
-#define RECON_OCC __attribute__((amdgpu_waves_per_eu(3)))
+#define RECON_OCC __attribute__((amdgpu_waves_per_eu(4)))
 // decoder reconstruction, MB-grouped block layout (blk_pos_mb), one block per
 // lane and no loop: 10 MBs per wave, each lane loads its MB's record, then its
 // levels and prediction, reconstructs and stores.  Without the persistent
@@ -812,9 +829,15 @@ __global__ __launch_bounds__(256) INTER_OCC void k_inter_mbg(p64gpu_encode_args 
   const uint32_t q2 = ck ? 0x20002u * (uint32_t)q : 0u, qq = ck ? 0x10001u * (uint32_t)(q - qe) : 0u;
   // IQ in level pairs + ChenIDct (all-zero levels / q2 = qq = 0 give zero)
   iq_idct_cols([&](int e, int f) { return pk2(v[e], v[f]); }, q2, qq, intra, v[0] * 8, v);
-  idct_rows(v);
 #pragma unroll
-  for (int k = 0; k < 8; k++) prow[k] = recon_row(v + 8 * k, prow[k]);  // now the reconstructed rows
+  for (int k = 0; k < 8; k++) {  // row pass + prediction: now the reconstructed rows
+    int o[8];
+    inv8<true>(v + 8 * k, o);
+#pragma unroll
+    for (int j = 0; j < 8; j++) o[j] = idct_final(o[j]);
+    prow[k] = recon_row(o, prow[k]);
+    SCHED_FENCE();
+  }
   // no levels at all in the MB: the reconstruction is the new prediction
   // (late, so its registers do not overlap the block's)
   if (repred) inter_pred(B, w, h, stride, pos, mt, mvx, mvy, prow);

@@ -52,6 +52,18 @@ def report(name, t):
 
 def main():
     w, h, S = 352, 288, 256
+    if len(sys.argv) > 1 and sys.argv[1] == "motion":  # the k_motion stamp build
+        nmb, pic = (w // 16) * (h // 16), w * h * 3 // 2
+        fr = bench.make_inputs(torch, p64_amd, "synth", w, h, 1, S, 3)
+        li = torch.zeros(S * nmb, dtype=torch.uint8, device="cuda")
+        r0 = torch.zeros(S * pic, dtype=torch.uint8, device="cuda")
+        p64_amd.encode_frames(fr[0].reshape(-1), None, r0, li, width=w, height=h, intra=True, quant=8)
+        for _ in range(2):
+            p64_amd.MotionEstimation(r0, fr[1].reshape(-1), w, h, mode=p64_amd.ME_FULL, search_limit=31)
+        grab(S * nmb)
+        p64_amd.MotionEstimation(r0, fr[1].reshape(-1), w, h, mode=p64_amd.ME_FULL, search_limit=31)
+        report("k_motion<2>", grab(S * nmb))
+        return
     nmb, pic = (w // 16) * (h // 16), w * h * 3 // 2
     nw = (S * nmb + 9) // 10
     fr = bench.make_inputs(torch, p64_amd, "synth", w, h, 1, S, 3)
