@@ -51,6 +51,33 @@ struct __align__(16) MbLds {
   uint32_t cpred[2 * 16];              // chroma prediction sources, 2 x 8x8 bytes
 };
 
+// The search reads its macroblock's window, current block and lower-bound map
+// through these views (Sx) and a geometry G -- dwords per window row, bytes
+// per map plane row and plane -- rather than one fixed LDS struct, so that
+// images with wider windows (several macroblocks sharing one window and map:
+// measured as a 4-MB tile per workgroup) reuse the same code.
+constexpr int MAP_ROWS = 42;
+template <int WS_, int MAP_ROW_>
+struct Geo {
+  static constexpr int WS = WS_, MAP_ROW = MAP_ROW_, MAP_PLANE = MAP_ROWS * MAP_ROW_;
+};
+using Geo1 = Geo<WIN_WORDS, 12>;  // MbLds: one macroblock per wave
+struct Sx {
+  const uint32_t *win;  // the MB's 46 x 48-byte window: row r at win + r * G::WS
+  uint32_t *cur;        // current 16x16 luma, 64 dwords
+  uint32_t *cpred;      // 16 bytes of scratch
+  uint32_t *list;       // survivor list (SURV_LIST_MAX)
+  uint32_t *map;        // the MB's origin in the lower-bound map
+};
+__device__ __forceinline__ Sx sx_of(MbLds &L) { return Sx{L.win, L.cur, L.cpred, L.list, L.map}; }
+
+// Wave-level LDS ordering: every search step below syncs within its wave only
+__device__ __forceinline__ void wsync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 // The search window (zero outside the picture: such candidates are never
 // valid, me.c:212/292) and the current luma block, fetched into registers
 // (LumaFetch) one macroblock ahead of its use, then stored to LDS (put_luma).
@@ -87,9 +114,10 @@ __device__ __forceinline__ void put_luma(MbLds &L, const LumaFetch &f, int lane)
 }
 
 // SAD of the zero vector (OMV, me.c:203/271): one dword per lane
-__device__ __forceinline__ int sad_zero(const MbLds &L, int lane) {
-  const uint32_t r = L.win[(WIN_OY + (lane >> 2)) * WIN_WORDS + WIN_OX / 4 + (lane & 3)];
-  return wave_sum((int)sad4(r, L.cur[lane], 0));
+template <class G>
+__device__ __forceinline__ int sad_zero(const Sx &S, int lane) {
+  const uint32_t r = S.win[(WIN_OY + (lane >> 2)) * G::WS + WIN_OX / 4 + (lane & 3)];
+  return wave_sum((int)sad4(r, S.cur[lane], 0));
 }
 
 // FastBME (me.c:187-227) over [-sl/2, sl/2)^2, exact, pruned by a lower bound
@@ -127,16 +155,16 @@ constexpr int KEY_SHIFT = 10;
 constexpr unsigned KEY_ORD = (1u << KEY_SHIFT) - 1;
 // lower-bound map: 4 phase planes (x mod 4) x MAP_ROWS rows x MAP_ROW_BYTES
 // bytes; plane p, row y, byte k holds m(4k + p, y) in window coordinates
-constexpr int MAP_ROWS = 42, MAP_ROW_BYTES = 12, MAP_PLANE_BYTES = MAP_ROWS * MAP_ROW_BYTES;
+constexpr int MAP_ROW_BYTES = Geo1::MAP_ROW, MAP_PLANE_BYTES = Geo1::MAP_PLANE;
 static_assert(4 * MAP_PLANE_BYTES == 4 * LB_MAP_WORDS, "map size");
 
 // rows [R0, R1) of the current block against window rows [I0, I1) of the lane
-template <int R0, int R1, int I0, int I1>
+template <class G, int R0, int R1, int I0, int I1>
 __device__ __forceinline__ void full_rows(const uint32_t *wrow, int sh, const uint32_t *cs,
                                           uint32_t *acc) {
 #pragma unroll
   for (int i = I0; i < I1; i++) {
-    const uint32_t *p = wrow + i * WIN_WORDS;
+    const uint32_t *p = wrow + i * G::WS;
     const uint32_t a0 = p[0], a1 = p[1], a2 = p[2], a3 = p[3], a4 = p[4];
     const uint32_t r0 = align4(a1, a0, sh), r1 = align4(a2, a1, sh);
     const uint32_t r2 = align4(a3, a2, sh), r3 = align4(a4, a3, sh);
@@ -204,7 +232,7 @@ __device__ __forceinline__ uint32_t from_next_lane_wave(uint32_t v) {
 // (chunk c of 9 map rows, natural dword n = x/4); vertical levels on the window
 // dwords, horizontal levels with the neighbour dword from lane + 1, the four
 // bytes of a natural dword scattered to the four phase planes.
-__device__ __forceinline__ void build_lb_map(MbLds &L, int lane) {
+__device__ __forceinline__ void build_lb_map(const Sx &S, int lane) {
   const int c = lane / 12, n = lane - 12 * c;
   const bool act = lane < 60;
   const int y0 = 9 * min(c, 4);
@@ -212,9 +240,9 @@ __device__ __forceinline__ void build_lb_map(MbLds &L, int lane) {
 #pragma unroll
   for (int t = 0; t < 11; t++) {
     const int ya = min(y0 + t, WIN_ROWS - 1), yb = min(y0 + t + 1, WIN_ROWS - 1);
-    v1[t] = lerp4(L.win[ya * WIN_WORDS + n], L.win[yb * WIN_WORDS + n]);
+    v1[t] = lerp4(S.win[ya * WIN_WORDS + n], S.win[yb * WIN_WORDS + n]);
   }
-  uint8_t *mp = reinterpret_cast<uint8_t *>(L.map) + n;
+  uint8_t *mp = reinterpret_cast<uint8_t *>(S.map) + n;
 #pragma unroll
   for (int t = 0; t < 9; t++) {
     const uint32_t v = lerp4(v1[t], v1[t + 2]);  // rows y..y+3
@@ -235,15 +263,15 @@ __device__ __forceinline__ void build_lb_map(MbLds &L, int lane) {
 // the current block's 16 sub-block averages (same nesting as the map), row j
 // of sub-blocks as one wave-uniform dword cm[j] (byte i = sub-block (i, j),
 // also left as bytes 0..15 of L.cpred); returns their range (max - min)
-__device__ __forceinline__ int cur_lb_map(MbLds &L, int lane, uint32_t cm[4]) {
+__device__ __forceinline__ int cur_lb_map(const Sx &S, int lane, uint32_t cm[4]) {
   unsigned lo = 255, hi = 0;
   if (lane < 16) {
     const int i = lane & 3, j = lane >> 2;
-    const uint32_t *r = L.cur + 16 * j + i;
+    const uint32_t *r = S.cur + 16 * j + i;
     const uint32_t v = lerp4(lerp4(r[0], r[4]), lerp4(r[8], r[12]));
     const uint32_t h1 = lerp4(v, v >> 8);
     const uint32_t h2 = lerp4(h1, h1 >> 16);
-    reinterpret_cast<uint8_t *>(L.cpred)[lane] = (uint8_t)h2;
+    reinterpret_cast<uint8_t *>(S.cpred)[lane] = (uint8_t)h2;
     lo = hi = h2 & 255u;
   }
   // min and max over DPP row 0 (lanes 0..15)
@@ -256,19 +284,20 @@ __device__ __forceinline__ int cur_lb_map(MbLds &L, int lane, uint32_t cm[4]) {
   lo = min(lo, dpp<0x140>(lo));
   hi = max(hi, dpp<0x140>(hi));
   const int range = __builtin_amdgcn_readlane((int)(hi - lo), 0);
-  __syncthreads();
+  wsync();
 #pragma unroll
-  for (int j = 0; j < 4; j++) cm[j] = (uint32_t)uni((int)L.cpred[j]);
+  for (int j = 0; j < 4; j++) cm[j] = (uint32_t)uni((int)S.cpred[j]);
   return range;
 }
 
 // SAD(0,0) (OMV, me.c:203/271) and, in the same wave reduction, the current
 // block's high-frequency energy E = sum |pixel - its 4x4 sub-block average|
 // (both < 2^16: one 32-bit sum carries the two)
-__device__ __forceinline__ void sad_zero_hf(const MbLds &L, int lane, int &sad0, int &ehf) {
-  const uint32_t r = L.win[(WIN_OY + (lane >> 2)) * WIN_WORDS + WIN_OX / 4 + (lane & 3)];
-  const uint32_t c = L.cur[lane];
-  const uint32_t m = reinterpret_cast<const uint8_t *>(L.cpred)[4 * (lane >> 4) + (lane & 3)];
+template <class G>
+__device__ __forceinline__ void sad_zero_hf(const Sx &S, int lane, int &sad0, int &ehf) {
+  const uint32_t r = S.win[(WIN_OY + (lane >> 2)) * G::WS + WIN_OX / 4 + (lane & 3)];
+  const uint32_t c = S.cur[lane];
+  const uint32_t m = reinterpret_cast<const uint8_t *>(S.cpred)[4 * (lane >> 4) + (lane & 3)];
   const int t = wave_sum((int)(sad4(r, c, 0u) | (sad4(c, m * 0x01010101u, 0u) << 16)));
   sad0 = t & 0xffff;
   ehf = (int)((unsigned)t >> 16);
@@ -276,13 +305,14 @@ __device__ __forceinline__ void sad_zero_hf(const MbLds &L, int lane, int &sad0,
 
 // every byte of the window equal: then every valid candidate block equals the
 // zero-vector block, all SADs equal SAD(0,0) and (0,0) wins (it wins ties)
-__device__ __forceinline__ bool window_constant(const MbLds &L, int lane) {
-  const uint32_t v = (L.win[0] & 255u) * 0x01010101u;
+template <class G>
+__device__ __forceinline__ bool window_constant(const Sx &S, int lane) {
+  const uint32_t v = (S.win[0] & 255u) * 0x01010101u;
   bool diff = false;
 #pragma unroll
   for (int k = 0; k < (WIN_ROWS * WIN_WORDS + 63) / 64; k++) {
-    const int t = lane + 64 * k;
-    if (t < WIN_ROWS * WIN_WORDS) diff |= L.win[t] != v;
+    const int t = lane + 64 * k, row = t / WIN_WORDS;
+    if (t < WIN_ROWS * WIN_WORDS) diff |= S.win[row * G::WS + t - row * WIN_WORDS] != v;
   }
   return !__any(diff);
 }
@@ -292,28 +322,28 @@ __device__ __forceinline__ void ord_pos(unsigned ord, int &cdx, int &cdy) {  // 
   cdy = (int)((ord - 1) & 31) - 15;
 }
 
-// full SADs of the n <= 32 listed candidates (ords in L.list), 4*RG lanes per
+// full SADs of the n <= 32 listed candidates (ords in S.list), 4*RG lanes per
 // candidate: lane (slot, rg, d) sums dword d of rows rg, rg+RG, ...; returns the
 // least key
-template <int RG>
-__device__ __forceinline__ unsigned finish_groups(const MbLds &L, int n, int lane) {
-  constexpr int G = 4 * RG, PER = 64 / G, NR = 16 / RG;
-  const int d = lane & 3, rg = (lane >> 2) & (RG - 1), slot = lane / G;
+template <class G, int RG>
+__device__ __forceinline__ unsigned finish_groups(const Sx &S, int n, int lane) {
+  constexpr int GL = 4 * RG, PER = 64 / GL, NR = 16 / RG;  // lanes per candidate
+  const int d = lane & 3, rg = (lane >> 2) & (RG - 1), slot = lane / GL;
   uint32_t cw[NR];
 #pragma unroll
-  for (int t = 0; t < NR; t++) cw[t] = L.cur[4 * (rg + RG * t) + d];
+  for (int t = 0; t < NR; t++) cw[t] = S.cur[4 * (rg + RG * t) + d];
   unsigned bk = 0xFFFFFFFFu;
   for (int c0 = 0; c0 < n; c0 += PER) {
     const int j = c0 + slot;
-    const unsigned ord = j < n ? L.list[j] : 1u;
+    const unsigned ord = j < n ? S.list[j] : 1u;
     int cdx, cdy;
     ord_pos(ord, cdx, cdy);
     const int cb = WIN_OX + cdx, csh = cb & 3;
-    const uint32_t *p0 = L.win + (WIN_OY + cdy + rg) * WIN_WORDS + (cb >> 2) + d;
+    const uint32_t *p0 = S.win + (WIN_OY + cdy + rg) * G::WS + (cb >> 2) + d;
     uint32_t a = 0;
 #pragma unroll
     for (int t = 0; t < NR; t++) {
-      const uint32_t *p = p0 + RG * t * WIN_WORDS;
+      const uint32_t *p = p0 + RG * t * G::WS;
       a = sad4(align4(p[1], p[0], csh), cw[t], a);
     }
     a += dpp<0xB1>(a);  // the group's lanes: quad, then 8, then 16
@@ -327,23 +357,24 @@ __device__ __forceinline__ unsigned finish_groups(const MbLds &L, int n, int lan
 
 // full SADs of the listed candidates (keys with the ord in the low bits), one
 // per lane; returns the least key
-__device__ __forceinline__ unsigned finish_list(const MbLds &L, int n, int lane) {
+template <class G>
+__device__ __forceinline__ unsigned finish_list(const Sx &S, int n, int lane) {
   unsigned bk = 0xFFFFFFFFu;
   for (int c0 = 0; c0 < n; c0 += 64) {
     if (c0 + lane < n) {
-      const unsigned ord = L.list[c0 + lane] & KEY_ORD;
+      const unsigned ord = S.list[c0 + lane] & KEY_ORD;
       int cdx, cdy;
       ord_pos(ord, cdx, cdy);
       const int cb = WIN_OX + cdx, csh = cb & 3;
-      const uint32_t *p0 = L.win + (WIN_OY + cdy) * WIN_WORDS + (cb >> 2);
+      const uint32_t *p0 = S.win + (WIN_OY + cdy) * G::WS + (cb >> 2);
       uint32_t a = 0;
 #pragma unroll
       for (int r = 0; r < 16; r++) {
-        const uint32_t *p = p0 + r * WIN_WORDS;
+        const uint32_t *p = p0 + r * G::WS;
         const uint32_t a0 = p[0], a1 = p[1], a2 = p[2], a3 = p[3], a4 = p[4];
         // LDS broadcast, re-read per chunk (opaque index: not hoisted out of
         // the loop into live registers)
-        const uint4 c = reinterpret_cast<const uint4 *>(L.cur)[opaque(r)];
+        const uint4 c = reinterpret_cast<const uint4 *>(S.cur)[opaque(r)];
         a = sad4(align4(a1, a0, csh), c.x, a);
         a = sad4(align4(a2, a1, csh), c.y, a);
         a = sad4(align4(a3, a2, csh), c.z, a);
@@ -356,7 +387,8 @@ __device__ __forceinline__ unsigned finish_list(const MbLds &L, int n, int lane)
 }
 
 
-__device__ __forceinline__ void me_full(MbLds &L, const uint8_t *cur_blk, int w, int h, int x0,
+template <class G>
+__device__ __forceinline__ void me_full(const Sx &S, const uint8_t *cur_blk, int w, int h, int x0,
                                         int y0, int sl, int lane, int &sad0_out, int &mx, int &my,
                                         int &best) {
   const int half = lane >> 5, dxi = lane & 31;
@@ -386,14 +418,14 @@ __device__ __forceinline__ void me_full(MbLds &L, const uint8_t *cur_blk, int w,
 
   SECTION("cur_map");
   uint32_t cm[4];
-  const int range = uni(cur_lb_map(L, lane, cm));
+  const int range = uni(cur_lb_map(S, lane, cm));
   int sad0, ehf;
-  sad_zero_hf(L, lane, sad0, ehf);
+  sad_zero_hf<G>(S, lane, sad0, ehf);
   sad0 = uni(sad0);
   sad0_out = sad0;
   unsigned bk = 0xFFFFFFFFu, ckey = 0xFFFFFFFFu, Ts = 0, pk = 0;
   uint32_t acc[15];
-  lds_u32 *list = as_lds(L.list);  // aliases the map once the map is dead
+  lds_u32 *list = as_lds(S.list);  // (one-MB image: aliases the map once the map is dead)
   int nsurv = 1000;
   // Low-contrast blocks (sub-block averages within a few levels) prune almost
   // nothing: they go to the dense search straight away (speed only, the result
@@ -408,18 +440,17 @@ __device__ __forceinline__ void me_full(MbLds &L, const uint8_t *cur_blk, int w,
   if (lb_path) {
     // 1. lower bounds S
     SECTION("lb_map");
-    build_lb_map(L, lane);
-    __syncthreads();
+    build_lb_map(S, lane);
+    wsync();
     SECTION("lb_pass");
     init(acc);
     {
       const int xq = colb >> 2;
-      const uint32_t *mrow =
-          L.map + ((colb & 3) * MAP_PLANE_BYTES + 15 * half * MAP_ROW_BYTES) / 4 + (xq >> 2);
+      const uint32_t *mrow = S.map + ((colb & 3) * G::MAP_PLANE + 15 * half * G::MAP_ROW) / 4 + (xq >> 2);
       const int msh = xq & 3;
 #pragma unroll
       for (int i = 0; i < 27; i++) {
-        const uint32_t *q = mrow + i * (MAP_ROW_BYTES / 4);
+        const uint32_t *q = mrow + i * (G::MAP_ROW / 4);
         const uint32_t m4 = align4(q[1], q[0], msh);
 #pragma unroll
         for (int j = 0; j < 4; j++) {
@@ -442,8 +473,8 @@ __device__ __forceinline__ void me_full(MbLds &L, const uint8_t *cur_blk, int w,
       int cdx, cdy;
       ord_pos(pk & KEY_ORD, cdx, cdy);
       const int cb = WIN_OX + cdx + 4 * (lane & 3);
-      const uint32_t *p = L.win + (WIN_OY + cdy + (lane >> 2)) * WIN_WORDS + (cb >> 2);
-      const uint32_t s = sad4(align4(p[1], p[0], cb & 3), L.cur[lane], 0u);
+      const uint32_t *p = S.win + (WIN_OY + cdy + (lane >> 2)) * G::WS + (cb >> 2);
+      const uint32_t s = sad4(align4(p[1], p[0], cb & 3), S.cur[lane], 0u);
       ckey = (pk & KEY_ORD) | ((unsigned)uni(wave_sum((int)s)) << KEY_SHIFT);
     }
     const unsigned T = min(ckey >> KEY_SHIFT, (unsigned)sad0);
@@ -469,31 +500,31 @@ __device__ __forceinline__ void me_full(MbLds &L, const uint8_t *cur_blk, int w,
 
   SECTION("finish");
   if (nsurv <= ME_LIST_MAX) {
-    __syncthreads();
+    wsync();
     // nothing to finish when c* (whose key is known) is the only survivor
     if (nsurv == 0 || (nsurv == 1 && (unsigned)uni((int)list[0]) == (pk & KEY_ORD)))
       ;
     else if (nsurv <= 4)
-      bk = finish_groups<4>(L, nsurv, lane);
+      bk = finish_groups<G, 4>(S, nsurv, lane);
     else if (nsurv <= 8)
-      bk = finish_groups<2>(L, nsurv, lane);
+      bk = finish_groups<G, 2>(S, nsurv, lane);
     else if (nsurv <= 32)
-      bk = finish_groups<1>(L, nsurv, lane);
+      bk = finish_groups<G, 1>(S, nsurv, lane);
     else
-      bk = finish_list(L, nsurv, lane);
-  } else if (range < 4 && uni(window_constant(L, lane))) {
+      bk = finish_list<G>(S, nsurv, lane);
+  } else if (range < 4 && uni(window_constant<G>(S, lane))) {
     bk = 0xFFFFFFFFu;  // constant window (checked for nearly flat blocks): (0,0), below
   } else {  // little pruned: every candidate densely, the current rows in SGPRs
-    const uint32_t *wrow = L.win + (15 * half) * WIN_WORDS + (colb >> 2);
+    const uint32_t *wrow = S.win + (15 * half) * G::WS + (colb >> 2);
     const int sh = colb & 3;
     uint32_t cs[64];
     init(acc);
     // (in two chunks of 8 rows: all 16 in SGPRs raise the kernel's SGPR
     // count past 80 and cost every macroblock a wave slot per SIMD)
     load_cur_rows8<0>(cur_blk, w, cs);
-    full_rows<0, 8, 0, 22>(wrow, sh, cs, acc);
+    full_rows<G, 0, 8, 0, 22>(wrow, sh, cs, acc);
     load_cur_rows8<8>(cur_blk, w, cs);
-    full_rows<8, 16, 8, 30>(wrow, sh, cs, acc);
+    full_rows<G, 8, 16, 8, 30>(wrow, sh, cs, acc);
 #pragma unroll
     for (int d = 0; d < 15; d++) bk = min(bk, (acc[d] << KEY_SHIFT) + base + d);
     bk = wave_min(bk);
@@ -513,14 +544,15 @@ __device__ __forceinline__ void me_full(MbLds &L, const uint8_t *cur_blk, int w,
 
 // StepBME (me.c:255-311): steps 8,4,2,1, 8 neighbours each in (diry, dirx)
 // raster order, strict '<' against the running best.
-__device__ __forceinline__ void me_tss(const MbLds &L, int w, int h, int x0, int y0, int lane,
+template <class G>
+__device__ __forceinline__ void me_tss(const Sx &S, int w, int h, int x0, int y0, int lane,
                                        int sad0, int &mx, int &my, int &best) {
   const int k = lane >> 3, rg = lane & 7;
   const int kk = k < 4 ? k : k + 1;  // skip the centre of the 3x3
   const int dirx = kk % 3 - 1, diry = kk / 3 - 1;
   uint32_t c[8];
 #pragma unroll
-  for (int j = 0; j < 8; j++) c[j] = L.cur[8 * rg + j];  // rows 2rg, 2rg+1
+  for (int j = 0; j < 8; j++) c[j] = S.cur[8 * rg + j];  // rows 2rg, 2rg+1
   int bx = 0, by = 0;
   unsigned bsad = (unsigned)sad0;
 #pragma unroll
@@ -532,10 +564,10 @@ __device__ __forceinline__ void me_tss(const MbLds &L, int w, int h, int x0, int
     uint32_t s = 0;
     if (ok) {
       const int colb = WIN_OX + dx, sh = colb & 3;
-      const uint32_t *p = L.win + (WIN_OY + dy + 2 * rg) * WIN_WORDS + (colb >> 2);
+      const uint32_t *p = S.win + (WIN_OY + dy + 2 * rg) * G::WS + (colb >> 2);
 #pragma unroll
       for (int rr = 0; rr < 2; rr++) {
-        const uint32_t *q = p + rr * WIN_WORDS;
+        const uint32_t *q = p + rr * G::WS;
         const uint32_t a0 = q[0], a1 = q[1], a2 = q[2], a3 = q[3], a4 = q[4];
         s = sad4(align4(a1, a0, sh), c[4 * rr + 0], s);
         s = sad4(align4(a2, a1, sh), c[4 * rr + 1], s);
@@ -564,10 +596,11 @@ __device__ __forceinline__ void me_tss(const MbLds &L, int w, int h, int x0, int
 
 // decision statistics on the chosen block (me.c:229-245 == 313-329), with the
 // byte dot product: sum (r-c)^2 = r.r - 2 r.c + c.c, all exact in u32
-__device__ __forceinline__ void me_stats(const MbLds &L, int lane, MeOut &o) {
+template <class G>
+__device__ __forceinline__ void me_stats(const Sx &S, int lane, MeOut &o) {
   const int colb = WIN_OX + o.mx + 4 * (lane & 3);
-  const uint32_t *p = L.win + (WIN_OY + o.my + (lane >> 2)) * WIN_WORDS + (colb >> 2);
-  const uint32_t rw = align4(p[1], p[0], colb & 3), cw = L.cur[lane];
+  const uint32_t *p = S.win + (WIN_OY + o.my + (lane >> 2)) * G::WS + (colb >> 2);
+  const uint32_t rw = align4(p[1], p[0], colb & 3), cw = S.cur[lane];
   const unsigned rr = __builtin_amdgcn_udot4(rw, rw, 0u, false);
   const unsigned rc = __builtin_amdgcn_udot4(rw, cw, 0u, false);
   const unsigned cc = __builtin_amdgcn_udot4(cw, cw, 0u, false);
@@ -580,20 +613,20 @@ __device__ __forceinline__ void me_stats(const MbLds &L, int lane, MeOut &o) {
 }
 
 
-template <int MODE>  // 1 = TSS, 2 = FULL
-__device__ __forceinline__ MeOut motion_estimate(MbLds &L, const uint8_t *cur_y, int w, int h,
+template <class G, int MODE>  // MODE 1 = TSS, 2 = FULL
+__device__ __forceinline__ MeOut motion_estimate(const Sx &S, const uint8_t *cur_y, int w, int h,
                                                  int x0, int y0, int sl, int lane) {
   MeOut o;
   if (MODE == 2) {
-    me_full(L, cur_y + (size_t)y0 * w + x0, w, h, x0, y0, sl, lane, o.sad0, o.mx, o.my, o.sad);
+    me_full<G>(S, cur_y + (size_t)y0 * w + x0, w, h, x0, y0, sl, lane, o.sad0, o.mx, o.my, o.sad);
   } else {
-    o.sad0 = uni(sad_zero(L, lane));
-    me_tss(L, w, h, x0, y0, lane, o.sad0, o.mx, o.my, o.sad);
+    o.sad0 = uni(sad_zero<G>(S, lane));
+    me_tss<G>(S, w, h, x0, y0, lane, o.sad0, o.mx, o.my, o.sad);
   }
   o.mx = uni(o.mx);
   o.my = uni(o.my);
   o.sad = uni(o.sad);
-  me_stats(L, lane, o);
+  me_stats<G>(S, lane, o);
   o.var = uni(o.var);
   o.varor = uni(o.varor);
   o.mwor = uni(o.mwor);
@@ -811,7 +844,7 @@ __device__ __forceinline__ void encode_mb(const p64gpu_encode_args &a, const uin
   if (MODE != 0) {
     __syncthreads();
     SECTION("e_me");
-    const MeOut me = motion_estimate<MODE>(L, cur.y, w, h, x0, y0, a.search_limit, lane);
+    const MeOut me = motion_estimate<Geo1, MODE>(sx_of(L), cur.y, w, h, x0, y0, a.search_limit, lane);
     if (a.me && lane == 0) {
       p64_me_rec o;
       o.mx = me.mx;
@@ -956,7 +989,7 @@ __global__ __launch_bounds__(64, 1) void k_motion(int w, int h, int64_t stride, 
            lane);
   __syncthreads();
   SECTION("m_fetched");
-  const MeOut me = motion_estimate<MODE>(L, cur_y + (size_t)fi * stride, w, h, x0, y0, sl, lane);
+  const MeOut me = motion_estimate<Geo1, MODE>(sx_of(L), cur_y + (size_t)fi * stride, w, h, x0, y0, sl, lane);
   SECTION("m_me_done");
   if (lane == 0) {
     p64_me_rec o;
@@ -970,6 +1003,7 @@ __global__ __launch_bounds__(64, 1) void k_motion(int w, int h, int64_t stride, 
     out[gid] = o;
   }
 }
+
 
 }  // namespace
 

@@ -13,6 +13,6 @@ for lib in "$@"; do
 import csv,sys
 for r in csv.DictReader(sys.stdin):
     n=r['Name'].replace('(anonymous namespace)::','').split('(')[0]
-    if 'k_motion' in n: print(f\"$tag $c {n:16s} calls {int(r['Calls']):4d} avg {float(r['AverageNs'])/1e3:8.1f} us  min {float(r['MinNs'])/1e3:8.1f}\")"
+    if 'k_motion' in n or 'tile' in n: print(f\"$tag $c {n:16s} calls {int(r['Calls']):4d} avg {float(r['AverageNs'])/1e3:8.1f} us  min {float(r['MinNs'])/1e3:8.1f}\")"
   done
 done
