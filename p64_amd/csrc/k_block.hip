@@ -520,15 +520,24 @@ __device__ __forceinline__ RecStageB rec_stage_b(const RecBufs &B, int w, int h,
   const uint32_t po = S.inter ? (uint32_t)((int64_t)p.fi * stride) + (uint32_t)plane_offset(p.plane, w, h) +
                                     (uint32_t)(mul24(sy, pw) + (sx & ~3))
                               : BUF_OOB;
-  // the third dword only when the row is misaligned (then it lies inside the
-  // row: sx <= pw - 9); an aligned row at the plane's end would reach past it
-  const uint32_t po3 = S.pred.sh ? po + 8 : BUF_OOB;
+  // rows 0..6 as 12-byte loads (the third dword matters only when the row is
+  // misaligned; otherwise it is the start of the next row, inside the
+  // buffer); row 7 takes its third dword only when misaligned (then it lies
+  // inside the row: sx <= pw - 9) -- an aligned last row at the end of the
+  // buffer would reach past it
 #pragma unroll
-  for (int k = 0; k < 8; k++) {
-    const auto v = __builtin_amdgcn_raw_buffer_load_b64(B.ref, po + (uint32_t)mul24(k, pw), 0, 0);
+  for (int k = 0; k < 7; k++) {
+    const auto v = __builtin_amdgcn_raw_buffer_load_b96(B.ref, po + (uint32_t)mul24(k, pw), 0, 0);
     S.pred.d[k][0] = v[0];
     S.pred.d[k][1] = v[1];
-    S.pred.d[k][2] = __builtin_amdgcn_raw_buffer_load_b32(B.ref, po3 + (uint32_t)mul24(k, pw), 0, 0);
+    S.pred.d[k][2] = v[2];
+  }
+  {
+    const uint32_t o7 = po + (uint32_t)mul24(7, pw);
+    const auto v = __builtin_amdgcn_raw_buffer_load_b64(B.ref, o7, 0, 0);
+    S.pred.d[7][0] = v[0];
+    S.pred.d[7][1] = v[1];
+    S.pred.d[7][2] = __builtin_amdgcn_raw_buffer_load_b32(B.ref, S.pred.sh ? o7 + 8 : BUF_OOB, 0, 0);
   }
   // the levels after the prediction source: the prediction is formed first,
   // and wait counts are in issue order
@@ -740,12 +749,14 @@ __global__ __launch_bounds__(256) INTER_OCC void k_inter_mbg(p64gpu_encode_args 
       __builtin_amdgcn_make_buffer_rsrc((void *)me, (short)0, (int)(nmbs * sizeof(p64_me_rec)), BUF_RSRC_W3);
   const uint32_t mo = gmb * (uint32_t)sizeof(p64_me_rec);
   InterMe m;
-  m.mx = (int)__builtin_amdgcn_raw_buffer_load_b32(mer, mo + 0, 0, 0);
-  m.my = (int)__builtin_amdgcn_raw_buffer_load_b32(mer, mo + 4, 0, 0);
-  m.sad = (int)__builtin_amdgcn_raw_buffer_load_b32(mer, mo + 8, 0, 0);
-  m.sad0 = (int)__builtin_amdgcn_raw_buffer_load_b32(mer, mo + 12, 0, 0);
-  m.var = (int)__builtin_amdgcn_raw_buffer_load_b32(mer, mo + 16, 0, 0);
-  m.varor = (int)__builtin_amdgcn_raw_buffer_load_b32(mer, mo + 20, 0, 0);
+  const auto r0 = __builtin_amdgcn_raw_buffer_load_b128(mer, mo, 0, 0);    // mx my sad sad0
+  const auto r1 = __builtin_amdgcn_raw_buffer_load_b64(mer, mo + 16, 0, 0);  // var varor
+  m.mx = (int)r0[0];
+  m.my = (int)r0[1];
+  m.sad = (int)r0[2];
+  m.sad0 = (int)r0[3];
+  m.var = (int)r1[0];
+  m.varor = (int)r1[1];
   // LastIntra and the -o override by buffer loads (an absent override array
   // reads as out of range: no branch around a load)
   const __amdgpu_buffer_rsrc_t lir =
