@@ -281,8 +281,7 @@ def cpu_baselines(args, legs):
         return {leg: cpu_port(args, p64_amd, w, h, nmb) for leg in legs if leg in ("inter", "4cif")}
     with tempfile.TemporaryDirectory() as td:
         for k in range(procs):
-            frames = [p64_amd.synth_frame(1 + k, t, w, h) for t in range(nfr)]
-            write_y4m(os.path.join(td, f"s{k}.y4m"), frames, w, h)
+            write_y4m(os.path.join(td, f"s{k}.y4m"), host_frames(p64_amd, args.content, 1 + k, nfr, w, h), w, h)
         env = dict(os.environ)
         env.pop("P64REF_DUMP", None)
 
@@ -290,7 +289,8 @@ def cpu_baselines(args, legs):
             return [[hook, fmt, "-y4m", "-a", "0", "-b", str(nfr - 1), "-q", str(args.quant),
                      "-i", str(args.search_limit), *extra, os.path.join(td, f"s{k}"), "-z", ".y4m",
                      "-s", os.path.join(td, f"s{k}.p64")] for k in range(n)]
-        desc = f"{nfr}-picture {w}x{h} y4m sequence per process (same generator), q={args.quant}"
+        desc = (f"{nfr}-picture {w}x{h} y4m sequence per process (content {args.content}, host "
+                f"generator{'' if args.content == 'synth' else ' of the same kind'}), q={args.quant}")
         if "inter" in legs or "decode" in legs:
             me = "FastBME SL=%d" % args.search_limit if args.mode == "full" else "StepBME (TSS)"
             env_i = dict(env, P64REF_ME="full") if args.mode == "full" else env
@@ -318,13 +318,41 @@ def cpu_baselines(args, legs):
     return out
 
 
+def host_frames(p64_amd, content, seed, n, w, h):
+    """Host pictures for the CPU legs: the synth generator (the same bytes as the
+    device one), or the stress contents of make_inputs in kind -- uniform noise,
+    one constant per sequence, picture 0 panned by +-15 px per picture with
+    +-3 noise (numpy, seeded; the device versions draw from torch's generator)."""
+    import numpy as np
+    if content == "synth":
+        return [p64_amd.synth_frame(seed, t, w, h) for t in range(n)]
+    pic = w * h * 3 // 2
+    rng = np.random.default_rng(1000 + seed)
+    if content == "noise":
+        return [rng.integers(0, 256, pic, dtype=np.uint8) for _ in range(n)]
+    if content == "flat":
+        return [np.full(pic, (seed * 37 + 1) % 224 + 16, np.uint8) for _ in range(n)]
+    base = p64_amd.synth_frame(seed, 0, w, h)
+    vx, vy = (15 if seed % 2 == 0 else -15), (15 if (seed // 2) % 2 == 0 else -15)
+    planes = ((0, w, h, 1), (w * h, w // 2, h // 2, 2), (w * h + w * h // 4, w // 2, h // 2, 2))
+    out = []
+    for t in range(n):
+        f = np.empty(pic, np.uint8)
+        for off, pw, ph, div in planes:
+            src = base[off:off + pw * ph].reshape(ph, pw).astype(np.int16)
+            moved = np.roll(src, (t * vy // div, t * vx // div), (0, 1))
+            f[off:off + pw * ph] = (moved + rng.integers(-3, 4, moved.shape)).clip(0, 255).reshape(-1)
+        out.append(f)
+    return out
+
+
 def cpu_port(args, p64_amd, w, h, nmb):
     """The clean-room port (scalar, one core) where the reference has no path."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle
 
     n = min(args.cpu_frames, 12 if nmb <= 396 else 4)
-    frames = [p64_amd.synth_frame(1, t, w, h) for t in range(n)]
+    frames = host_frames(p64_amd, args.content, 1, n, w, h)
     t0 = time.perf_counter()
     oracle.encode_sequence(frames, w, h, quant=args.quant, me_mode=1 if args.mode == "full" else 0,
                            search_limit=args.search_limit)
@@ -483,7 +511,7 @@ def main(argv=None):
         return dry_main(args, rank, world)
 
     cpus = {}
-    if rank == 0 and world == 1 and not args.no_cpu and args.content == "synth":
+    if rank == 0 and world == 1 and not args.no_cpu:
         legs = {"inter": ["inter"] + ([] if args.no_extra else ["intra", "decode"]),
                 "4cif": ["inter"], "intra": ["intra"], "decode": ["decode"]}[args.config]
         cpus = cpu_baselines(args, legs)
