@@ -475,8 +475,16 @@ static inline BlkDiv blk_div(int w, int h) {
 }
 __device__ __forceinline__ unsigned mdiv(unsigned n, uint32_t m, uint32_t s) { return __umulhi(n, m) >> s; }
 
+// dword 3 of a raw buffer resource on gfx9-family parts (CDNA): 32-bit data format
+constexpr int BUF_RSRC_W3 = 0x00020000;
+constexpr uint32_t BUF_OOB = 0x80000000u;  // >= every buffer's num_records: loads 0, stores dropped
+
 // MB-grouped block layout (k_block.hip): a wave takes 10 consecutive
 // macroblocks, lane 6m + b block b of its m-th MB (lanes 60..63 idle)
 constexpr int MBS_PER_WAVE = 10;
+// waves per workgroup of those kernels (each wave is independent)
+#ifndef MBG_WAVES
+#define MBG_WAVES 4u
+#endif
 
 }  // namespace

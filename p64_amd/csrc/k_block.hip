@@ -306,10 +306,6 @@ __device__ __forceinline__ void put_levels(uint8_t *lds, int lane, int k, uint4 
   *reinterpret_cast<uint4 *>(lds + lane * LVL_STRIDE + k * 16) = v;
 }
 
-// dword 3 of a raw buffer resource on gfx9-family parts (CDNA): 32-bit data format
-constexpr int BUF_RSRC_W3 = 0x00020000;
-constexpr uint32_t BUF_OOB = 0x80000000u;  // >= every buffer's num_records: loads 0, stores dropped
-
 struct IntraFetch {
   BlkPos p;
   uint2 rows[8];  // the block's pixels
@@ -425,11 +421,11 @@ __device__ __forceinline__ void mbg_store(const p64gpu_encode_args &a, const uin
 // intra picture, MB-grouped block layout (blk_pos_mb): one wave = 10 MBs, a
 // lane per block; levels leave as one contiguous 7,680-byte run per wave
 template <bool QMB>
-__global__ __launch_bounds__(256) void k_intra_mbg(p64gpu_encode_args a, BlkDiv kd, unsigned nmbs) {
-  __shared__ __align__(16) uint8_t lvl[4 * LVL_WAVE];
+__global__ __launch_bounds__(64 * MBG_WAVES) void k_intra_mbg(p64gpu_encode_args a, BlkDiv kd, unsigned nmbs) {
+  __shared__ __align__(16) uint8_t lvl[MBG_WAVES * LVL_WAVE];
   const int lane = threadIdx.x & 63;
   uint8_t *lds = lvl + (threadIdx.x >> 6) * LVL_WAVE;
-  const unsigned gmb0 = (xcd_remap(blockIdx.x, gridDim.x) * 4u + (threadIdx.x >> 6)) * MBS_PER_WAVE;
+  const unsigned gmb0 = (xcd_remap(blockIdx.x, gridDim.x) * MBG_WAVES + (threadIdx.x >> 6)) * MBS_PER_WAVE;
   if (gmb0 >= nmbs) return;  // whole wave
   PRIO_HIGH();
   const int l = min(lane, 6 * MBS_PER_WAVE - 1);
@@ -636,6 +632,13 @@ __device__ __forceinline__ void rec_block_pk(int w, int h, int64_t stride, __amd
 // occupancy targets: 4 waves per SIMD (<= 128 VGPRs)
 #define INTER_OCC __attribute__((amdgpu_waves_per_eu(4)))
 #define RECON_OCC __attribute__((amdgpu_waves_per_eu(4)))
+// the decoder's waves each form a workgroup of their own: a freed wave slot
+// takes the next wave at once instead of waiting for three others to free
+// theirs (-1.5 us on a launch of ~35; the encoders, whose waves finish more
+// evenly, keep 4-wave workgroups: 1-wave groups cost k_intra_mbg 2.5 us)
+#ifndef REC_WAVES
+#define REC_WAVES 1u
+#endif
 // decoder reconstruction, MB-grouped block layout (blk_pos_mb), one block per
 // lane and no loop: 10 MBs per wave, each lane loads its MB's record, then its
 // levels and prediction, reconstructs and stores.  Without the persistent
@@ -643,12 +646,12 @@ __device__ __forceinline__ void rec_block_pk(int w, int h, int64_t stride, __amd
 // waves hide each other's two dependent load latencies (measured faster than
 // k_recon_blk, whose 237 VGPRs allow 2).  Lanes past the batch (and lanes
 // 60..63) get coded = 0: every load and store of theirs is out of range.
-__global__ __launch_bounds__(256) RECON_OCC void k_recon_mbg(int w, int h, int64_t stride, const uint8_t *refp,
+__global__ __launch_bounds__(64 * REC_WAVES) RECON_OCC void k_recon_mbg(int w, int h, int64_t stride, const uint8_t *refp,
                                                            uint8_t *recp, const int16_t *coef,
                                                            const p64_mb_rec *mbr, const uint8_t *quant_mb,
                                                            const uint8_t *coded_mask, BlkDiv kd, unsigned nmbs) {
   const int lane = threadIdx.x & 63;
-  const unsigned gmb0 = (xcd_remap(blockIdx.x, gridDim.x) * 4u + (threadIdx.x >> 6)) * MBS_PER_WAVE;
+  const unsigned gmb0 = (xcd_remap(blockIdx.x, gridDim.x) * REC_WAVES + (threadIdx.x >> 6)) * MBS_PER_WAVE;
   if (gmb0 >= nmbs) return;  // whole wave
   const int nmb = (w >> 4) * (h >> 4), nfr = (int)(nmbs / (unsigned)nmb);
   RecBufs B;
@@ -728,12 +731,12 @@ __device__ __forceinline__ void pred_rows(const PredSrc &P, bool filter, uint2 p
   }
 }
 template <bool QMB>
-__global__ __launch_bounds__(256) INTER_OCC void k_inter_mbg(p64gpu_encode_args a, BlkDiv kd, unsigned nmbs,
+__global__ __launch_bounds__(64 * MBG_WAVES) INTER_OCC void k_inter_mbg(p64gpu_encode_args a, BlkDiv kd, unsigned nmbs,
                                                              const p64_me_rec *me) {
-  __shared__ __align__(16) uint8_t lvl[4 * LVL_WAVE];
+  __shared__ __align__(16) uint8_t lvl[MBG_WAVES * LVL_WAVE];
   const int lane = threadIdx.x & 63;
   uint8_t *lds = lvl + (threadIdx.x >> 6) * LVL_WAVE;
-  const unsigned gmb0 = (xcd_remap(blockIdx.x, gridDim.x) * 4u + (threadIdx.x >> 6)) * MBS_PER_WAVE;
+  const unsigned gmb0 = (xcd_remap(blockIdx.x, gridDim.x) * MBG_WAVES + (threadIdx.x >> 6)) * MBS_PER_WAVE;
   if (gmb0 >= nmbs) return;  // whole wave
   const int w = a.width, h = a.height, nmb = (w >> 4) * (h >> 4), nfr = (int)(nmbs / (unsigned)nmb);
   const int64_t stride = a.frame_stride;
@@ -868,18 +871,18 @@ __global__ __launch_bounds__(256) INTER_OCC void k_inter_mbg(p64gpu_encode_args 
 
 namespace p64k {
 
-static unsigned mbg_workgroups(unsigned nmbs) {
+static unsigned mbg_workgroups(unsigned nmbs, unsigned per = MBG_WAVES) {
   const unsigned waves = (nmbs + MBS_PER_WAVE - 1) / MBS_PER_WAVE;
-  return (waves + 3) / 4;
+  return (waves + per - 1) / per;
 }
 
 hipError_t intra_mbg(const p64gpu_encode_args &a, hipStream_t st) {
   const unsigned nm = (unsigned)((int64_t)a.nframes * (a.width / 16) * (a.height / 16));
   if (a.quant_mb)
-    hipLaunchKernelGGL(k_intra_mbg<true>, dim3(mbg_workgroups(nm)), dim3(256), 0, st, a,
+    hipLaunchKernelGGL(k_intra_mbg<true>, dim3(mbg_workgroups(nm)), dim3(64 * MBG_WAVES), 0, st, a,
                        blk_div(a.width, a.height), nm);
   else
-    hipLaunchKernelGGL(k_intra_mbg<false>, dim3(mbg_workgroups(nm)), dim3(256), 0, st, a,
+    hipLaunchKernelGGL(k_intra_mbg<false>, dim3(mbg_workgroups(nm)), dim3(64 * MBG_WAVES), 0, st, a,
                        blk_div(a.width, a.height), nm);
   return hipGetLastError();
 }
@@ -887,10 +890,10 @@ hipError_t intra_mbg(const p64gpu_encode_args &a, hipStream_t st) {
 hipError_t inter_mbg(const p64gpu_encode_args &a, const p64_me_rec *me, hipStream_t st) {
   const unsigned nm = (unsigned)((int64_t)a.nframes * (a.width / 16) * (a.height / 16));
   if (a.quant_mb)
-    hipLaunchKernelGGL(k_inter_mbg<true>, dim3(mbg_workgroups(nm)), dim3(256), 0, st, a,
+    hipLaunchKernelGGL(k_inter_mbg<true>, dim3(mbg_workgroups(nm)), dim3(64 * MBG_WAVES), 0, st, a,
                        blk_div(a.width, a.height), nm, me);
   else
-    hipLaunchKernelGGL(k_inter_mbg<false>, dim3(mbg_workgroups(nm)), dim3(256), 0, st, a,
+    hipLaunchKernelGGL(k_inter_mbg<false>, dim3(mbg_workgroups(nm)), dim3(64 * MBG_WAVES), 0, st, a,
                        blk_div(a.width, a.height), nm, me);
   return hipGetLastError();
 }
@@ -899,7 +902,7 @@ hipError_t recon_mbg(int w, int h, int nframes, int64_t stride, const uint8_t *r
                      const int16_t *coef, const p64_mb_rec *mb, const uint8_t *quant_mb,
                      const uint8_t *coded_mask, hipStream_t st) {
   const unsigned nm = (unsigned)((int64_t)nframes * (w / 16) * (h / 16));
-  hipLaunchKernelGGL(k_recon_mbg, dim3(mbg_workgroups(nm)), dim3(256), 0, st, w, h, stride, ref, recon,
+  hipLaunchKernelGGL(k_recon_mbg, dim3(mbg_workgroups(nm, REC_WAVES)), dim3(64 * REC_WAVES), 0, st, w, h, stride, ref, recon,
                      coef, mb, quant_mb, coded_mask, blk_div(w, h), nm);
   return hipGetLastError();
 }

@@ -78,9 +78,12 @@ __device__ __forceinline__ void wsync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// The search window (zero outside the picture: such candidates are never
-// valid, me.c:212/292) and the current luma block, fetched into registers
+// The search window and the current luma block, fetched into registers
 // (LumaFetch) one macroblock ahead of its use, then stored to LDS (put_luma).
+// Buffer loads over the luma plane, no bounds test: segments above or below
+// the picture read zeros (offset out of range), segments left or right of it
+// the neighbouring rows' pixels -- neither is part of any valid candidate
+// (me.c:212/292) or of the prediction of a valid vector.
 constexpr int WIN_SEGS = WIN_ROWS * 3, WIN_NIT = (WIN_SEGS + 63) / 64;  // 16-byte segments
 struct LumaFetch {
   uint4 v[WIN_NIT];
@@ -88,18 +91,15 @@ struct LumaFetch {
 };
 __device__ __forceinline__ LumaFetch fetch_luma(const uint8_t *ref_y, const uint8_t *cur_y, int w,
                                                 int h, int x0, int y0, int lane) {
-  // interior macroblocks (the whole window inside the picture) skip the
-  // per-segment bounds test
-  const bool inside = y0 >= WIN_OY && y0 - WIN_OY + WIN_ROWS <= h && x0 >= WIN_OX &&
-                      x0 - WIN_OX + WIN_BYTES <= w;
+  const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc((void *)ref_y, (short)0, w * h, BUF_RSRC_W3);
+  const int base = (y0 - WIN_OY) * w + x0 - WIN_OX;  // (negative above the picture: out of range)
   LumaFetch f;
 #pragma unroll
   for (int i = 0; i < WIN_NIT; i++) {
     const int t = lane + 64 * i, row = t / 3, seg = t - row * 3;
-    const int gy = y0 - WIN_OY + row, gx = x0 - WIN_OX + seg * 16;
-    f.v[i] = make_uint4(0, 0, 0, 0);
-    if (t < WIN_SEGS && (inside || (gy >= 0 && gy < h && gx >= 0 && gx < w)))
-      f.v[i] = *reinterpret_cast<const uint4 *>(ref_y + (uint32_t)(mul24(gy, w) + gx));
+    const uint32_t off = (64 * i + 63 < WIN_SEGS || t < WIN_SEGS) ? (uint32_t)(base + mul24(row, w) + 16 * seg) : BUF_OOB;
+    const auto v = __builtin_amdgcn_raw_buffer_load_b128(rr, off, 0, 0);
+    f.v[i] = make_uint4(v[0], v[1], v[2], v[3]);
   }
   f.c = *reinterpret_cast<const uint32_t *>(cur_y + (uint32_t)(mul24(y0 + (lane >> 2), w) + x0 + 4 * (lane & 3)));
   return f;
@@ -298,7 +298,8 @@ __device__ __forceinline__ void sad_zero_hf(const Sx &S, int lane, int &sad0, in
   const uint32_t r = S.win[(WIN_OY + (lane >> 2)) * G::WS + WIN_OX / 4 + (lane & 3)];
   const uint32_t c = S.cur[lane];
   const uint32_t m = reinterpret_cast<const uint8_t *>(S.cpred)[4 * (lane >> 4) + (lane & 3)];
-  const int t = wave_sum((int)(sad4(r, c, 0u) | (sad4(c, m * 0x01010101u, 0u) << 16)));
+  const uint32_t m4 = __builtin_amdgcn_perm(0u, m, 0x00000000u);  // m in every byte (not the quarter-rate v_mul_lo)
+  const int t = wave_sum((int)(sad4(r, c, 0u) | (sad4(c, m4, 0u) << 16)));
   sad0 = t & 0xffff;
   ehf = (int)((unsigned)t >> 16);
 }
@@ -404,16 +405,21 @@ __device__ __forceinline__ void me_full(const Sx &S, const uint8_t *cur_blk, int
   const int dlo = max(-hl, -y0) + 15 - 15 * half, dhi = min(hl, h - 16 - y0) + 15 - 15 * half;
   const bool all_rows = dlo <= 0 && dhi >= 15;
   const bool interior = uni(__all(!lane_ok || (col_ok && all_rows)));
-  auto init = [&](uint32_t *a) {
-    if (interior) {  // one select for all
-      const uint32_t v = lane_ok ? 0u : ME_INVALID;
+  // the sums start at 0; invalid candidates are marked afterwards (bit 19 of a
+  // sum < 2^17): interior macroblocks only mask the two idle lanes, the others
+  // OR in the lane's invalid rows, ~valid [dlo, dhi) (or every row)
+  uint32_t inv = 0;
+  if (!interior) {
+    const int lo = min(max(dlo, 0), 15), hi = min(max(dhi, 0), 15);
+    inv = ~((col_ok && hi > lo) ? (1u << hi) - (1u << lo) : 0u);
+  }
+  auto mark_invalid = [&](uint32_t *a) {
+    if (!interior) {
 #pragma unroll
-      for (int d = 0; d < 15; d++) a[d] = v;
-    } else {
-#pragma unroll
-      for (int d = 0; d < 15; d++) a[d] = (col_ok && d >= dlo && d < dhi) ? 0u : ME_INVALID;
+      for (int d = 0; d < 15; d++) a[d] |= ((inv >> d) & 1u) << 19;
     }
   };
+  static_assert(ME_INVALID == 1u << 19, "invalid mark");
   const unsigned base = ((unsigned)dxi << 5) + (unsigned)(15 * half) + 1u;  // ord of d = 0
 
   SECTION("cur_map");
@@ -443,7 +449,8 @@ __device__ __forceinline__ void me_full(const Sx &S, const uint8_t *cur_blk, int
     build_lb_map(S, lane);
     wsync();
     SECTION("lb_pass");
-    init(acc);
+#pragma unroll
+    for (int d = 0; d < 15; d++) acc[d] = 0;
     {
       const int xq = colb >> 2;
       const uint32_t *mrow = S.map + ((colb & 3) * G::MAP_PLANE + 15 * half * G::MAP_ROW) / 4 + (xq >> 2);
@@ -459,6 +466,7 @@ __device__ __forceinline__ void me_full(const Sx &S, const uint8_t *cur_blk, int
         }
       }
     }
+    mark_invalid(acc);
 
     // 2. c* and its full SAD
     SECTION("cstar");
@@ -466,6 +474,7 @@ __device__ __forceinline__ void me_full(const Sx &S, const uint8_t *cur_blk, int
       unsigned m = 0xFFFFFFFFu;
 #pragma unroll
       for (int d = 0; d < 15; d++) m = min(m, (acc[d] << 4) | (unsigned)d);
+      if (!lane_ok) m = ME_INVALID << 4;
       pk = m == 0xFFFFFFFFu ? m : ((m >> 4) << KEY_SHIFT) + base + (m & 15u);
     }
     pk = uni((int)wave_min(pk));
@@ -484,6 +493,7 @@ __device__ __forceinline__ void me_full(const Sx &S, const uint8_t *cur_blk, int
     // 3. survivors: their ords compacted into L.list with ballot + mbcnt (the
     // first ME_LIST_MAX of them), counted on the way
     nsurv = 0;
+    if (lane_ok) {  // (the two idle lanes sit out: their sums are not masked)
 #pragma unroll
     for (int d = 0; d < 15; d++) {
       const bool sv = acc[d] <= Ts;
@@ -494,6 +504,7 @@ __device__ __forceinline__ void me_full(const Sx &S, const uint8_t *cur_blk, int
         if (sv && idx < ME_LIST_MAX) list[idx] = base + d;
         nsurv += __popcll(bl);
       }
+    }
     }
     nsurv = uni(nsurv);
   }
@@ -518,15 +529,18 @@ __device__ __forceinline__ void me_full(const Sx &S, const uint8_t *cur_blk, int
     const uint32_t *wrow = S.win + (15 * half) * G::WS + (colb >> 2);
     const int sh = colb & 3;
     uint32_t cs[64];
-    init(acc);
+#pragma unroll
+    for (int d = 0; d < 15; d++) acc[d] = 0;
     // (in two chunks of 8 rows: all 16 in SGPRs raise the kernel's SGPR
     // count past 80 and cost every macroblock a wave slot per SIMD)
     load_cur_rows8<0>(cur_blk, w, cs);
     full_rows<G, 0, 8, 0, 22>(wrow, sh, cs, acc);
     load_cur_rows8<8>(cur_blk, w, cs);
     full_rows<G, 8, 16, 8, 30>(wrow, sh, cs, acc);
+    mark_invalid(acc);
 #pragma unroll
     for (int d = 0; d < 15; d++) bk = min(bk, (acc[d] << KEY_SHIFT) + base + d);
+    if (!lane_ok) bk = 0xFFFFFFFFu;
     bk = wave_min(bk);
   }
 
