@@ -1,6 +1,7 @@
 """Per-wave timeline of the block-layout kernels (development aid, never
 shipped): writes abtest/k_block_stamp.hip, a copy of k_block.hip whose
-kernels stamp s_memrealtime (100 MHz) at wave start (T0), once the first
+kernels stamp s_memrealtime (100 MHz) at wave start (T0, with the wave's XCD in
+bits 56..59), once the first
 loads have arrived (T1, after an s_waitcnt 0), before the stores (T2) and
 once the stores have completed (T3), into a device array read back through
 p64dbg_stamps().  Build with tools/ablib.sh stamp abtest/k_block_stamp.hip
@@ -23,9 +24,13 @@ __device__ unsigned long long g_stamp[4u << 16];
 #define STAMP(k)                                                                 \\
   do {                                                                           \\
     if ((threadIdx.x & 63) == 0)                                                 \\
-      g_stamp[4u * (blockIdx.x * 4u + (threadIdx.x >> 6)) + (k)] = __builtin_amdgcn_s_memrealtime(); \\
+      g_stamp[4u * (blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) + (k)] =                    \\
+          __builtin_amdgcn_s_memrealtime() |                                                           \\
+          ((k) == 0 ? (unsigned long long)__builtin_amdgcn_s_getreg(XCC_ID_REG) << 56 : 0ull);        \\
   } while (0)
 #define WAIT_ALL() __builtin_amdgcn_s_waitcnt(0)
+// s_getreg HW_REG_XCC_ID (gfx940+: hwreg 20, bits 3:0): the XCD the wave runs on
+#define XCC_ID_REG ((3 << 11) | 20)
 """)
 # intra
 sub("""  if (gmb0 >= nmbs) return;  // whole wave

@@ -28,12 +28,15 @@ def grab(nw):
     L.p64dbg_stamps_clear()
     t = buf.reshape(nw, 4).astype(np.int64)
     t = t[t[:, 0] > 0]
+    xcd = t[:, 0] >> 56
+    t[:, 0] &= (1 << 56) - 1
     t0 = t[:, 0].min()
-    return (t - t0) / 100.0  # 100 MHz -> us
+    return np.concatenate([(t - t0) / 100.0, xcd[:, None]], axis=1)  # 100 MHz -> us; column 4 = XCD
 
 
 def report(name, t):
     span = t[:, 3].max()
+    t = t.copy()
     ld, cp, st = t[:, 1] - t[:, 0], t[:, 2] - t[:, 1], t[:, 3] - t[:, 2]
     q = lambda a: " ".join(f"{x:6.2f}" for x in np.percentile(a, [10, 50, 90]))  # noqa: E731
     print(f"== {name}: {len(t)} waves, span {span:.1f} us")
@@ -47,7 +50,8 @@ def report(name, t):
         a = ((t[:, 0] <= mid) & (t[:, 1] > mid)).sum()
         b = ((t[:, 1] <= mid) & (t[:, 2] > mid)).sum()
         c = ((t[:, 2] <= mid) & (t[:, 3] > mid)).sum()
-        print(f"   t={mid:6.1f}  loading {a:5d}  computing {b:5d}  storing {c:5d}")
+        per = [int(((t[:, 0] <= mid) & (t[:, 3] > mid) & (t[:, 4] == x)).sum()) for x in range(8)]
+        print(f"   t={mid:6.1f}  loading {a:5d}  computing {b:5d}  storing {c:5d}   per XCD {per}")
 
 
 def main():
@@ -74,14 +78,14 @@ def main():
         p64_amd.encode_frames(fr[0].reshape(-1), None, r0, li, width=w, height=h, intra=True, quant=8)
     grab(nw)
     p64_amd.encode_frames(fr[0].reshape(-1), None, r0, li, width=w, height=h, intra=True, quant=8)
-    report("k_intra_mbg", grab(nw))
+    report("k_intra_mbg", grab(nw + 4))
     o = p64_amd.encode_frames(fr[1].reshape(-1), r0, r1, li, width=w, height=h, intra=False, quant=8,
                               me_mode=p64_amd.ME_FULL, search_limit=31)
-    report("k_inter_mbg", grab(nw))
+    report("k_inter_mbg", grab(nw + 4))
     qmb = torch.full((S * nmb,), 8, dtype=torch.uint8, device="cuda")
     d = torch.empty_like(r1)
     p64_amd.decode_recon(r0, d, o.coef, o.mb, qmb, torch.ones_like(qmb), width=w, height=h)
-    report("k_recon_mbg", grab(nw))
+    report("k_recon_mbg", grab(nw + 4))
 
 
 if __name__ == "__main__":
