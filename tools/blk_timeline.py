@@ -35,6 +35,8 @@ def grab(nw):
 
 
 def report(name, t):
+    if os.environ.get("TL_SAVE"):  # raw per-wave rows for offline analysis
+        np.save(os.path.join(os.environ["TL_SAVE"], name.replace("<", "_").replace(">", "") + ".npy"), t)
     span = t[:, 3].max()
     t = t.copy()
     ld, cp, st = t[:, 1] - t[:, 0], t[:, 2] - t[:, 1], t[:, 3] - t[:, 2]
