@@ -378,11 +378,11 @@ __device__ __forceinline__ void intra_block(const p64gpu_encode_args &a, const I
 // (nvalid MBs x 768 bytes at coef + gmb0 x 768) from the LDS staging, the
 // lane's 8 reconstructed rows (rec_off, plane width pw), and from the record
 // lanes (rl) the MB record dword and the LastIntra byte of MB gmb
-__device__ __forceinline__ void mbg_store(const p64gpu_encode_args &a, const uint8_t *lds, int lane,
+__device__ __forceinline__ void mbg_store(const p64gpu_encode_args &a, const BlkDiv &kd, const uint8_t *lds, int lane,
                                           unsigned nmbs, unsigned gmb0, uint32_t nvalid, uint32_t rec_off,
                                           int pw, const uint2 rows[8], bool rl, unsigned gmb, uint32_t mbw,
                                           uint8_t li) {
-  const int nfr = (int)(nmbs / (unsigned)((a.width >> 4) * (a.height >> 4)));
+  const int nfr = (int)mdiv(nmbs, kd.mn, kd.sn);
   const __amdgpu_buffer_rsrc_t coef =
       __builtin_amdgcn_make_buffer_rsrc((void *)a.coef, (short)0, (int)(nmbs * 768u), BUF_RSRC_W3);
   const uint32_t nbytes = nvalid * 768u;
@@ -438,7 +438,7 @@ __global__ __launch_bounds__(64 * MBG_WAVES) void k_intra_mbg(p64gpu_encode_args
   // the MB's record and LastIntra (p64.c:909-910: MTYPE 0, CBP 0x3f, LastIntra
   // reset) from lane b = 0 of each MB
   const bool rl = l % 6 == 0 && lane < 6 * MBS_PER_WAVE && gmb0 + (unsigned)(l / 6) < nmbs;
-  mbg_store(a, lds, lane, nmbs, gmb0, nvalid, o.rec_off, o.pw, o.rec, rl, gmb, 0x3f00u, 0);
+  mbg_store(a, kd, lds, lane, nmbs, gmb0, nvalid, o.rec_off, o.pw, o.rec, rl, gmb, 0x3f00u, 0);
 }
 // The source of an 8x8 prediction at (x, y) of a plane (any byte alignment):
 // three aligned dwords per row (the third only matters when the row is
@@ -653,7 +653,8 @@ __global__ __launch_bounds__(64 * REC_WAVES) RECON_OCC void k_recon_mbg(int w, i
   const int lane = threadIdx.x & 63;
   const unsigned gmb0 = (xcd_remap(blockIdx.x, gridDim.x) * REC_WAVES + (threadIdx.x >> 6)) * MBS_PER_WAVE;
   if (gmb0 >= nmbs) return;  // whole wave
-  const int nmb = (w >> 4) * (h >> 4), nfr = (int)(nmbs / (unsigned)nmb);
+  PRIO_HIGH();
+  const int nmb = (w >> 4) * (h >> 4), nfr = (int)mdiv(nmbs, kd.mn, kd.sn);
   RecBufs B;
   B.ref = __builtin_amdgcn_make_buffer_rsrc((void *)refp, (short)0, (int)(nfr * stride), BUF_RSRC_W3);
   B.coef = __builtin_amdgcn_make_buffer_rsrc((void *)coef, (short)0, nfr * nmb * 768, BUF_RSRC_W3);
@@ -662,7 +663,6 @@ __global__ __launch_bounds__(64 * REC_WAVES) RECON_OCC void k_recon_mbg(int w, i
   B.mask = __builtin_amdgcn_make_buffer_rsrc((void *)coded_mask, (short)0, nfr * nmb, BUF_RSRC_W3);
   const __amdgpu_buffer_rsrc_t rec =
       __builtin_amdgcn_make_buffer_rsrc((void *)recp, (short)0, (int)(nfr * stride), BUF_RSRC_W3);
-  PRIO_HIGH();
   const int l = min(lane, 6 * MBS_PER_WAVE - 1);
   const unsigned g = gmb0 + (unsigned)(l / 6);
   const bool valid = lane < 6 * MBS_PER_WAVE && g < nmbs;
@@ -738,11 +738,11 @@ __global__ __launch_bounds__(64 * MBG_WAVES) INTER_OCC void k_inter_mbg(p64gpu_e
   uint8_t *lds = lvl + (threadIdx.x >> 6) * LVL_WAVE;
   const unsigned gmb0 = (xcd_remap(blockIdx.x, gridDim.x) * MBG_WAVES + (threadIdx.x >> 6)) * MBS_PER_WAVE;
   if (gmb0 >= nmbs) return;  // whole wave
-  const int w = a.width, h = a.height, nmb = (w >> 4) * (h >> 4), nfr = (int)(nmbs / (unsigned)nmb);
+  PRIO_HIGH();  // first: a fresh wave's loads go out before the older waves' arithmetic
+  const int w = a.width, h = a.height, nfr = (int)mdiv(nmbs, kd.mn, kd.sn);
   const int64_t stride = a.frame_stride;
   RecBufs B;
   B.ref = __builtin_amdgcn_make_buffer_rsrc((void *)a.ref, (short)0, (int)(nfr * stride), BUF_RSRC_W3);
-  PRIO_HIGH();
   const int l = min(lane, 6 * MBS_PER_WAVE - 1), b = l % 6;
   const unsigned gmb = min(gmb0 + (unsigned)(l / 6), nmbs - 1);  // tail lanes repeat the last MB
   const BlkPos pos = blk_pos_mb(gmb, b, w, h, kd);
@@ -863,7 +863,7 @@ __global__ __launch_bounds__(64 * MBG_WAVES) INTER_OCC void k_inter_mbg(p64gpu_e
   const bool rl = b == 0 && lane < 6 * MBS_PER_WAVE && gmb0 + (unsigned)(l / 6) < nmbs;
   const uint32_t mbw = (uint32_t)(mt & 0xff) | ((uint32_t)(cbp & 0xff) << 8) |
                        (mt_mf(mt) ? ((uint32_t)(mvx & 0xff) << 16) | ((uint32_t)(mvy & 0xff) << 24) : 0u);
-  mbg_store(a, lds, lane, nmbs, gmb0, nvalid, ro, pw, prow, rl, gmb, mbw,
+  mbg_store(a, kd, lds, lane, nmbs, gmb0, nvalid, ro, pw, prow, rl, gmb, mbw,
             mt_intra(mt) ? (uint8_t)0 : (uint8_t)(li + 1));
 }
 

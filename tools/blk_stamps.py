@@ -47,9 +47,9 @@ sub("""  if (gmb0 >= nmbs) return;  // whole wave
   PRIO_LOW();
   WAIT_ALL();
   STAMP(1);""")
-sub("""  mbg_store(a, lds, lane, nmbs, gmb0, nvalid, o.rec_off, o.pw, o.rec, rl, gmb, 0x3f00u, 0);
+sub("""  mbg_store(a, kd, lds, lane, nmbs, gmb0, nvalid, o.rec_off, o.pw, o.rec, rl, gmb, 0x3f00u, 0);
 }""", """  STAMP(2);
-  mbg_store(a, lds, lane, nmbs, gmb0, nvalid, o.rec_off, o.pw, o.rec, rl, gmb, 0x3f00u, 0);
+  mbg_store(a, kd, lds, lane, nmbs, gmb0, nvalid, o.rec_off, o.pw, o.rec, rl, gmb, 0x3f00u, 0);
   WAIT_ALL();
   STAMP(3);
 }""")
@@ -66,12 +66,10 @@ sub("""  const RecStageB S = rec_stage_b(B, w, h, stride, A);
   WAIT_ALL();
   STAMP(3);
 }""")
-sub("""  const int nmb = (w >> 4) * (h >> 4), nfr = (int)(nmbs / (unsigned)nmb);
-  RecBufs B;
-  B.ref = __builtin_amdgcn_make_buffer_rsrc((void *)refp""", """  STAMP(0);
-  const int nmb = (w >> 4) * (h >> 4), nfr = (int)(nmbs / (unsigned)nmb);
-  RecBufs B;
-  B.ref = __builtin_amdgcn_make_buffer_rsrc((void *)refp""")
+sub("""  const int nmb = (w >> 4) * (h >> 4), nfr = (int)mdiv(nmbs, kd.mn, kd.sn);
+  RecBufs B;""", """  STAMP(0);
+  const int nmb = (w >> 4) * (h >> 4), nfr = (int)mdiv(nmbs, kd.mn, kd.sn);
+  RecBufs B;""")
 # inter
 sub("""  const int64_t stride = a.frame_stride;
   RecBufs B;""", """  STAMP(0);
@@ -82,10 +80,10 @@ sub("""  const IntraFetch f = intra_fetch_at<QMB>(a, pos);  // current rows, q
   WAIT_ALL();
   STAMP(1);
 """)
-sub("""  mbg_store(a, lds, lane, nmbs, gmb0, nvalid, ro, pw, prow, rl, gmb, mbw,
+sub("""  mbg_store(a, kd, lds, lane, nmbs, gmb0, nvalid, ro, pw, prow, rl, gmb, mbw,
             mt_intra(mt) ? (uint8_t)0 : (uint8_t)(li + 1));
 }""", """  STAMP(2);
-  mbg_store(a, lds, lane, nmbs, gmb0, nvalid, ro, pw, prow, rl, gmb, mbw,
+  mbg_store(a, kd, lds, lane, nmbs, gmb0, nvalid, ro, pw, prow, rl, gmb, mbw,
             mt_intra(mt) ? (uint8_t)0 : (uint8_t)(li + 1));
   WAIT_ALL();
   STAMP(3);
