@@ -289,11 +289,6 @@ __device__ __forceinline__ void iq_idct_intra_rec(int v[64], int q, uint2 rec[8]
 // intra picture (p64.c:635, 770-771: every MB is MTYPE 0, CBP 0x3f), block
 // layout: load -> ChenDct -> BoundDct + CCITTFlatQuantize + FlatBound ->
 // zigzag store -> ICCITTFlatQuantize -> ChenIDct -> BoundIDct -> recon.
-// Persistent: a lane walks blocks t, t + stride, ... and issues the loads of
-// its next block before transforming the current one, so every wave keeps
-// HBM reads in flight under its own VALU work (without it the waves of a round
-// load, compute and store in lock step and the memory system idles while they
-// compute).
 // Levels leave through LDS: a lane's block is 128 bytes of levels, and 64
 // lanes storing their own 16-byte pieces touch 64 cache lines per store
 // instruction (measured: the level stores alone took 44 us of the 63 us a
