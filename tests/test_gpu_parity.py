@@ -148,6 +148,41 @@ def test_full_search_adversarial_vs_oracle(p64, oracle_mod, torch_dev, w, h):
             np.testing.assert_array_equal(got[i], exp, err_msg=f"sl {sl} picture {i}")
 
 
+def test_search_windows_at_picture_edges_vs_oracle(p64, oracle_mod, torch_dev):
+    """The search window is fetched without bounds tests (k_search.hip
+    fetch_luma): left/right of the picture it holds the neighbouring rows'
+    pixels, above/below zeros.  Edge MBs whose current block equals exactly
+    that wrapped or zero data (a perfect, but invalid, match at dx/dy beyond
+    the picture) must still get FastBME's answer over the valid candidates
+    (me.c:206-212), in every search mode."""
+    torch = torch_dev
+    w, h = 176, 144
+    rng = np.random.default_rng(99)
+    refs, curs = [], []
+    for k in range(3):
+        ref = rng.integers(0, 256, w * h, dtype=np.uint8)
+        cur = rng.integers(0, 256, (h, w), dtype=np.uint8)
+        for mby in range(h // 16):
+            y0 = 16 * mby
+            for x0, d in ((0, -(3 + 4 * k)), (w - 16, 5 + 3 * k)):  # left: previous rows' ends, right: next rows' starts
+                for r in range(16):
+                    s = (y0 + r) * w + x0 + d
+                    if 0 <= s and s + 16 <= w * h:
+                        cur[y0 + r, x0:x0 + 16] = ref[s:s + 16]
+        cur[0:16, 16:w - 16] = 0        # top row: a zero block matches the zeros above the picture
+        cur[h - 16:h, 16:w - 16] = 0    # bottom row: and below it
+        refs.append(ref)
+        curs.append(cur.reshape(-1))
+    cur_d = dev(torch, np.stack(curs))
+    ref_d = dev(torch, np.stack(refs))
+    for mode, sl in ((1, 31), (1, 15), (1, 7), (0, 31), (0, 15)):
+        got = host(p64.MotionEstimation(ref_d, cur_d, w, h, mode=mode, search_limit=sl, frame_stride=w * h))
+        for i in range(len(curs)):
+            exp = oracle_mod.motion_estimation(refs[i], curs[i], w, h, mode, sl)
+            exp = np.stack([exp[f] for f in exp.dtype.names], axis=1)
+            np.testing.assert_array_equal(got[i], exp, err_msg=f"mode {mode} sl {sl} picture {i}")
+
+
 # ---------------------------------------------------------------------------
 # whole-encoder fixtures, through the batched device API and the host context
 
