@@ -636,11 +636,11 @@ __device__ __forceinline__ void rec_block_pk(int w, int h, int64_t stride, __amd
 #endif
 // decoder reconstruction, MB-grouped block layout (blk_pos_mb), one block per
 // lane and no loop: 10 MBs per wave, each lane loads its MB's record, then its
-// levels and prediction, reconstructs and stores.  Without the persistent
-// kernel's in-flight registers it fits 3 waves per SIMD (139 VGPRs), and those
-// waves hide each other's two dependent load latencies (measured faster than
-// k_recon_blk, whose 237 VGPRs allow 2).  Lanes past the batch (and lanes
-// 60..63) get coded = 0: every load and store of theirs is out of range.
+// levels and prediction, reconstructs and stores.  93 VGPRs: 5 waves per
+// SIMD, which hide each other's two dependent load latencies (a persistent
+// variant with the next block's loads in flight needed 237 VGPRs, 2 waves,
+// and was slower).  Lanes past the batch (and lanes 60..63) get coded = 0:
+// every load and store of theirs is out of range.
 __global__ __launch_bounds__(64 * REC_WAVES) RECON_OCC void k_recon_mbg(int w, int h, int64_t stride, const uint8_t *refp,
                                                            uint8_t *recp, const int16_t *coef,
                                                            const p64_mb_rec *mbr, const uint8_t *quant_mb,
