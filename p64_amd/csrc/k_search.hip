@@ -160,11 +160,11 @@ static_assert(4 * MAP_PLANE_BYTES == 4 * LB_MAP_WORDS, "map size");
 
 // rows [R0, R1) of the current block against window rows [I0, I1) of the lane
 template <class G, int R0, int R1, int I0, int I1>
-__device__ __forceinline__ void full_rows(const uint32_t *wrow, int sh, const uint32_t *cs,
+__device__ __forceinline__ void full_rows(const lds_u32 *wrow, int sh, const uint32_t *cs,
                                           uint32_t *acc) {
 #pragma unroll
   for (int i = I0; i < I1; i++) {
-    const uint32_t *p = wrow + i * G::WS;
+    const lds_u32 *p = wrow + i * G::WS;
     const uint32_t a0 = p[0], a1 = p[1], a2 = p[2], a3 = p[3], a4 = p[4];
     const uint32_t r0 = align4(a1, a0, sh), r1 = align4(a2, a1, sh);
     const uint32_t r2 = align4(a3, a2, sh), r3 = align4(a4, a3, sh);
@@ -318,6 +318,15 @@ __device__ __forceinline__ bool window_constant(const Sx &S, int lane) {
   return !__any(diff);
 }
 
+// an LDS pointer whose whole address is one opaque register: constant row
+// offsets from it then fit the 8-bit dword offsets of ds_read2 (the compiler
+// otherwise keeps the struct offset as an immediate and adds per row pair)
+__device__ __forceinline__ const lds_u32 *lds_base(const uint32_t *p) {
+  uint32_t a = (uint32_t)(uintptr_t)as_lds(const_cast<uint32_t *>(p));
+  asm volatile("" : "+v"(a));
+  return (const lds_u32 *)(uintptr_t)a;
+}
+
 __device__ __forceinline__ void ord_pos(unsigned ord, int &cdx, int &cdy) {  // ord >= 1
   cdx = (int)((ord - 1) >> 5) - 15;
   cdy = (int)((ord - 1) & 31) - 15;
@@ -340,11 +349,11 @@ __device__ __forceinline__ unsigned finish_groups(const Sx &S, int n, int lane) 
     int cdx, cdy;
     ord_pos(ord, cdx, cdy);
     const int cb = WIN_OX + cdx, csh = cb & 3;
-    const uint32_t *p0 = S.win + (WIN_OY + cdy + rg) * G::WS + (cb >> 2) + d;
+    const lds_u32 *p0 = lds_base(S.win + (WIN_OY + cdy + rg) * G::WS + (cb >> 2) + d);
     uint32_t a = 0;
 #pragma unroll
     for (int t = 0; t < NR; t++) {
-      const uint32_t *p = p0 + RG * t * G::WS;
+      const lds_u32 *p = p0 + RG * t * G::WS;
       a = sad4(align4(p[1], p[0], csh), cw[t], a);
     }
     a += dpp<0xB1>(a);  // the group's lanes: quad, then 8, then 16
@@ -367,11 +376,11 @@ __device__ __forceinline__ unsigned finish_list(const Sx &S, int n, int lane) {
       int cdx, cdy;
       ord_pos(ord, cdx, cdy);
       const int cb = WIN_OX + cdx, csh = cb & 3;
-      const uint32_t *p0 = S.win + (WIN_OY + cdy) * G::WS + (cb >> 2);
+      const lds_u32 *p0 = lds_base(S.win + (WIN_OY + cdy) * G::WS + (cb >> 2));
       uint32_t a = 0;
 #pragma unroll
       for (int r = 0; r < 16; r++) {
-        const uint32_t *p = p0 + r * G::WS;
+        const lds_u32 *p = p0 + r * G::WS;
         const uint32_t a0 = p[0], a1 = p[1], a2 = p[2], a3 = p[3], a4 = p[4];
         // LDS broadcast, re-read per chunk (opaque index: not hoisted out of
         // the loop into live registers)
@@ -526,7 +535,7 @@ __device__ __forceinline__ void me_full(const Sx &S, const uint8_t *cur_blk, int
   } else if (range < 4 && uni(window_constant<G>(S, lane))) {
     bk = 0xFFFFFFFFu;  // constant window (checked for nearly flat blocks): (0,0), below
   } else {  // little pruned: every candidate densely, the current rows in SGPRs
-    const uint32_t *wrow = S.win + (15 * half) * G::WS + (colb >> 2);
+    const lds_u32 *wrow = lds_base(S.win + (15 * half) * G::WS + (colb >> 2));
     const int sh = colb & 3;
     uint32_t cs[64];
 #pragma unroll
