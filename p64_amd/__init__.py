@@ -221,8 +221,12 @@ def synth_frames_device(width: int, height: int, seed0: int, nseeds: int, frame0
     _dev_check(out, torch.uint8, "out")
     if out.numel() < nslots * nseeds * pic:
         raise P64GpuError("out too small")
-    _check(lib().p64gpu_synth_frames(width, height, seed0, nseeds, frame0, nslots, pic,
-                                     out.data_ptr(), _stream(torch)))
+    # one launch covers at most 65535 pictures (its grid's y extent): slot chunks
+    step = max(1, 65535 // nseeds)
+    for t0 in range(0, nslots, step):
+        n = min(step, nslots - t0)
+        _check(lib().p64gpu_synth_frames(width, height, seed0, nseeds, frame0 + t0, n, pic,
+                                         out.data_ptr() + t0 * nseeds * pic, _stream(torch)))
     return out
 
 def _torch():

@@ -639,6 +639,12 @@ def test_device_synth_matches_host(p64, torch_dev):
         for t in range(2):
             for s in range(3):
                 np.testing.assert_array_equal(d[t, s], p64.synth_frame(5 + s, 10 + t, w, h))
+    # more than 65535 pictures: the wrapper splits the slots over launches
+    w, h = 176, 144
+    big = p64.synth_frames_device(w, h, 3, 4096, 7, 17)
+    for t, s in ((0, 0), (15, 4095), (16, 0), (16, 4095)):
+        np.testing.assert_array_equal(host(big[t, s]), p64.synth_frame(3 + s, 7 + t, w, h))
+    del big
 
 
 # ---------------------------------------------------------------------------
