@@ -626,11 +626,14 @@ __device__ __forceinline__ void rec_block_pk(int w, int h, int64_t stride, __amd
 }
 // occupancy targets: 4 waves per SIMD (<= 128 VGPRs)
 #define INTER_OCC __attribute__((amdgpu_waves_per_eu(4)))
+// workgroup sizes: the decoder and the inter encoder run one-wave workgroups
+// (a wave's slot and its LDS free as soon as it ends; with the priority
+// raised first, that is -1.5 us for the decoder and -1 us for k_inter_mbg);
+// k_intra_mbg keeps four (one-wave groups cost it 3 us)
+#ifndef INTER_WAVES
+#define INTER_WAVES 1u
+#endif
 #define RECON_OCC __attribute__((amdgpu_waves_per_eu(4)))
-// the decoder's waves each form a workgroup of their own: a freed wave slot
-// takes the next wave at once instead of waiting for three others to free
-// theirs (-1.5 us on a launch of ~35; the encoders, whose waves finish more
-// evenly, keep 4-wave workgroups: 1-wave groups cost k_intra_mbg 2.5 us)
 #ifndef REC_WAVES
 #define REC_WAVES 1u
 #endif
@@ -726,12 +729,12 @@ __device__ __forceinline__ void pred_rows(const PredSrc &P, bool filter, uint2 p
   }
 }
 template <bool QMB>
-__global__ __launch_bounds__(64 * MBG_WAVES) INTER_OCC void k_inter_mbg(p64gpu_encode_args a, BlkDiv kd, unsigned nmbs,
+__global__ __launch_bounds__(64 * INTER_WAVES) INTER_OCC void k_inter_mbg(p64gpu_encode_args a, BlkDiv kd, unsigned nmbs,
                                                              const p64_me_rec *me) {
-  __shared__ __align__(16) uint8_t lvl[MBG_WAVES * LVL_WAVE];
+  __shared__ __align__(16) uint8_t lvl[INTER_WAVES * LVL_WAVE];
   const int lane = threadIdx.x & 63;
   uint8_t *lds = lvl + (threadIdx.x >> 6) * LVL_WAVE;
-  const unsigned gmb0 = (xcd_remap(blockIdx.x, gridDim.x) * MBG_WAVES + (threadIdx.x >> 6)) * MBS_PER_WAVE;
+  const unsigned gmb0 = (xcd_remap(blockIdx.x, gridDim.x) * INTER_WAVES + (threadIdx.x >> 6)) * MBS_PER_WAVE;
   if (gmb0 >= nmbs) return;  // whole wave
   PRIO_HIGH();  // first: a fresh wave's loads go out before the older waves' arithmetic
   const int w = a.width, h = a.height, nfr = (int)mdiv(nmbs, kd.mn, kd.sn);
@@ -885,10 +888,10 @@ hipError_t intra_mbg(const p64gpu_encode_args &a, hipStream_t st) {
 hipError_t inter_mbg(const p64gpu_encode_args &a, const p64_me_rec *me, hipStream_t st) {
   const unsigned nm = (unsigned)((int64_t)a.nframes * (a.width / 16) * (a.height / 16));
   if (a.quant_mb)
-    hipLaunchKernelGGL(k_inter_mbg<true>, dim3(mbg_workgroups(nm)), dim3(64 * MBG_WAVES), 0, st, a,
+    hipLaunchKernelGGL(k_inter_mbg<true>, dim3(mbg_workgroups(nm, INTER_WAVES)), dim3(64 * INTER_WAVES), 0, st, a,
                        blk_div(a.width, a.height), nm, me);
   else
-    hipLaunchKernelGGL(k_inter_mbg<false>, dim3(mbg_workgroups(nm)), dim3(64 * MBG_WAVES), 0, st, a,
+    hipLaunchKernelGGL(k_inter_mbg<false>, dim3(mbg_workgroups(nm, INTER_WAVES)), dim3(64 * INTER_WAVES), 0, st, a,
                        blk_div(a.width, a.height), nm, me);
   return hipGetLastError();
 }
