@@ -83,45 +83,53 @@ __device__ __forceinline__ int mad_c(int v, int acc) {  // C v + acc
   return r;
 }
 
-// forward butterfly on scaled sums s[k] and differences d[k] (chendct.c:135-159)
-template <bool N>
+// forward butterfly on scaled sums s[k] and differences d[k] (chendct.c:135-159).
+// S: the scale the caller left out of s and d (the column pass's <<2,
+// chendct.c:120-133): every s and the d[1], d[2] terms only meet constant
+// multiplies, so S folds into the constants (same bits mod 2^32); d[0] and
+// d[3] are added to products, so they take the shift themselves
+template <bool N, int S = 1>
 __device__ __forceinline__ void fwd8(const int s[4], const int d[4], int o[8]) {
+  static_assert(S == 1 || S == 4, "scale");
+  constexpr int L = S == 4 ? 2 : 0;
   const int e0 = s[0] + s[3], e1 = s[1] + s[2], e2 = s[1] - s[2], e3 = s[0] - s[3];
+  const int d0 = d[0] << L, d3 = d[3] << L;
   if (N) {  // operands proven < 2^23 (callers: pixels or residuals)
-    o[0] = ms9(mul_c<C1D4>(e0 + e1));
-    o[4] = ms9(mul_c<C1D4>(e0 - e1));
-    o[2] = ms9(mad_c<C3D8>(e2, mul_c<C1D8>(e3)));
-    o[6] = ms9(mad_c<C3D8>(e3, mul_c<-C1D8>(e2)));
-    const int r0 = ms9(mul_c<C1D4>(d[1] - d[2])), r1 = ms9(mul_c<C1D4>(d[1] + d[2]));
-    const int u0 = d[3] + r0, u1 = d[3] - r0, u2 = d[0] - r1, u3 = d[0] + r1;
+    o[0] = ms9(mul_c<S * C1D4>(e0 + e1));
+    o[4] = ms9(mul_c<S * C1D4>(e0 - e1));
+    o[2] = ms9(mad_c<S * C3D8>(e2, mul_c<S * C1D8>(e3)));
+    o[6] = ms9(mad_c<S * C3D8>(e3, mul_c<-S * C1D8>(e2)));
+    const int r0 = ms9(mul_c<S * C1D4>(d[1] - d[2])), r1 = ms9(mul_c<S * C1D4>(d[1] + d[2]));
+    const int u0 = d3 + r0, u1 = d3 - r0, u2 = d0 - r1, u3 = d0 + r1;
     o[1] = ms9(mad_c<C7D16>(u0, mul_c<C1D16>(u3)));
     o[3] = ms9(mad_c<C3D16>(u2, mul_c<-C5D16>(u1)));
     o[5] = ms9(mad_c<C3D16>(u1, mul_c<C5D16>(u2)));
     o[7] = ms9(mad_c<C7D16>(u3, mul_c<-C1D16>(u0)));
     return;
   }
-  o[0] = ms9(kmul<N>(C1D4, e0 + e1));
-  o[4] = ms9(kmul<N>(C1D4, e0 - e1));
-  o[2] = ms9(kmul<N>(C3D8, e2) + kmul<N>(C1D8, e3));
-  o[6] = ms9(kmul<N>(C3D8, e3) - kmul<N>(C1D8, e2));
-  const int r0 = ms9(kmul<N>(C1D4, d[1] - d[2])), r1 = ms9(kmul<N>(C1D4, d[1] + d[2]));
-  const int u0 = d[3] + r0, u1 = d[3] - r0, u2 = d[0] - r1, u3 = d[0] + r1;
+  o[0] = ms9(kmul<N>(S * C1D4, e0 + e1));
+  o[4] = ms9(kmul<N>(S * C1D4, e0 - e1));
+  o[2] = ms9(kmul<N>(S * C3D8, e2) + kmul<N>(S * C1D8, e3));
+  o[6] = ms9(kmul<N>(S * C3D8, e3) - kmul<N>(S * C1D8, e2));
+  const int r0 = ms9(kmul<N>(S * C1D4, d[1] - d[2])), r1 = ms9(kmul<N>(S * C1D4, d[1] + d[2]));
+  const int u0 = d3 + r0, u1 = d3 - r0, u2 = d0 - r1, u3 = d0 + r1;
   o[1] = ms9(kmul<N>(C7D16, u0) + kmul<N>(C1D16, u3));
   o[3] = ms9(kmul<N>(C3D16, u2) - kmul<N>(C5D16, u1));
   o[5] = ms9(kmul<N>(C3D16, u1) + kmul<N>(C5D16, u2));
   o[7] = ms9(kmul<N>(C7D16, u3) - kmul<N>(C1D16, u0));
 }
 
-// column pass: sums/differences scaled <<2 (chendct.c:120-133)
+// column pass: sums/differences scaled <<2 (chendct.c:120-133), the scale
+// folded into fwd8
 template <bool N>
 __device__ __forceinline__ void fwd_col(const int x[8], int o[8]) {
   int s[4], d[4];
 #pragma unroll
   for (int k = 0; k < 4; k++) {
-    s[k] = (x[k] + x[7 - k]) << 2;
-    d[k] = (x[k] - x[7 - k]) << 2;
+    s[k] = x[k] + x[7 - k];
+    d[k] = x[k] - x[7 - k];
   }
-  fwd8<N>(s, d, o);
+  fwd8<N, 4>(s, d, o);
 }
 // row pass: sums/differences >>1 (chendct.c:167-174)
 template <bool N>
