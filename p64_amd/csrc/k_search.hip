@@ -3,8 +3,8 @@
 //
 //   * the 16x16 current luma block and a 46x48-byte window of the previous
 //     reconstruction around it are staged in LDS with 16-byte loads;
-//   * FULL search (FastBME me.c:187): lane = (dx, dy-half), 15 candidates per
-//     lane; a lower bound on every candidate's SAD from 4x4 sub-block averages
+//   * FULL search (FastBME me.c:187): lane = (dx, dy group), 15 candidates per
+//     lane (4 for search limits up to 15); a lower bound on every candidate's SAD from 4x4 sub-block averages
 //     (v_lerp_u8 map, four v_sad_u8 per candidate) prunes all but a handful,
 //     which get full SADs; low-contrast blocks, where nothing prunes, take the
 //     dense exhaustive pass.  The argmin is one wave-wide min over packed
@@ -142,8 +142,9 @@ __device__ __forceinline__ int sad_zero(const Sx &S, int lane) {
 //     (0,0), which wins ties because FastBME evaluates it first (me.c:203, 220).
 // The result is identical to the exhaustive search for every input.
 //
-// Lane layout of the bound: lane = (dy half, dx index), 15 candidates
-// dy = -15 + 15*half + d, d = 0..14, of the column dx = dxi - 15.  Keys are
+// Lane layout (MeLayout below): lane = (dy group q, dx index), ND candidates
+// dy = D0 + ND*q + d, d = 0..ND-1, of the column dx = dxi + D0 (SL 31: two
+// groups of 15, dx from -15; SL <= 15: four groups of 4, dx from -7).  Keys are
 // SUM << 10 | ord, ord = 1 + (dx+15)*32 + (dy+15): FastBME's dx-major scan order
 // (ord 0 is reserved for the zero vector).
 constexpr int ME_LIST_MAX = 256;
@@ -158,8 +159,9 @@ constexpr unsigned KEY_ORD = (1u << KEY_SHIFT) - 1;
 constexpr int MAP_ROW_BYTES = Geo1::MAP_ROW, MAP_PLANE_BYTES = Geo1::MAP_PLANE;
 static_assert(4 * MAP_PLANE_BYTES == 4 * LB_MAP_WORDS, "map size");
 
-// rows [R0, R1) of the current block against window rows [I0, I1) of the lane
-template <class G, int R0, int R1, int I0, int I1>
+// rows [R0, R1) of the current block against window rows [I0, I1) of the
+// lane, candidate d = i - r of ND
+template <class G, int ND, int R0, int R1, int I0, int I1>
 __device__ __forceinline__ void full_rows(const lds_u32 *wrow, int sh, const uint32_t *cs,
                                           uint32_t *acc) {
 #pragma unroll
@@ -171,7 +173,7 @@ __device__ __forceinline__ void full_rows(const lds_u32 *wrow, int sh, const uin
 #pragma unroll
     for (int r = R0; r < R1; r++) {
       const int d = i - r;
-      if (d >= 0 && d < 15) {
+      if (d >= 0 && d < ND) {
         uint32_t a = acc[d];
         a = sad4(r0, cs[4 * r + 0], a);
         a = sad4(r1, cs[4 * r + 1], a);
@@ -397,39 +399,54 @@ __device__ __forceinline__ unsigned finish_list(const Sx &S, int n, int lane) {
 }
 
 
-template <class G>
+// Candidate layouts of the FULL search: lane = (dy group q, dx lane dxi),
+// ND vertically consecutive candidates per lane.  Search limits up to 15
+// (the reference's default, me.c:62) span dx, dy in [-7, 7): 14 dx lanes x
+// 4 groups x 4 dy; up to 31 span [-15, 15): 30 dx lanes x 2 groups x 15 dy.
+template <int DXL_, int NDX_, int ND_, int D0_>
+struct MeLayout {
+  static constexpr int DXL = DXL_, NDX = NDX_, ND = ND_, D0 = D0_;  // D0: dx of dxi 0, dy of (q 0, d 0)
+  static_assert(64 % DXL == 0 && NDX <= DXL && ND <= 15, "layout");
+};
+using MeLay31 = MeLayout<32, 30, 15, -15>;
+using MeLay15 = MeLayout<16, 14, 4, -7>;
+
+template <class G, class LY>
 __device__ __forceinline__ void me_full(const Sx &S, const uint8_t *cur_blk, int w, int h, int x0,
                                         int y0, int sl, int lane, int &sad0_out, int &mx, int &my,
                                         int &best) {
-  const int half = lane >> 5, dxi = lane & 31;
-  const bool lane_ok = dxi < 30;
-  const int colb = (lane_ok ? dxi : 29) + 1;  // window byte column of dx = dxi-15
+  constexpr int ND = LY::ND;
+  const int q = lane / LY::DXL, dxi = lane % LY::DXL;
+  const bool lane_ok = dxi < LY::NDX;
+  const int dx = (lane_ok ? dxi : LY::NDX - 1) + LY::D0;  // (idle lanes repeat the last column)
+  const int colb = dx + WIN_OX;                            // window byte column of dx
+  const int dy0 = LY::D0 + ND * q;                         // dy of the lane's d = 0
 
   // Validity (me.c:206-212: range and `< W-16`) is folded into the sums: an
   // invalid candidate starts at ME_INVALID, so it never survives and never wins.
   const int hl = sl >> 1;
-  const int dx = dxi - 15, px = x0 + dx;
+  const int px = x0 + dx;
   const bool col_ok = lane_ok && dx >= -hl && dx < hl && px >= 0 && px < w - 16;
-  // valid dy: [max(-hl, -y0), min(hl, h-16-y0)), i.e. d in [dlo, dhi) for this half
-  const int dlo = max(-hl, -y0) + 15 - 15 * half, dhi = min(hl, h - 16 - y0) + 15 - 15 * half;
-  const bool all_rows = dlo <= 0 && dhi >= 15;
+  // valid dy: [max(-hl, -y0), min(hl, h-16-y0)), i.e. d in [dlo, dhi) for this group
+  const int dlo = max(-hl, -y0) - dy0, dhi = min(hl, h - 16 - y0) - dy0;
+  const bool all_rows = dlo <= 0 && dhi >= ND;
   const bool interior = uni(__all(!lane_ok || (col_ok && all_rows)));
   // the sums start at 0; invalid candidates are marked afterwards (bit 19 of a
   // sum < 2^17): interior macroblocks only mask the two idle lanes, the others
   // OR in the lane's invalid rows, ~valid [dlo, dhi) (or every row)
   uint32_t inv = 0;
   if (!interior) {
-    const int lo = min(max(dlo, 0), 15), hi = min(max(dhi, 0), 15);
+    const int lo = min(max(dlo, 0), ND), hi = min(max(dhi, 0), ND);
     inv = ~((col_ok && hi > lo) ? (1u << hi) - (1u << lo) : 0u);
   }
   auto mark_invalid = [&](uint32_t *a) {
     if (!interior) {
 #pragma unroll
-      for (int d = 0; d < 15; d++) a[d] |= ((inv >> d) & 1u) << 19;
+      for (int d = 0; d < ND; d++) a[d] |= ((inv >> d) & 1u) << 19;
     }
   };
   static_assert(ME_INVALID == 1u << 19, "invalid mark");
-  const unsigned base = ((unsigned)dxi << 5) + (unsigned)(15 * half) + 1u;  // ord of d = 0
+  const unsigned base = ((unsigned)(dx + 15) << 5) + (unsigned)(dy0 + 15) + 1u;  // ord of d = 0
 
   SECTION("cur_map");
   uint32_t cm[4];
@@ -439,7 +456,7 @@ __device__ __forceinline__ void me_full(const Sx &S, const uint8_t *cur_blk, int
   sad0 = uni(sad0);
   sad0_out = sad0;
   unsigned bk = 0xFFFFFFFFu, ckey = 0xFFFFFFFFu, Ts = 0, pk = 0;
-  uint32_t acc[15];
+  uint32_t acc[ND];
   lds_u32 *list = as_lds(S.list);  // (one-MB image: aliases the map once the map is dead)
   int nsurv = 1000;
   // Low-contrast blocks (sub-block averages within a few levels) prune almost
@@ -459,19 +476,19 @@ __device__ __forceinline__ void me_full(const Sx &S, const uint8_t *cur_blk, int
     wsync();
     SECTION("lb_pass");
 #pragma unroll
-    for (int d = 0; d < 15; d++) acc[d] = 0;
+    for (int d = 0; d < ND; d++) acc[d] = 0;
     {
       const int xq = colb >> 2;
-      const uint32_t *mrow = S.map + ((colb & 3) * G::MAP_PLANE + 15 * half * G::MAP_ROW) / 4 + (xq >> 2);
+      const uint32_t *mrow = S.map + ((colb & 3) * G::MAP_PLANE + (dy0 + WIN_OY) * G::MAP_ROW) / 4 + (xq >> 2);
       const int msh = xq & 3;
 #pragma unroll
-      for (int i = 0; i < 27; i++) {
-        const uint32_t *q = mrow + i * (G::MAP_ROW / 4);
-        const uint32_t m4 = align4(q[1], q[0], msh);
+      for (int i = 0; i < ND + 12; i++) {
+        const uint32_t *mq = mrow + i * (G::MAP_ROW / 4);
+        const uint32_t m4 = align4(mq[1], mq[0], msh);
 #pragma unroll
         for (int j = 0; j < 4; j++) {
           const int d = i - 4 * j;
-          if (d >= 0 && d < 15) acc[d] = sad4(m4, cm[j], acc[d]);
+          if (d >= 0 && d < ND) acc[d] = sad4(m4, cm[j], acc[d]);
         }
       }
     }
@@ -482,7 +499,7 @@ __device__ __forceinline__ void me_full(const Sx &S, const uint8_t *cur_blk, int
     {  // least (S, d) of the lane as S << 4 | d, then its key S << 10 | ord
       unsigned m = 0xFFFFFFFFu;
 #pragma unroll
-      for (int d = 0; d < 15; d++) m = min(m, (acc[d] << 4) | (unsigned)d);
+      for (int d = 0; d < ND; d++) m = min(m, (acc[d] << 4) | (unsigned)d);
       if (!lane_ok) m = ME_INVALID << 4;
       pk = m == 0xFFFFFFFFu ? m : ((m >> 4) << KEY_SHIFT) + base + (m & 15u);
     }
@@ -502,9 +519,9 @@ __device__ __forceinline__ void me_full(const Sx &S, const uint8_t *cur_blk, int
     // 3. survivors: their ords compacted into L.list with ballot + mbcnt (the
     // first ME_LIST_MAX of them), counted on the way
     nsurv = 0;
-    if (lane_ok) {  // (the two idle lanes sit out: their sums are not masked)
+    if (lane_ok) {  // (the idle lanes sit out: their sums are not masked)
 #pragma unroll
-    for (int d = 0; d < 15; d++) {
+    for (int d = 0; d < ND; d++) {
       const bool sv = acc[d] <= Ts;
       const uint64_t bl = __ballot(sv);
       if (bl) {
@@ -535,20 +552,20 @@ __device__ __forceinline__ void me_full(const Sx &S, const uint8_t *cur_blk, int
   } else if (range < 4 && uni(window_constant<G>(S, lane))) {
     bk = 0xFFFFFFFFu;  // constant window (checked for nearly flat blocks): (0,0), below
   } else {  // little pruned: every candidate densely, the current rows in SGPRs
-    const lds_u32 *wrow = lds_base(S.win + (15 * half) * G::WS + (colb >> 2));
+    const lds_u32 *wrow = lds_base(S.win + (dy0 + WIN_OY) * G::WS + (colb >> 2));
     const int sh = colb & 3;
     uint32_t cs[64];
 #pragma unroll
-    for (int d = 0; d < 15; d++) acc[d] = 0;
+    for (int d = 0; d < ND; d++) acc[d] = 0;
     // (in two chunks of 8 rows: all 16 in SGPRs raise the kernel's SGPR
     // count past 80 and cost every macroblock a wave slot per SIMD)
     load_cur_rows8<0>(cur_blk, w, cs);
-    full_rows<G, 0, 8, 0, 22>(wrow, sh, cs, acc);
+    full_rows<G, ND, 0, 8, 0, ND + 7>(wrow, sh, cs, acc);
     load_cur_rows8<8>(cur_blk, w, cs);
-    full_rows<G, 8, 16, 8, 30>(wrow, sh, cs, acc);
+    full_rows<G, ND, 8, 16, 8, ND + 15>(wrow, sh, cs, acc);
     mark_invalid(acc);
 #pragma unroll
-    for (int d = 0; d < 15; d++) bk = min(bk, (acc[d] << KEY_SHIFT) + base + d);
+    for (int d = 0; d < ND; d++) bk = min(bk, (acc[d] << KEY_SHIFT) + base + d);
     if (!lane_ok) bk = 0xFFFFFFFFu;
     bk = wave_min(bk);
   }
@@ -641,7 +658,10 @@ __device__ __forceinline__ MeOut motion_estimate(const Sx &S, const uint8_t *cur
                                                  int x0, int y0, int sl, int lane) {
   MeOut o;
   if (MODE == 2) {
-    me_full<G>(S, cur_y + (size_t)y0 * w + x0, w, h, x0, y0, sl, lane, o.sad0, o.mx, o.my, o.sad);
+    if (sl <= 15)  // (uniform: one search limit per launch)
+      me_full<G, MeLay15>(S, cur_y + (size_t)y0 * w + x0, w, h, x0, y0, sl, lane, o.sad0, o.mx, o.my, o.sad);
+    else
+      me_full<G, MeLay31>(S, cur_y + (size_t)y0 * w + x0, w, h, x0, y0, sl, lane, o.sad0, o.mx, o.my, o.sad);
   } else {
     o.sad0 = uni(sad_zero<G>(S, lane));
     me_tss<G>(S, w, h, x0, y0, lane, o.sad0, o.mx, o.my, o.sad);

@@ -6,9 +6,9 @@ cd /tmp && export TMPDIR=/tmp
 for lib in "$@"; do
   tag=$(basename $lib .so)
   for c in ${CONTENTS:-synth pan15 noise flat}; do
-    OUT=$R/gpurun_out/meprof_${tag}_$c
+    OUT=$R/gpurun_out/meprof_${tag}_${c}_sl${SL:-31}
     rm -rf $OUT
-    P64GPU_LIB=$R/$lib timeout -k 10 120 rocprofv3 --kernel-trace --stats -d $OUT -o run --output-format csv -- python3 $R/tools/me_time.py --reps ${REPS:-20} --contents $c > $OUT.log 2>&1 || { echo "prof $tag $c failed"; tail -3 $OUT.log; exit 1; }
+    P64GPU_LIB=$R/$lib timeout -k 10 120 rocprofv3 --kernel-trace --stats -d $OUT -o run --output-format csv -- python3 $R/tools/me_time.py --reps ${REPS:-20} --contents $c --search-limit ${SL:-31} > $OUT.log 2>&1 || { echo "prof $tag $c failed"; tail -3 $OUT.log; exit 1; }
     find $OUT -name "*kernel_stats.csv" | xargs cat | python3 -c "
 import csv,sys
 for r in csv.DictReader(sys.stdin):

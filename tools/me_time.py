@@ -3,7 +3,7 @@ reference = the intra reconstruction of picture t-1, current = picture t, for
 the bench's contents (synth, pan15, noise, flat; bench.make_inputs).  Median
 of R launches by HIP events; also checks that the library's records equal
 those of P64GPU_REF_LIB (if given) -- timing probes that drop work differ.
-usage: [P64GPU_LIB=...] python tools/me_time.py [--reps R] [--streams S]
+usage: [P64GPU_LIB=...] python tools/me_time.py [--reps R] [--streams S] [--search-limit SL]
 """
 import argparse
 import os
@@ -23,6 +23,7 @@ def main():
     ap.add_argument("--reps", type=int, default=15)
     ap.add_argument("--streams", type=int, default=256)
     ap.add_argument("--contents", default="synth,pan15,noise,flat")
+    ap.add_argument("--search-limit", type=int, default=31)
     a = ap.parse_args()
     w, h, S = 352, 288, a.streams
     nmb, pic = (w // 16) * (h // 16), w * h * 3 // 2
@@ -37,7 +38,7 @@ def main():
         for _ in range(a.reps):
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
-            me = p64_amd.MotionEstimation(rec, cur, w, h, mode=p64_amd.ME_FULL, search_limit=31)
+            me = p64_amd.MotionEstimation(rec, cur, w, h, mode=p64_amd.ME_FULL, search_limit=a.search_limit)
             e1.record()
             torch.cuda.synchronize()
             ts.append(e0.elapsed_time(e1) * 1e3)
