@@ -234,19 +234,22 @@ __device__ __forceinline__ uint32_t from_next_lane_wave(uint32_t v) {
 // (chunk c of 9 map rows, natural dword n = x/4); vertical levels on the window
 // dwords, horizontal levels with the neighbour dword from lane + 1, the four
 // bytes of a natural dword scattered to the four phase planes.
+// RB, RPC: first map row and rows per chunk (5 chunks): rows RB .. RB+5*RPC-1
+// (the SL 31 layout reads rows 0..41, the SL <= 15 one rows 8..35)
+template <int RB = 0, int RPC = 9>
 __device__ __forceinline__ void build_lb_map(const Sx &S, int lane) {
   const int c = lane / 12, n = lane - 12 * c;
   const bool act = lane < 60;
-  const int y0 = 9 * min(c, 4);
-  uint32_t v1[11];
+  const int y0 = RB + RPC * min(c, 4);
+  uint32_t v1[RPC + 2];
 #pragma unroll
-  for (int t = 0; t < 11; t++) {
+  for (int t = 0; t < RPC + 2; t++) {
     const int ya = min(y0 + t, WIN_ROWS - 1), yb = min(y0 + t + 1, WIN_ROWS - 1);
     v1[t] = lerp4(S.win[ya * WIN_WORDS + n], S.win[yb * WIN_WORDS + n]);
   }
   uint8_t *mp = reinterpret_cast<uint8_t *>(S.map) + n;
 #pragma unroll
-  for (int t = 0; t < 9; t++) {
+  for (int t = 0; t < RPC; t++) {
     const uint32_t v = lerp4(v1[t], v1[t + 2]);  // rows y..y+3
     const uint32_t h1 = lerp4(v, align4(from_next_lane_wave(v), v, 1));
     const uint32_t h2 = lerp4(h1, align4(from_next_lane_wave(h1), h1, 2));
@@ -472,7 +475,10 @@ __device__ __forceinline__ void me_full(const Sx &S, const uint8_t *cur_blk, int
   if (lb_path) {
     // 1. lower bounds S
     SECTION("lb_map");
-    build_lb_map(S, lane);
+    if (ND < 15)
+      build_lb_map<8, 6>(S, lane);
+    else
+      build_lb_map(S, lane);
     wsync();
     SECTION("lb_pass");
 #pragma unroll
