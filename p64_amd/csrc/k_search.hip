@@ -89,29 +89,37 @@ struct LumaFetch {
   uint4 v[WIN_NIT];
   uint32_t c;
 };
+// window rows [R0, R0 + NR) (the SL <= 15 search reads rows 8..38 only)
+template <int R0 = 0, int NR = WIN_ROWS>
 __device__ __forceinline__ LumaFetch fetch_luma(const uint8_t *ref_y, const uint8_t *cur_y, int w,
                                                 int h, int x0, int y0, int lane) {
+  constexpr int SEGS = NR * 3, NIT = (SEGS + 63) / 64;
   const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc((void *)ref_y, (short)0, w * h, BUF_RSRC_W3);
-  const int base = (y0 - WIN_OY) * w + x0 - WIN_OX;  // (negative above the picture: out of range)
+  const int base = (y0 - WIN_OY + R0) * w + x0 - WIN_OX;  // (negative above the picture: out of range)
   LumaFetch f;
 #pragma unroll
-  for (int i = 0; i < WIN_NIT; i++) {
+  for (int i = 0; i < NIT; i++) {
     const int t = lane + 64 * i, row = t / 3, seg = t - row * 3;
-    const uint32_t off = (64 * i + 63 < WIN_SEGS || t < WIN_SEGS) ? (uint32_t)(base + mul24(row, w) + 16 * seg) : BUF_OOB;
+    const uint32_t off = (64 * i + 63 < SEGS || t < SEGS) ? (uint32_t)(base + mul24(row, w) + 16 * seg) : BUF_OOB;
     const auto v = __builtin_amdgcn_raw_buffer_load_b128(rr, off, 0, 0);
     f.v[i] = make_uint4(v[0], v[1], v[2], v[3]);
   }
   f.c = *reinterpret_cast<const uint32_t *>(cur_y + (uint32_t)(mul24(y0 + (lane >> 2), w) + x0 + 4 * (lane & 3)));
   return f;
 }
+template <int R0 = 0, int NR = WIN_ROWS>
 __device__ __forceinline__ void put_luma(MbLds &L, const LumaFetch &f, int lane) {
+  constexpr int SEGS = NR * 3, NIT = (SEGS + 63) / 64;
 #pragma unroll
-  for (int i = 0; i < WIN_NIT; i++) {
+  for (int i = 0; i < NIT; i++) {
     const int t = lane + 64 * i;
-    if (t < WIN_SEGS) reinterpret_cast<uint4 *>(L.win)[t] = f.v[i];
+    if (64 * i + 63 < SEGS || t < SEGS) reinterpret_cast<uint4 *>(L.win)[3 * R0 + t] = f.v[i];
   }
   L.cur[lane] = f.c;
 }
+// the rows the SL <= 15 search reads: its candidates' rows 8..36 (dy in
+// [-7, 7)), the dense pass's up to 38
+constexpr int WIN15_R0 = 8, WIN15_NR = 31;
 
 // SAD of the zero vector (OMV, me.c:203/271): one dword per lane
 template <class G>
@@ -311,14 +319,14 @@ __device__ __forceinline__ void sad_zero_hf(const Sx &S, int lane, int &sad0, in
 
 // every byte of the window equal: then every valid candidate block equals the
 // zero-vector block, all SADs equal SAD(0,0) and (0,0) wins (it wins ties)
-template <class G>
+template <class G, int R0 = 0, int NR = WIN_ROWS>  // window rows [R0, R0 + NR)
 __device__ __forceinline__ bool window_constant(const Sx &S, int lane) {
-  const uint32_t v = (S.win[0] & 255u) * 0x01010101u;
+  const uint32_t v = (S.win[R0 * G::WS] & 255u) * 0x01010101u;
   bool diff = false;
 #pragma unroll
-  for (int k = 0; k < (WIN_ROWS * WIN_WORDS + 63) / 64; k++) {
+  for (int k = 0; k < (NR * WIN_WORDS + 63) / 64; k++) {
     const int t = lane + 64 * k, row = t / WIN_WORDS;
-    if (t < WIN_ROWS * WIN_WORDS) diff |= S.win[row * G::WS + t - row * WIN_WORDS] != v;
+    if (t < NR * WIN_WORDS) diff |= S.win[(R0 + row) * G::WS + t - row * WIN_WORDS] != v;
   }
   return !__any(diff);
 }
@@ -555,7 +563,8 @@ __device__ __forceinline__ void me_full(const Sx &S, const uint8_t *cur_blk, int
       bk = finish_groups<G, 1>(S, nsurv, lane);
     else
       bk = finish_list<G>(S, nsurv, lane);
-  } else if (range < 4 && uni(window_constant<G>(S, lane))) {
+  } else if (range < 4 && uni(ND < 15 ? window_constant<G, WIN15_R0, WIN15_NR>(S, lane)
+                                       : window_constant<G>(S, lane))) {
     bk = 0xFFFFFFFFu;  // constant window (checked for nearly flat blocks): (0,0), below
   } else {  // little pruned: every candidate densely, the current rows in SGPRs
     const lds_u32 *wrow = lds_base(S.win + (dy0 + WIN_OY) * G::WS + (colb >> 2));
@@ -1034,8 +1043,12 @@ __global__ __launch_bounds__(64, 1) void k_motion(int w, int h, int64_t stride, 
   const unsigned gid = xcd_remap(blockIdx.x, gridDim.x);
   const MbPos ps = mb_pos(gid, nmb, mbw, kd);
   const int fi = ps.fi, x0 = 16 * ps.mbx, y0 = 16 * ps.mby;
-  put_luma(L, fetch_luma(ref_y + (size_t)fi * stride, cur_y + (size_t)fi * stride, w, h, x0, y0, lane),
-           lane);
+  if (MODE == 2 && sl <= 15)  // (the SL <= 15 layout reads window rows 8..38 only)
+    put_luma<WIN15_R0, WIN15_NR>(
+        L, fetch_luma<WIN15_R0, WIN15_NR>(ref_y + (size_t)fi * stride, cur_y + (size_t)fi * stride, w, h, x0, y0, lane),
+        lane);
+  else
+    put_luma(L, fetch_luma(ref_y + (size_t)fi * stride, cur_y + (size_t)fi * stride, w, h, x0, y0, lane), lane);
   __syncthreads();
   SECTION("m_fetched");
   const MeOut me = motion_estimate<Geo1, MODE>(sx_of(L), cur_y + (size_t)fi * stride, w, h, x0, y0, sl, lane);
