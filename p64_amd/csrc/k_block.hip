@@ -227,8 +227,7 @@ __device__ __forceinline__ uint32_t pk2(int lo, int hi) { return __builtin_amdgc
 // the intra DC (dequantised as dc8 = DC x 8)
 // ChenIDct column pass of column c from its dequantised natural pairs
 // (x_c, x_4c) (x_1c, x_7c) (x_5c, x_3c) (x_2c, x_6c) -- x_rc = row r
-__device__ __forceinline__ void idct_col_pairs(int c, uint32_t p04, uint32_t p17, uint32_t p53, uint32_t p26,
-                                               int v[64]) {
+__device__ __forceinline__ void idct_col8(uint32_t p04, uint32_t p17, uint32_t p53, uint32_t p26, int o[8]) {
   const s16x2 a04 = __builtin_bit_cast(s16x2, p04), a17 = __builtin_bit_cast(s16x2, p17);
   const s16x2 a53 = __builtin_bit_cast(s16x2, p53), a26 = __builtin_bit_cast(s16x2, p26);
   const int p0 = ms9(dot2(a17, 4 * C7D16, -4 * C1D16)), p3 = ms9(dot2(a17, 4 * C1D16, 4 * C7D16));
@@ -238,14 +237,21 @@ __device__ __forceinline__ void idct_col_pairs(int c, uint32_t p04, uint32_t p17
   const int e0 = q0 + q3, e1 = q1 + q2_, e2 = q1 - q2_, e3 = q0 - q3;
   const int f0 = p0 + p1, f1 = p0 - p1, f2 = p3 - p2, f3 = p3 + p2;
   const int g1 = ms9(kmul<true>(C1D4, f2 - f1)), g2 = ms9(kmul<true>(C1D4, f2 + f1));
-  v[c] = e0 + f3;
-  v[8 + c] = e1 + g2;
-  v[16 + c] = e2 + g1;
-  v[24 + c] = e3 + f0;
-  v[32 + c] = e3 - f0;
-  v[40 + c] = e2 - g1;
-  v[48 + c] = e1 - g2;
-  v[56 + c] = e0 - f3;
+  o[0] = e0 + f3;
+  o[1] = e1 + g2;
+  o[2] = e2 + g1;
+  o[3] = e3 + f0;
+  o[4] = e3 - f0;
+  o[5] = e2 - g1;
+  o[6] = e1 - g2;
+  o[7] = e0 - f3;
+}
+__device__ __forceinline__ void idct_col_pairs(int c, uint32_t p04, uint32_t p17, uint32_t p53, uint32_t p26,
+                                               int v[64]) {
+  int o[8];
+  idct_col8(p04, p17, p53, p26, o);
+#pragma unroll
+  for (int k = 0; k < 8; k++) v[8 * k + c] = o[k];
 }
 template <class PairFn>
 __device__ __forceinline__ void iq_idct_cols(PairFn pair, uint32_t q2, uint32_t qq, bool dcfix, int dc8,
@@ -373,11 +379,8 @@ __device__ __forceinline__ void intra_block(const p64gpu_encode_args &a, const I
 // (nvalid MBs x 768 bytes at coef + gmb0 x 768) from the LDS staging, the
 // lane's 8 reconstructed rows (rec_off, plane width pw), and from the record
 // lanes (rl) the MB record dword and the LastIntra byte of MB gmb
-__device__ __forceinline__ void mbg_store(const p64gpu_encode_args &a, const BlkDiv &kd, const uint8_t *lds, int lane,
-                                          unsigned nmbs, unsigned gmb0, uint32_t nvalid, uint32_t rec_off,
-                                          int pw, const uint2 rows[8], bool rl, unsigned gmb, uint32_t mbw,
-                                          uint8_t li) {
-  const int nfr = (int)mdiv(nmbs, kd.mn, kd.sn);
+__device__ __forceinline__ void mbg_store_levels(const p64gpu_encode_args &a, const uint8_t *lds, int lane,
+                                                 unsigned nmbs, unsigned gmb0, uint32_t nvalid) {
   const __amdgpu_buffer_rsrc_t coef =
       __builtin_amdgcn_make_buffer_rsrc((void *)a.coef, (short)0, (int)(nmbs * 768u), BUF_RSRC_W3);
   const uint32_t nbytes = nvalid * 768u;
@@ -395,8 +398,17 @@ __device__ __forceinline__ void mbg_store(const p64gpu_encode_args &a, const Blk
     __builtin_amdgcn_raw_buffer_store_b128(d, coef, ob < nbytes ? gmb0 * 768u + ob : BUF_OOB, 0, 0);
   }
   __builtin_amdgcn_wave_barrier();
-  const __amdgpu_buffer_rsrc_t rec =
-      __builtin_amdgcn_make_buffer_rsrc((void *)a.recon, (short)0, (int)(nfr * a.frame_stride), BUF_RSRC_W3);
+}
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t recon_rsrc(const p64gpu_encode_args &a, const BlkDiv &kd,
+                                                             unsigned nmbs) {
+  const int nfr = (int)mdiv(nmbs, kd.mn, kd.sn);
+  return __builtin_amdgcn_make_buffer_rsrc((void *)a.recon, (short)0, (int)(nfr * a.frame_stride), BUF_RSRC_W3);
+}
+// the rows (rec_off out of range: none) and the record of an MB-grouped wave
+__device__ __forceinline__ void mbg_store_rows(const p64gpu_encode_args &a, const BlkDiv &kd, unsigned nmbs,
+                                               uint32_t rec_off, int pw, const uint2 rows[8], bool rl,
+                                               unsigned gmb, uint32_t mbw, uint8_t li) {
+  const __amdgpu_buffer_rsrc_t rec = recon_rsrc(a, kd, nmbs);
 #pragma unroll
   for (int k = 0; k < 8; k++) {
     typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
@@ -411,6 +423,13 @@ __device__ __forceinline__ void mbg_store(const p64gpu_encode_args &a, const Blk
       __builtin_amdgcn_make_buffer_rsrc((void *)a.last_intra, (short)0, (int)nmbs, BUF_RSRC_W3);
   __builtin_amdgcn_raw_buffer_store_b32(mbw, mbr, rl ? 4u * gmb : BUF_OOB, 0, 0);
   __builtin_amdgcn_raw_buffer_store_b8(li, lir, rl ? gmb : BUF_OOB, 0, 0);
+}
+__device__ __forceinline__ void mbg_store(const p64gpu_encode_args &a, const BlkDiv &kd, const uint8_t *lds, int lane,
+                                          unsigned nmbs, unsigned gmb0, uint32_t nvalid, uint32_t rec_off,
+                                          int pw, const uint2 rows[8], bool rl, unsigned gmb, uint32_t mbw,
+                                          uint8_t li) {
+  mbg_store_levels(a, lds, lane, nmbs, gmb0, nvalid);
+  mbg_store_rows(a, kd, nmbs, rec_off, pw, rows, rl, gmb, mbw, li);
 }
 
 // intra picture, MB-grouped block layout (blk_pos_mb): one wave = 10 MBs, a
@@ -643,6 +662,120 @@ __device__ __forceinline__ void rec_block_pk(int w, int h, int64_t stride, __amd
     SCHED_FENCE();
   }
 }
+// IQ + ChenIDct + reconstruction over a wave's CODED blocks only (decoder
+// and k_inter_mbg).  A wave holds 60 blocks, typically a quarter of them with
+// levels (1.5 of 6 per MB on the bench stream), but a one-lane-per-block
+// transform costs the wave the same whatever that count.  Here the coded
+// blocks are ranked (ballot + mbcnt) and go through the transform eight at a
+// time with eight lanes per block: each pass, the coded lanes of rank
+// 8p..8p+7 put their raw natural level pairs (per column), prediction rows
+// and output offset into the wave's LDS slots; lane 8j+c dequantises and runs
+// the column pass of column c of slot j, lane 8j+r the row pass, the
+// reconstruction and the store of row r.  ceil(n/8) passes of one column and
+// one row per lane instead of eight of each per lane; the caller stores the
+// uncoded blocks (their prediction).  All exchanges stay inside one wave: a
+// wave's LDS operations complete in order, so no barrier; the wavefront-scope
+// fences only keep the compiler from moving LDS accesses across an exchange.
+//   ck       this lane's block carries levels
+//   np       its raw levels as natural column pairs: np[c] = (x0c,x4c) (x1c,x7c)
+//            (x5c,x3c) (x2c,x6c), x_rc = level of row r, column c
+//   q, intra UseQuant and the intra-DC rule (DC x 8, transform.c:371)
+//   prow     prediction rows (zeros for intra); ro, pw: output offset, plane width
+constexpr int RSLOT = 88;  // dwords per slot: 64 row-major values, 16 prediction, header
+                           // (88 = 24 mod 64: lane 8j+c's row-major writes hit 64 banks)
+constexpr int RSLOT_PRED = 64, RSLOT_HDR = 80;
+#define WAVE_FENCE() __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront")
+__device__ __forceinline__ void idct_coded_blocks(bool ck, const uint32_t np[8][4], int q, bool intra,
+                                                  const uint2 prow[8], uint32_t ro, int pw,
+                                                  __amdgpu_buffer_rsrc_t rec, uint32_t *slots, int lane) {
+  const uint64_t cm = __builtin_amdgcn_ballot_w64(ck);
+  const int n = __builtin_popcountll(cm);
+  const int rank = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(cm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)cm, 0u));
+  const int j = lane >> 3, c = lane & 7;  // this lane's slot and column (row)
+  uint32_t *const mine = slots + RSLOT * j;
+  for (int pass = 0; pass < n; pass += 8) {  // uniform
+    WAVE_FENCE();
+    if (ck && rank >= pass && rank < pass + 8) {
+      uint32_t *const s = slots + RSLOT * (rank - pass);
+#pragma unroll
+      for (int cc = 0; cc < 8; cc++) *(uint4 *)(s + 4 * cc) = make_uint4(np[cc][0], np[cc][1], np[cc][2], np[cc][3]);
+#pragma unroll
+      for (int k = 0; k < 8; k += 2)
+        *(uint4 *)(s + RSLOT_PRED + 2 * k) = make_uint4(prow[k].x, prow[k].y, prow[k + 1].x, prow[k + 1].y);
+      *(uint4 *)(s + RSLOT_HDR) = make_uint4((uint32_t)q | (intra ? 0x100u : 0u), ro, (uint32_t)pw, 0u);
+    }
+    WAVE_FENCE();
+    const uint4 hd = *(const uint4 *)(mine + RSLOT_HDR);
+    {  // column pass: column c of slot j, written back row-major in place
+      const uint4 lv = *(const uint4 *)(mine + 4 * c);
+      const int qj = (int)(hd.x & 0xff);
+      const uint32_t q2 = 0x20002u * (uint32_t)qj, qq = 0x10001u * (uint32_t)(qj - (int)!(qj & 1));
+      uint32_t p04 = dequantise_pk(lv.x, q2, qq);
+      if (c == 0 && (hd.x & 0x100u))  // intra DC: DC x 8
+        p04 = __builtin_amdgcn_perm(p04, (uint32_t)((int)(int16_t)(lv.x & 0xffff) * 8), 0x07060100u);
+      int o[8];
+      idct_col8(p04, dequantise_pk(lv.y, q2, qq), dequantise_pk(lv.z, q2, qq), dequantise_pk(lv.w, q2, qq), o);
+      WAVE_FENCE();
+#pragma unroll
+      for (int k = 0; k < 8; k++) mine[8 * k + c] = (uint32_t)o[k];
+    }
+    WAVE_FENCE();
+    {  // row pass of row c of slot j, + prediction, BoundIDctMatrix, store
+      const uint4 x0 = *(const uint4 *)(mine + 8 * c), x1 = *(const uint4 *)(mine + 8 * c + 4);
+      const uint2 pr = *(const uint2 *)(mine + RSLOT_PRED + 2 * c);
+      const int x[8] = {(int)x0.x, (int)x0.y, (int)x0.z, (int)x0.w, (int)x1.x, (int)x1.y, (int)x1.z, (int)x1.w};
+      int o[8];
+      inv8<true>(x, o);
+#pragma unroll
+      for (int k = 0; k < 8; k++) o[k] = idct_final(o[k]);
+      const uint2 r = recon_row(o, pr);
+      typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+      u32x2 d;
+      d[0] = r.x;
+      d[1] = r.y;
+      const uint32_t off = pass + j < n ? hd.y + (uint32_t)mul24(c, (int)hd.z) : BUF_OOB;
+      __builtin_amdgcn_raw_buffer_store_b64(d, rec, off, 0, 0);
+    }
+  }
+  WAVE_FENCE();
+}
+// the decoder's reconstruction through idct_coded_blocks
+__device__ __forceinline__ void rec_wave_compact(int w, int h, int64_t stride, __amdgpu_buffer_rsrc_t rec,
+                                                 const RecStageA &A, const RecStageB &S, uint32_t *slots,
+                                                 int lane) {
+  const BlkPos &p = A.p;
+  uint2 prow[8];
+  pred_rows<true>(S.pred, S.filter && S.inter, prow);  // zeros for intra (source not loaded)
+  const int pw = p.plane ? w >> 1 : w;
+  const uint32_t ro = (uint32_t)((int64_t)p.fi * stride) + (uint32_t)plane_offset(p.plane, w, h) +
+                      (uint32_t)(mul24(p.y, pw) + p.x);
+  {  // uncoded blocks of coded MBs: the prediction is the reconstruction
+    const uint32_t uo = (A.coded && !S.ck) ? ro : BUF_OOB;
+    typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      u32x2 d;
+      d[0] = prow[k].x;
+      d[1] = prow[k].y;
+      __builtin_amdgcn_raw_buffer_store_b64(d, rec, uo + (uint32_t)mul24(k, pw), 0, 0);
+    }
+  }
+  // natural column pairs straight from the packed zigzag words (one v_perm each)
+  auto pair = [&](int e, int f) {
+    const int s1 = k_zz.pos[e], s2 = k_zz.pos[f];
+    const uint32_t sel = ((s1 & 1) ? 0x0302u : 0x0100u) | (((s2 & 1) ? 0x0706u : 0x0504u) << 16);
+    return __builtin_amdgcn_perm(S.lq[s2 >> 3][(s2 >> 1) & 3], S.lq[s1 >> 3][(s1 >> 1) & 3], sel);
+  };
+  uint32_t np[8][4];
+#pragma unroll
+  for (int c = 0; c < 8; c++) {
+    np[c][0] = pair(c, 32 + c);
+    np[c][1] = pair(8 + c, 56 + c);
+    np[c][2] = pair(40 + c, 24 + c);
+    np[c][3] = pair(16 + c, 48 + c);
+  }
+  idct_coded_blocks(S.ck, np, A.q, !S.inter, prow, ro, pw, rec, slots, lane);
+}
 // occupancy targets: 4 waves per SIMD (<= 128 VGPRs)
 #define INTER_OCC __attribute__((amdgpu_waves_per_eu(4)))
 // workgroup sizes: the decoder and the inter encoder run one-wave workgroups
@@ -655,6 +788,9 @@ __device__ __forceinline__ void rec_block_pk(int w, int h, int64_t stride, __amd
 #define RECON_OCC __attribute__((amdgpu_waves_per_eu(4)))
 #ifndef REC_WAVES
 #define REC_WAVES 1u
+#endif
+#ifndef REC_COMPACT
+#define REC_COMPACT 1
 #endif
 // decoder reconstruction, MB-grouped block layout (blk_pos_mb), one block per
 // lane and no loop: 10 MBs per wave, each lane loads its MB's record, then its
@@ -691,7 +827,12 @@ __global__ __launch_bounds__(64 * REC_WAVES) RECON_OCC void k_recon_mbg(int w, i
   A.coded = __builtin_amdgcn_raw_buffer_load_b8(B.mask, valid ? gmb : BUF_OOB, 0, 0);
   const RecStageB S = rec_stage_b(B, w, h, stride, A);
   PRIO_LOW();
+#if REC_COMPACT
+  __shared__ uint32_t slots[REC_WAVES][8 * RSLOT];
+  rec_wave_compact(w, h, stride, rec, A, S, slots[threadIdx.x >> 6], lane);
+#else
   rec_block_pk(w, h, stride, rec, A, S);
+#endif
 }
 
 // ---------------------------------------------------------------------------
@@ -808,7 +949,6 @@ __global__ __launch_bounds__(64 * INTER_WAVES) INTER_OCC void k_inter_mbg(p64gpu
 
   const bool intra = mt_intra(mt), tc = mt_tcoeff(mt);
   const int q = f.q;
-  const int qe = (int)!(q & 1);
   const p64_qint qt = c_qint.ac[q], qd = c_qint.dc[q];
   // levels & tcm: 0 when the MB type carries no coefficients (through an
   // opaque mask: as a select hipcc branches around every quantisation)
@@ -859,31 +999,32 @@ __global__ __launch_bounds__(64 * INTER_WAVES) INTER_OCC void k_inter_mbg(p64gpu
     }
   }
   const bool ck = mt_tcoeff(mt) && ((cbp >> (5 - b)) & 1);
-  const uint32_t q2 = ck ? 0x20002u * (uint32_t)q : 0u, qq = ck ? 0x10001u * (uint32_t)(q - qe) : 0u;
-  // IQ in level pairs + ChenIDct (all-zero levels / q2 = qq = 0 give zero)
-  iq_idct_cols([&](int e, int f) { return pk2(v[e], v[f]); }, q2, qq, intra, v[0] * 8, v);
+  // the levels as natural column pairs (the 64 level registers die here)
+  uint32_t np[8][4];
 #pragma unroll
-  for (int k = 0; k < 8; k++) {  // row pass + prediction: now the reconstructed rows
-    int o[8];
-    inv8<true>(v + 8 * k, o);
-#pragma unroll
-    for (int j = 0; j < 8; j++) o[j] = idct_final(o[j]);
-    prow[k] = recon_row(o, prow[k]);
-    SCHED_FENCE();
+  for (int c = 0; c < 8; c++) {
+    np[c][0] = pk2(v[c], v[32 + c]);
+    np[c][1] = pk2(v[8 + c], v[56 + c]);
+    np[c][2] = pk2(v[40 + c], v[24 + c]);
+    np[c][3] = pk2(v[16 + c], v[48 + c]);
   }
-  // no levels at all in the MB: the reconstruction is the new prediction
-  // (late, so its registers do not overlap the block's)
-  if (repred) inter_pred(B, w, h, stride, pos, mt, mvx, mvy, prow);
+  // the levels leave first: the staging then holds idct_coded_blocks' slots
   const uint32_t nvalid = min((unsigned)MBS_PER_WAVE, nmbs - gmb0);
+  mbg_store_levels(a, lds, lane, nmbs, gmb0, nvalid);
   const int pw = pos.plane ? w >> 1 : w;
   const uint32_t ro = (uint32_t)((int64_t)pos.fi * stride) + (uint32_t)plane_offset(pos.plane, w, h) +
                       (uint32_t)mul24(pos.y, pw) + (uint32_t)pos.x;
+  // IQ + ChenIDct + reconstruction of the coded blocks, stored there
+  idct_coded_blocks(ck, np, q, intra, prow, ro, pw, recon_rsrc(a, kd, nmbs), (uint32_t *)lds, lane);
+  // no levels at all in the MB: the reconstruction is the new prediction
+  if (repred) inter_pred(B, w, h, stride, pos, mt, mvx, mvy, prow);
   // p64.c:909-910: the record (transmitted vector only for MC types) and LastIntra
   const bool rl = b == 0 && lane < 6 * MBS_PER_WAVE && gmb0 + (unsigned)(l / 6) < nmbs;
   const uint32_t mbw = (uint32_t)(mt & 0xff) | ((uint32_t)(cbp & 0xff) << 8) |
                        (mt_mf(mt) ? ((uint32_t)(mvx & 0xff) << 16) | ((uint32_t)(mvy & 0xff) << 24) : 0u);
-  mbg_store(a, kd, lds, lane, nmbs, gmb0, nvalid, ro, pw, prow, rl, gmb, mbw,
-            mt_intra(mt) ? (uint8_t)0 : (uint8_t)(li + 1));
+  // uncoded blocks: the prediction is the reconstruction
+  mbg_store_rows(a, kd, nmbs, ck ? BUF_OOB : ro, pw, prow, rl, gmb, mbw,
+                 mt_intra(mt) ? (uint8_t)0 : (uint8_t)(li + 1));
 }
 
 }  // namespace
