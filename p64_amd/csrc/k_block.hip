@@ -469,6 +469,49 @@ __device__ __forceinline__ void pred_row(const PredSrc &p, int r, int s[8]) {
 // source row with the taps as byte weights, no unpacking (decoder: -0.5 us);
 // otherwise unpacked adds (the inter encoder measured 2.7 us slower with the
 // dot products, although it issues ~90 fewer VALU per wave)
+// the horizontal taps of a row as four packed 16-bit pairs (hz_2i, hz_2i+1):
+// every tap sum is at most 4 x 255 = 1,020
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void hz_row_pk(const PredSrc &p, int r, u16x2 hz[4]) {
+  const uint32_t lo = align4(p.d[r][1], p.d[r][0], p.sh), hi = align4(p.d[r][2], p.d[r][1], p.sh);
+  const uint32_t mid = align4(hi, lo, 2);  // pixels 2..5
+  const uint32_t w[8] = {__builtin_amdgcn_udot4(lo, 0x00000004u, 0u, false),
+                         __builtin_amdgcn_udot4(lo, 0x00010201u, 0u, false),
+                         __builtin_amdgcn_udot4(lo, 0x01020100u, 0u, false),
+                         __builtin_amdgcn_udot4(mid, 0x00010201u, 0u, false),
+                         __builtin_amdgcn_udot4(mid, 0x01020100u, 0u, false),
+                         __builtin_amdgcn_udot4(hi, 0x00010201u, 0u, false),
+                         __builtin_amdgcn_udot4(hi, 0x01020100u, 0u, false),
+                         __builtin_amdgcn_udot4(hi, 0x04000000u, 0u, false)};
+#pragma unroll
+  for (int i = 0; i < 4; i++) hz[i] = __builtin_bit_cast(u16x2, (w[2 * i + 1] << 16) | w[2 * i]);
+}
+// pred_rows' loop filter in packed 16-bit arithmetic (decoder): the vertical
+// [1 2 1] + 8 >> 4 of the tap pairs (at most 4 x 1,020 + 8 = 4,088) as
+// v_pk_ operations, half the registers of the unpacked rows
+__device__ __forceinline__ void pred_rows_filter_pk(const PredSrc &P, uint2 prow[8]) {
+  u16x2 hp[4], hc[4], hn[4];
+  hz_row_pk(P, 0, hc);
+  hz_row_pk(P, 1, hn);
+  const u16x2 c8 = {8, 8};
+#pragma unroll
+  for (int r = 0; r < 8; r++) {
+    uint32_t t[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      const u16x2 v = (r == 0 || r == 7) ? (u16x2)((hc[i] << (u16x2){2, 2}) + c8) >> (u16x2){4, 4}
+                                         : (u16x2)(hp[i] + (hc[i] << (u16x2){1, 1}) + hn[i] + c8) >> (u16x2){4, 4};
+      t[i] = __builtin_bit_cast(uint32_t, v);
+    }
+    prow[r] = make_uint2(__builtin_amdgcn_perm(t[1], t[0], 0x06040200u), __builtin_amdgcn_perm(t[3], t[2], 0x06040200u));
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      hp[i] = hc[i];
+      hc[i] = hn[i];
+    }
+    if (r + 2 < 8) hz_row_pk(P, r + 2, hn);
+  }
+}
 template <bool DOT>
 __device__ __forceinline__ void hz_row(const PredSrc &p, int r, int hz[8]) {
   if (DOT) {
@@ -681,22 +724,36 @@ __device__ __forceinline__ void rec_block_pk(int w, int h, int64_t stride, __amd
 //            (x5c,x3c) (x2c,x6c), x_rc = level of row r, column c
 //   q, intra UseQuant and the intra-DC rule (DC x 8, transform.c:371)
 //   prow     prediction rows (zeros for intra); ro, pw: output offset, plane width
-constexpr int RSLOT = 88;  // dwords per slot: 64 row-major values, 16 prediction, header
-                           // (88 = 24 mod 64: lane 8j+c's row-major writes hit 64 banks)
+// LPB lanes per block (8 or 4): a pass takes 64/LPB blocks, lane LPB*j+g
+// columns (rows) g, g+LPB, ... of slot j.  Slot: 64 row-major values, 16
+// prediction dwords, header; its stride keeps the row-major writes of the
+// column pass free of bank conflicts (88 = 24 mod 64 for eight lanes per block,
+// 84 = 20 mod 64 for four)
+#ifndef REC_LPB
+#define REC_LPB 4
+#endif
 constexpr int RSLOT_PRED = 64, RSLOT_HDR = 80;
+constexpr int rslot(int lpb) { return lpb == 8 ? 88 : 84; }
+#ifndef DEC_LPB
+#define DEC_LPB REC_LPB
+#endif
+constexpr int RSLOTS_BYTES = 4 * rslot(REC_LPB) * (64 / REC_LPB);
+static_assert(RSLOTS_BYTES <= LVL_WAVE, "k_inter_mbg's slots live in its level staging");
 #define WAVE_FENCE() __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront")
+template <int LPB = REC_LPB>
 __device__ __forceinline__ void idct_coded_blocks(bool ck, const uint32_t np[8][4], int q, bool intra,
                                                   const uint2 prow[8], uint32_t ro, int pw,
                                                   __amdgpu_buffer_rsrc_t rec, uint32_t *slots, int lane) {
+  constexpr int NS = 64 / LPB, CPL = 8 / LPB, RS = rslot(LPB);
   const uint64_t cm = __builtin_amdgcn_ballot_w64(ck);
   const int n = __builtin_popcountll(cm);
   const int rank = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(cm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)cm, 0u));
-  const int j = lane >> 3, c = lane & 7;  // this lane's slot and column (row)
-  uint32_t *const mine = slots + RSLOT * j;
-  for (int pass = 0; pass < n; pass += 8) {  // uniform
+  const int j = lane / LPB, g = lane % LPB;  // this lane's slot, first column (row)
+  uint32_t *const mine = slots + RS * j;
+  for (int pass = 0; pass < n; pass += NS) {  // uniform
     WAVE_FENCE();
-    if (ck && rank >= pass && rank < pass + 8) {
-      uint32_t *const s = slots + RSLOT * (rank - pass);
+    if (ck && rank >= pass && rank < pass + NS) {
+      uint32_t *const s = slots + RS * (rank - pass);
 #pragma unroll
       for (int cc = 0; cc < 8; cc++) *(uint4 *)(s + 4 * cc) = make_uint4(np[cc][0], np[cc][1], np[cc][2], np[cc][3]);
 #pragma unroll
@@ -705,36 +762,47 @@ __device__ __forceinline__ void idct_coded_blocks(bool ck, const uint32_t np[8][
       *(uint4 *)(s + RSLOT_HDR) = make_uint4((uint32_t)q | (intra ? 0x100u : 0u), ro, (uint32_t)pw, 0u);
     }
     WAVE_FENCE();
-    const uint4 hd = *(const uint4 *)(mine + RSLOT_HDR);
-    {  // column pass: column c of slot j, written back row-major in place
-      const uint4 lv = *(const uint4 *)(mine + 4 * c);
-      const int qj = (int)(hd.x & 0xff);
-      const uint32_t q2 = 0x20002u * (uint32_t)qj, qq = 0x10001u * (uint32_t)(qj - (int)!(qj & 1));
-      uint32_t p04 = dequantise_pk(lv.x, q2, qq);
-      if (c == 0 && (hd.x & 0x100u))  // intra DC: DC x 8
-        p04 = __builtin_amdgcn_perm(p04, (uint32_t)((int)(int16_t)(lv.x & 0xffff) * 8), 0x07060100u);
-      int o[8];
-      idct_col8(p04, dequantise_pk(lv.y, q2, qq), dequantise_pk(lv.z, q2, qq), dequantise_pk(lv.w, q2, qq), o);
-      WAVE_FENCE();
+    {  // column pass: columns g + LPB i of slot j, written back row-major in place
+      uint4 lv[CPL];
 #pragma unroll
-      for (int k = 0; k < 8; k++) mine[8 * k + c] = (uint32_t)o[k];
+      for (int i = 0; i < CPL; i++) lv[i] = *(const uint4 *)(mine + 4 * (g + LPB * i));
+      const uint32_t hx = mine[RSLOT_HDR];  // q | intra << 8
+      const int qj = (int)(hx & 0xff);
+      const uint32_t q2 = 0x20002u * (uint32_t)qj, qq = 0x10001u * (uint32_t)(qj - (int)!(qj & 1));
+      WAVE_FENCE();  // every column read before the first write
+#pragma unroll
+      for (int i = 0; i < CPL; i++) {
+        uint32_t p04 = dequantise_pk(lv[i].x, q2, qq);
+        if (i == 0 && g == 0 && (hx & 0x100u))  // intra DC: DC x 8
+          p04 = __builtin_amdgcn_perm(p04, (uint32_t)((int)(int16_t)(lv[i].x & 0xffff) * 8), 0x07060100u);
+        int o[8];
+        idct_col8(p04, dequantise_pk(lv[i].y, q2, qq), dequantise_pk(lv[i].z, q2, qq),
+                  dequantise_pk(lv[i].w, q2, qq), o);
+#pragma unroll
+        for (int k = 0; k < 8; k++) mine[8 * k + g + LPB * i] = (uint32_t)o[k];
+        SCHED_FENCE();
+      }
     }
     WAVE_FENCE();
-    {  // row pass of row c of slot j, + prediction, BoundIDctMatrix, store
-      const uint4 x0 = *(const uint4 *)(mine + 8 * c), x1 = *(const uint4 *)(mine + 8 * c + 4);
-      const uint2 pr = *(const uint2 *)(mine + RSLOT_PRED + 2 * c);
+#pragma unroll
+    for (int i = 0; i < CPL; i++) {  // row pass of row g + LPB i of slot j, + prediction, BoundIDctMatrix, store
+      const int r = g + LPB * i;
+      const uint4 x0 = *(const uint4 *)(mine + 8 * r), x1 = *(const uint4 *)(mine + 8 * r + 4);
+      const uint2 pr = *(const uint2 *)(mine + RSLOT_PRED + 2 * r);
+      const uint2 hd = *(const uint2 *)(mine + RSLOT_HDR + 1);  // ro, pw
       const int x[8] = {(int)x0.x, (int)x0.y, (int)x0.z, (int)x0.w, (int)x1.x, (int)x1.y, (int)x1.z, (int)x1.w};
       int o[8];
       inv8<true>(x, o);
 #pragma unroll
       for (int k = 0; k < 8; k++) o[k] = idct_final(o[k]);
-      const uint2 r = recon_row(o, pr);
+      const uint2 rr = recon_row(o, pr);
       typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
       u32x2 d;
-      d[0] = r.x;
-      d[1] = r.y;
-      const uint32_t off = pass + j < n ? hd.y + (uint32_t)mul24(c, (int)hd.z) : BUF_OOB;
+      d[0] = rr.x;
+      d[1] = rr.y;
+      const uint32_t off = pass + j < n ? hd.x + (uint32_t)mul24(r, (int)hd.y) : BUF_OOB;
       __builtin_amdgcn_raw_buffer_store_b64(d, rec, off, 0, 0);
+      SCHED_FENCE();
     }
   }
   WAVE_FENCE();
@@ -774,7 +842,7 @@ __device__ __forceinline__ void rec_wave_compact(int w, int h, int64_t stride, _
     np[c][2] = pair(40 + c, 24 + c);
     np[c][3] = pair(16 + c, 48 + c);
   }
-  idct_coded_blocks(S.ck, np, A.q, !S.inter, prow, ro, pw, rec, slots, lane);
+  idct_coded_blocks<DEC_LPB>(S.ck, np, A.q, !S.inter, prow, ro, pw, rec, slots, lane);
 }
 // occupancy targets: 4 waves per SIMD (<= 128 VGPRs)
 #define INTER_OCC __attribute__((amdgpu_waves_per_eu(4)))
@@ -785,7 +853,10 @@ __device__ __forceinline__ void rec_wave_compact(int w, int h, int64_t stride, _
 #ifndef INTER_WAVES
 #define INTER_WAVES 1u
 #endif
-#define RECON_OCC __attribute__((amdgpu_waves_per_eu(4)))
+#ifndef RECON_WPE
+#define RECON_WPE 4
+#endif
+#define RECON_OCC __attribute__((amdgpu_waves_per_eu(RECON_WPE)))
 #ifndef REC_WAVES
 #define REC_WAVES 1u
 #endif
@@ -828,7 +899,7 @@ __global__ __launch_bounds__(64 * REC_WAVES) RECON_OCC void k_recon_mbg(int w, i
   const RecStageB S = rec_stage_b(B, w, h, stride, A);
   PRIO_LOW();
 #if REC_COMPACT
-  __shared__ uint32_t slots[REC_WAVES][8 * RSLOT];
+  __shared__ uint32_t slots[REC_WAVES][rslot(DEC_LPB) * (64 / DEC_LPB)];
   rec_wave_compact(w, h, stride, rec, A, S, slots[threadIdx.x >> 6], lane);
 #else
   rec_block_pk(w, h, stride, rec, A, S);
@@ -866,7 +937,9 @@ __device__ __forceinline__ void inter_pred(const RecBufs &B, int w, int h, int64
 // the prediction as packed rows (all zero when the source was not loaded)
 template <bool DOT>
 __device__ __forceinline__ void pred_rows(const PredSrc &P, bool filter, uint2 prow[8]) {
-  if (filter) {  // add_pred's loop filter, one packed row at a time
+  if (DOT && filter) {
+    pred_rows_filter_pk(P, prow);
+  } else if (filter) {  // add_pred's loop filter, one packed row at a time
     int hp[8], hc[8], hn[8];
     hz_row<DOT>(P, 0, hc);
     hz_row<DOT>(P, 1, hn);
