@@ -191,28 +191,6 @@ __device__ __forceinline__ uint2 final_clamp_pack8(const int o[8]) {
   for (int k = 0; k < 8; k++) x[k] = (o[k] + 8) >> 4;
   return make_uint2(sat4(x), sat4(x + 4));
 }
-// ChenIDct (chendct.c:217-375) on a register block: column pass (inputs <<2,
-// folded into the constants), row pass, final rounding
-__device__ __forceinline__ void idct_block(int v[64]) {
-#pragma unroll
-  for (int c = 0; c < 8; c++) {
-    int x[8], o[8];
-#pragma unroll
-    for (int k = 0; k < 8; k++) x[k] = v[8 * k + c];
-    inv8<true, 4>(x, o);
-#pragma unroll
-    for (int k = 0; k < 8; k++) v[8 * k + c] = o[k];
-    SCHED_FENCE();
-  }
-#pragma unroll
-  for (int r = 0; r < 8; r++) {
-    int o[8];
-    inv8<true>(v + 8 * r, o);
-#pragma unroll
-    for (int k = 0; k < 8; k++) v[8 * r + k] = idct_final(o[k]);
-    SCHED_FENCE();
-  }
-}
 // ICCITTFlatQuantize + ChenIDct + BoundIDctMatrix of an intra block from its
 // levels (natural order in v; the DC dequantised as DC x 8): the dequantiser
 // runs on natural level pairs (x_k, x_k') of a column in packed 16-bit
@@ -535,10 +513,10 @@ __device__ __forceinline__ void hz_row(const PredSrc &p, int r, int hz[8]) {
   hz[7] = s[7] << 2;
 }
 // decoder reconstruction (DecompressMDU p64.c:1179-1237 + DecodeSaveMDU
-// p64.c:971-1013), block layout, persistent, as a two-stage load pipeline:
-// while block i is transformed, the levels and prediction source of block
-// i+1 (whose record arrived during block i-1) and the record of block i+2 are
-// in flight.  Every load is a buffer load: where a block needs no levels
+// p64.c:971-1013), block layout: a lane loads its MB's record, then its
+// block's levels and prediction source (rec_stage_b), forms the prediction,
+// and the wave's coded blocks go through idct_coded_blocks (below).  Every
+// load is a buffer load: where a block needs no levels
 // (uncoded) or no prediction (intra MB) its offset is out of range, which
 // reads zeros without touching memory -- no branch around any load, so the
 // wait counts stay exact and only the algorithmic bytes move.
@@ -625,11 +603,6 @@ __device__ __forceinline__ RecStageB rec_stage_b(const RecBufs &B, int w, int h,
   }
   return S;
 }
-// pred_rows (below) + dequantise + ChenIDct + reconstruction for the
-// non-persistent decoder: the prediction is formed first and kept as 8 packed
-// rows (16 registers instead of the 24-dword source), the dequantisation and
-// IDCT run unconditionally (an uncoded block's levels were read as zeros and
-// give a zero residual), so the register peak is the IDCT's
 // one reconstructed row: residual v[0..7] (after idct_final) + prediction
 // row pr (packed bytes), clamped to 0..255 (BoundIDctMatrix), packed -- in
 // 16-bit pairs: v_cvt_pk_i16_i32 (saturating), the prediction bytes widened by
@@ -651,60 +624,6 @@ __device__ __forceinline__ uint2 recon_row(const int v[8], uint2 pr) {
 }
 template <bool DOT>
 __device__ __forceinline__ void pred_rows(const PredSrc &P, bool filter, uint2 prow[8]);
-__device__ __forceinline__ void rec_block_pk(int w, int h, int64_t stride, __amdgpu_buffer_rsrc_t rec,
-                                             const RecStageA &A, const RecStageB &S) {
-  const BlkPos &p = A.p;
-  uint2 prow[8];
-  pred_rows<true>(S.pred, S.filter && S.inter, prow);  // zeros for intra (source not loaded)
-  int v[64];
-  const int q = A.q;
-  const uint32_t q2 = 0x20002u * (uint32_t)q, qq = 0x10001u * (uint32_t)(q - (int)!(q & 1));
-  // natural level pairs straight from the packed zigzag words (one v_perm each)
-  auto pair = [&](int e, int f) {
-    const int s1 = k_zz.pos[e], s2 = k_zz.pos[f];
-    const uint32_t sel = ((s1 & 1) ? 0x0302u : 0x0100u) | (((s2 & 1) ? 0x0706u : 0x0504u) << 16);
-    return __builtin_amdgcn_perm(S.lq[s2 >> 3][(s2 >> 1) & 3], S.lq[s1 >> 3][(s1 >> 1) & 3], sel);
-  };
-  // every column's dequantised natural pairs first: the zigzag words die
-  // here, so the IDCT's 64 values never share the registers with them
-  // (peak 84 instead of 112 live values: 4 waves per SIMD instead of 3)
-  uint32_t np[8][4];
-#pragma unroll
-  for (int c = 0; c < 8; c++) {
-    np[c][0] = dequantise_pk(pair(c, 32 + c), q2, qq);
-    np[c][1] = dequantise_pk(pair(8 + c, 56 + c), q2, qq);
-    np[c][2] = dequantise_pk(pair(40 + c, 24 + c), q2, qq);
-    np[c][3] = dequantise_pk(pair(16 + c, 48 + c), q2, qq);
-  }
-  if (!S.inter)  // intra DC: DC x 8 (transform.c:371)
-    np[0][0] = __builtin_amdgcn_perm(np[0][0], (uint32_t)((int)(int16_t)(S.lq[0][0] & 0xffff) * 8), 0x07060100u);
-  SCHED_FENCE();
-#pragma unroll
-  for (int c = 0; c < 8; c++) {
-    idct_col_pairs(c, np[c][0], np[c][1], np[c][2], np[c][3], v);
-    SCHED_FENCE();
-  }
-  const int pw = p.plane ? w >> 1 : w;
-  const uint32_t ro = A.coded ? (uint32_t)((int64_t)p.fi * stride) + (uint32_t)plane_offset(p.plane, w, h) +
-                                    (uint32_t)(mul24(p.y, pw) + p.x)
-                              : BUF_OOB;
-  // row pass, + prediction, BoundIDctMatrix and the store, row by row: each
-  // row's values die at its store
-#pragma unroll
-  for (int k = 0; k < 8; k++) {
-    int o[8];
-    inv8<true>(v + 8 * k, o);
-#pragma unroll
-    for (int j = 0; j < 8; j++) o[j] = idct_final(o[j]);
-    const uint2 r = recon_row(o, prow[k]);
-    typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
-    u32x2 d;
-    d[0] = r.x;
-    d[1] = r.y;
-    __builtin_amdgcn_raw_buffer_store_b64(d, rec, ro + (uint32_t)mul24(k, pw), 0, 0);
-    SCHED_FENCE();
-  }
-}
 // IQ + ChenIDct + reconstruction over a wave's CODED blocks only (decoder
 // and k_inter_mbg).  A wave holds 60 blocks, typically a quarter of them with
 // levels (1.5 of 6 per MB on the bench stream), but a one-lane-per-block
@@ -853,6 +772,9 @@ __device__ __forceinline__ void rec_wave_compact(int w, int h, int64_t stride, _
 #ifndef INTER_WAVES
 #define INTER_WAVES 1u
 #endif
+#ifndef INTER_DOT
+#define INTER_DOT false  // the packed filter here: no gain measured (bench step -0.25 us, k_inter +0.9 us)
+#endif
 #ifndef RECON_WPE
 #define RECON_WPE 4
 #endif
@@ -860,13 +782,12 @@ __device__ __forceinline__ void rec_wave_compact(int w, int h, int64_t stride, _
 #ifndef REC_WAVES
 #define REC_WAVES 1u
 #endif
-#ifndef REC_COMPACT
-#define REC_COMPACT 1
-#endif
 // decoder reconstruction, MB-grouped block layout (blk_pos_mb), one block per
-// lane and no loop: 10 MBs per wave, each lane loads its MB's record, then its
-// levels and prediction, reconstructs and stores.  93 VGPRs: 5 waves per
-// SIMD, which hide each other's two dependent load latencies (a persistent
+// lane: 10 MBs per wave, each lane loads its MB's record, then its levels and
+// prediction; uncoded blocks store the prediction, coded ones go through
+// idct_coded_blocks.  85 VGPRs: 5 waves per SIMD, which hide each other's two
+// dependent load latencies (eight lanes per block: 80 VGPRs, 6 waves, but two
+// passes per wave instead of one and 1.7 us slower; a persistent
 // variant with the next block's loads in flight needed 237 VGPRs, 2 waves,
 // and was slower).  Lanes past the batch (and lanes 60..63) get coded = 0:
 // every load and store of theirs is out of range.
@@ -898,12 +819,8 @@ __global__ __launch_bounds__(64 * REC_WAVES) RECON_OCC void k_recon_mbg(int w, i
   A.coded = __builtin_amdgcn_raw_buffer_load_b8(B.mask, valid ? gmb : BUF_OOB, 0, 0);
   const RecStageB S = rec_stage_b(B, w, h, stride, A);
   PRIO_LOW();
-#if REC_COMPACT
   __shared__ uint32_t slots[REC_WAVES][rslot(DEC_LPB) * (64 / DEC_LPB)];
   rec_wave_compact(w, h, stride, rec, A, S, slots[threadIdx.x >> 6], lane);
-#else
-  rec_block_pk(w, h, stride, rec, A, S);
-#endif
 }
 
 // ---------------------------------------------------------------------------
@@ -932,7 +849,7 @@ __device__ __forceinline__ void inter_pred(const RecBufs &B, int w, int h, int64
   A.coded = 1;
   const RecStageB S = rec_stage_b<false>(B, w, h, stride, A);  // source OOB (zeros) if intra
   PRIO_LOW();  // the loads are out: the loop filter at normal priority
-  pred_rows<false>(S.pred, S.filter, prow);
+  pred_rows<INTER_DOT>(S.pred, S.filter, prow);
 }
 // the prediction as packed rows (all zero when the source was not loaded)
 template <bool DOT>
