@@ -659,9 +659,13 @@ constexpr int rslot(int lpb) { return lpb == 8 ? 88 : 84; }
 constexpr int RSLOTS_BYTES = 4 * rslot(REC_LPB) * (64 / REC_LPB);
 static_assert(RSLOTS_BYTES <= LVL_WAVE, "k_inter_mbg's slots live in its level staging");
 #define WAVE_FENCE() __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront")
-template <int LPB = REC_LPB>
+// WB: the row pass writes the reconstructed rows back into the slot and each
+// coded lane reads its block's rows into prow, so that the caller stores every
+// block of the wave with the same wave-wide row stores (contiguous 8-byte row
+// pieces of adjacent blocks); otherwise the row pass stores them itself.
+template <int LPB = REC_LPB, bool WB = false>
 __device__ __forceinline__ void idct_coded_blocks(bool ck, const uint32_t np[8][4], int q, bool intra,
-                                                  const uint2 prow[8], uint32_t ro, int pw,
+                                                  uint2 prow[8], uint32_t ro, int pw,
                                                   __amdgpu_buffer_rsrc_t rec, uint32_t *slots, int lane) {
   constexpr int NS = 64 / LPB, CPL = 8 / LPB, RS = rslot(LPB);
   const uint64_t cm = __builtin_amdgcn_ballot_w64(ck);
@@ -715,13 +719,29 @@ __device__ __forceinline__ void idct_coded_blocks(bool ck, const uint32_t np[8][
 #pragma unroll
       for (int k = 0; k < 8; k++) o[k] = idct_final(o[k]);
       const uint2 rr = recon_row(o, pr);
-      typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
-      u32x2 d;
-      d[0] = rr.x;
-      d[1] = rr.y;
-      const uint32_t off = pass + j < n ? hd.x + (uint32_t)mul24(r, (int)hd.y) : BUF_OOB;
-      __builtin_amdgcn_raw_buffer_store_b64(d, rec, off, 0, 0);
+      if (WB) {
+        *(uint2 *)(mine + RSLOT_PRED + 2 * r) = rr;  // (this lane's own row: read above)
+      } else {
+        typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+        u32x2 d;
+        d[0] = rr.x;
+        d[1] = rr.y;
+        const uint32_t off = pass + j < n ? hd.x + (uint32_t)mul24(r, (int)hd.y) : BUF_OOB;
+        __builtin_amdgcn_raw_buffer_store_b64(d, rec, off, 0, 0);
+      }
       SCHED_FENCE();
+    }
+    if (WB) {  // the pass's coded lanes take their reconstructed rows back
+      WAVE_FENCE();
+      if (ck && rank >= pass && rank < pass + NS) {
+        const uint32_t *const s = slots + RS * (rank - pass);
+#pragma unroll
+        for (int k = 0; k < 8; k += 2) {
+          const uint4 t = *(const uint4 *)(s + RSLOT_PRED + 2 * k);
+          prow[k] = make_uint2(t.x, t.y);
+          prow[k + 1] = make_uint2(t.z, t.w);
+        }
+      }
     }
   }
   WAVE_FENCE();
@@ -736,17 +756,6 @@ __device__ __forceinline__ void rec_wave_compact(int w, int h, int64_t stride, _
   const int pw = p.plane ? w >> 1 : w;
   const uint32_t ro = (uint32_t)((int64_t)p.fi * stride) + (uint32_t)plane_offset(p.plane, w, h) +
                       (uint32_t)(mul24(p.y, pw) + p.x);
-  {  // uncoded blocks of coded MBs: the prediction is the reconstruction
-    const uint32_t uo = (A.coded && !S.ck) ? ro : BUF_OOB;
-    typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
-#pragma unroll
-    for (int k = 0; k < 8; k++) {
-      u32x2 d;
-      d[0] = prow[k].x;
-      d[1] = prow[k].y;
-      __builtin_amdgcn_raw_buffer_store_b64(d, rec, uo + (uint32_t)mul24(k, pw), 0, 0);
-    }
-  }
   // natural column pairs straight from the packed zigzag words (one v_perm each)
   auto pair = [&](int e, int f) {
     const int s1 = k_zz.pos[e], s2 = k_zz.pos[f];
@@ -761,7 +770,19 @@ __device__ __forceinline__ void rec_wave_compact(int w, int h, int64_t stride, _
     np[c][2] = pair(40 + c, 24 + c);
     np[c][3] = pair(16 + c, 48 + c);
   }
-  idct_coded_blocks<DEC_LPB>(S.ck, np, A.q, !S.inter, prow, ro, pw, rec, slots, lane);
+  idct_coded_blocks<DEC_LPB, true>(S.ck, np, A.q, !S.inter, prow, ro, pw, rec, slots, lane);
+  {  // every block of a coded MB, wave-wide: the reconstruction (coded blocks,
+     // read back from the pass) or the prediction (uncoded blocks)
+    const uint32_t uo = A.coded ? ro : BUF_OOB;
+    typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      u32x2 d;
+      d[0] = prow[k].x;
+      d[1] = prow[k].y;
+      __builtin_amdgcn_raw_buffer_store_b64(d, rec, uo + (uint32_t)mul24(k, pw), 0, 0);
+    }
+  }
 }
 // occupancy targets: 4 waves per SIMD (<= 128 VGPRs)
 #define INTER_OCC __attribute__((amdgpu_waves_per_eu(4)))
@@ -771,6 +792,9 @@ __device__ __forceinline__ void rec_wave_compact(int w, int h, int64_t stride, _
 // k_intra_mbg keeps four (one-wave groups cost it 3 us)
 #ifndef INTER_WAVES
 #define INTER_WAVES 1u
+#endif
+#ifndef INTER_WB
+#define INTER_WB false
 #endif
 #ifndef INTER_DOT
 #define INTER_DOT false  // the packed filter here: no gain measured (bench step -0.25 us, k_inter +0.9 us)
@@ -1005,7 +1029,7 @@ __global__ __launch_bounds__(64 * INTER_WAVES) INTER_OCC void k_inter_mbg(p64gpu
   const uint32_t ro = (uint32_t)((int64_t)pos.fi * stride) + (uint32_t)plane_offset(pos.plane, w, h) +
                       (uint32_t)mul24(pos.y, pw) + (uint32_t)pos.x;
   // IQ + ChenIDct + reconstruction of the coded blocks, stored there
-  idct_coded_blocks(ck, np, q, intra, prow, ro, pw, recon_rsrc(a, kd, nmbs), (uint32_t *)lds, lane);
+  idct_coded_blocks<REC_LPB, INTER_WB>(ck, np, q, intra, prow, ro, pw, recon_rsrc(a, kd, nmbs), (uint32_t *)lds, lane);
   // no levels at all in the MB: the reconstruction is the new prediction
   if (repred) inter_pred(B, w, h, stride, pos, mt, mvx, mvy, prow);
   // p64.c:909-910: the record (transmitted vector only for MC types) and LastIntra
@@ -1013,7 +1037,7 @@ __global__ __launch_bounds__(64 * INTER_WAVES) INTER_OCC void k_inter_mbg(p64gpu
   const uint32_t mbw = (uint32_t)(mt & 0xff) | ((uint32_t)(cbp & 0xff) << 8) |
                        (mt_mf(mt) ? ((uint32_t)(mvx & 0xff) << 16) | ((uint32_t)(mvy & 0xff) << 24) : 0u);
   // uncoded blocks: the prediction is the reconstruction
-  mbg_store_rows(a, kd, nmbs, ck ? BUF_OOB : ro, pw, prow, rl, gmb, mbw,
+  mbg_store_rows(a, kd, nmbs, (ck && !INTER_WB) ? BUF_OOB : ro, pw, prow, rl, gmb, mbw,
                  mt_intra(mt) ? (uint8_t)0 : (uint8_t)(li + 1));
 }
 
