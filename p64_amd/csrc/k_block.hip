@@ -628,21 +628,24 @@ __device__ __forceinline__ void pred_rows(const PredSrc &P, bool filter, uint2 p
 // and k_inter_mbg).  A wave holds 60 blocks, typically a quarter of them with
 // levels (1.5 of 6 per MB on the bench stream), but a one-lane-per-block
 // transform costs the wave the same whatever that count.  Here the coded
-// blocks are ranked (ballot + mbcnt) and go through the transform eight at a
-// time with eight lanes per block: each pass, the coded lanes of rank
-// 8p..8p+7 put their raw natural level pairs (per column), prediction rows
-// and output offset into the wave's LDS slots; lane 8j+c dequantises and runs
-// the column pass of column c of slot j, lane 8j+r the row pass, the
-// reconstruction and the store of row r.  ceil(n/8) passes of one column and
-// one row per lane instead of eight of each per lane; the caller stores the
-// uncoded blocks (their prediction).  All exchanges stay inside one wave: a
+// blocks are ranked (ballot + mbcnt) and go through the transform 64/LPB at
+// a time with LPB lanes per block: each pass, the coded lanes of rank
+// NS p .. NS p + NS - 1 put their raw natural level pairs (per column) and
+// prediction rows into the wave's LDS slots; lane LPB j + g dequantises and
+// runs the column pass of columns g, g + LPB, ... of slot j, then the row
+// pass and the reconstruction of rows g, g + LPB, ..., written back over the
+// slot's prediction rows, which the block's own lane then reads back into
+// prow.  ceil(n/NS) passes of 8/LPB columns and rows per lane instead of
+// eight of each per lane; the caller stores every block (reconstruction or
+// prediction) with its wave-wide row stores.  All exchanges stay inside one wave: a
 // wave's LDS operations complete in order, so no barrier; the wavefront-scope
 // fences only keep the compiler from moving LDS accesses across an exchange.
 //   ck       this lane's block carries levels
 //   np       its raw levels as natural column pairs: np[c] = (x0c,x4c) (x1c,x7c)
 //            (x5c,x3c) (x2c,x6c), x_rc = level of row r, column c
 //   q, intra UseQuant and the intra-DC rule (DC x 8, transform.c:371)
-//   prow     prediction rows (zeros for intra); ro, pw: output offset, plane width
+//   prow     in: prediction rows (zeros for intra); out: the reconstruction
+//            if ck (else unchanged)
 // LPB lanes per block (8 or 4): a pass takes 64/LPB blocks, lane LPB*j+g
 // columns (rows) g, g+LPB, ... of slot j.  Slot: 64 row-major values, 16
 // prediction dwords, header; its stride keeps the row-major writes of the
@@ -659,14 +662,15 @@ constexpr int rslot(int lpb) { return lpb == 8 ? 88 : 84; }
 constexpr int RSLOTS_BYTES = 4 * rslot(REC_LPB) * (64 / REC_LPB);
 static_assert(RSLOTS_BYTES <= LVL_WAVE, "k_inter_mbg's slots live in its level staging");
 #define WAVE_FENCE() __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront")
-// WB: the row pass writes the reconstructed rows back into the slot and each
-// coded lane reads its block's rows into prow, so that the caller stores every
+// The row pass writes the reconstructed rows back into the slot and each
+// coded lane reads its block's rows into prow: the caller then stores every
 // block of the wave with the same wave-wide row stores (contiguous 8-byte row
-// pieces of adjacent blocks); otherwise the row pass stores them itself.
-template <int LPB = REC_LPB, bool WB = false>
+// pieces of adjacent blocks).  Stores from the pass itself (one block row per
+// lane, scattered) cost the decoder 34.3 vs 28.6 us and +14 MB of HBM writes
+// per launch, k_inter_mbg ~1.5 us.
+template <int LPB = REC_LPB>
 __device__ __forceinline__ void idct_coded_blocks(bool ck, const uint32_t np[8][4], int q, bool intra,
-                                                  uint2 prow[8], uint32_t ro, int pw,
-                                                  __amdgpu_buffer_rsrc_t rec, uint32_t *slots, int lane) {
+                                                  uint2 prow[8], uint32_t *slots, int lane) {
   constexpr int NS = 64 / LPB, CPL = 8 / LPB, RS = rslot(LPB);
   const uint64_t cm = __builtin_amdgcn_ballot_w64(ck);
   const int n = __builtin_popcountll(cm);
@@ -682,7 +686,7 @@ __device__ __forceinline__ void idct_coded_blocks(bool ck, const uint32_t np[8][
 #pragma unroll
       for (int k = 0; k < 8; k += 2)
         *(uint4 *)(s + RSLOT_PRED + 2 * k) = make_uint4(prow[k].x, prow[k].y, prow[k + 1].x, prow[k + 1].y);
-      *(uint4 *)(s + RSLOT_HDR) = make_uint4((uint32_t)q | (intra ? 0x100u : 0u), ro, (uint32_t)pw, 0u);
+      *(uint4 *)(s + RSLOT_HDR) = make_uint4((uint32_t)q | (intra ? 0x100u : 0u), 0u, 0u, 0u);
     }
     WAVE_FENCE();
     {  // column pass: columns g + LPB i of slot j, written back row-major in place
@@ -712,35 +716,23 @@ __device__ __forceinline__ void idct_coded_blocks(bool ck, const uint32_t np[8][
       const int r = g + LPB * i;
       const uint4 x0 = *(const uint4 *)(mine + 8 * r), x1 = *(const uint4 *)(mine + 8 * r + 4);
       const uint2 pr = *(const uint2 *)(mine + RSLOT_PRED + 2 * r);
-      const uint2 hd = *(const uint2 *)(mine + RSLOT_HDR + 1);  // ro, pw
       const int x[8] = {(int)x0.x, (int)x0.y, (int)x0.z, (int)x0.w, (int)x1.x, (int)x1.y, (int)x1.z, (int)x1.w};
       int o[8];
       inv8<true>(x, o);
 #pragma unroll
       for (int k = 0; k < 8; k++) o[k] = idct_final(o[k]);
       const uint2 rr = recon_row(o, pr);
-      if (WB) {
-        *(uint2 *)(mine + RSLOT_PRED + 2 * r) = rr;  // (this lane's own row: read above)
-      } else {
-        typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
-        u32x2 d;
-        d[0] = rr.x;
-        d[1] = rr.y;
-        const uint32_t off = pass + j < n ? hd.x + (uint32_t)mul24(r, (int)hd.y) : BUF_OOB;
-        __builtin_amdgcn_raw_buffer_store_b64(d, rec, off, 0, 0);
-      }
+      *(uint2 *)(mine + RSLOT_PRED + 2 * r) = rr;  // (this lane's own row: read above)
       SCHED_FENCE();
     }
-    if (WB) {  // the pass's coded lanes take their reconstructed rows back
-      WAVE_FENCE();
-      if (ck && rank >= pass && rank < pass + NS) {
-        const uint32_t *const s = slots + RS * (rank - pass);
+    WAVE_FENCE();  // the pass's coded lanes take their reconstructed rows back
+    if (ck && rank >= pass && rank < pass + NS) {
+      const uint32_t *const s = slots + RS * (rank - pass);
 #pragma unroll
-        for (int k = 0; k < 8; k += 2) {
-          const uint4 t = *(const uint4 *)(s + RSLOT_PRED + 2 * k);
-          prow[k] = make_uint2(t.x, t.y);
-          prow[k + 1] = make_uint2(t.z, t.w);
-        }
+      for (int k = 0; k < 8; k += 2) {
+        const uint4 t = *(const uint4 *)(s + RSLOT_PRED + 2 * k);
+        prow[k] = make_uint2(t.x, t.y);
+        prow[k + 1] = make_uint2(t.z, t.w);
       }
     }
   }
@@ -770,7 +762,7 @@ __device__ __forceinline__ void rec_wave_compact(int w, int h, int64_t stride, _
     np[c][2] = pair(40 + c, 24 + c);
     np[c][3] = pair(16 + c, 48 + c);
   }
-  idct_coded_blocks<DEC_LPB, true>(S.ck, np, A.q, !S.inter, prow, ro, pw, rec, slots, lane);
+  idct_coded_blocks<DEC_LPB>(S.ck, np, A.q, !S.inter, prow, slots, lane);
   {  // every block of a coded MB, wave-wide: the reconstruction (coded blocks,
      // read back from the pass) or the prediction (uncoded blocks)
     const uint32_t uo = A.coded ? ro : BUF_OOB;
@@ -792,9 +784,6 @@ __device__ __forceinline__ void rec_wave_compact(int w, int h, int64_t stride, _
 // k_intra_mbg keeps four (one-wave groups cost it 3 us)
 #ifndef INTER_WAVES
 #define INTER_WAVES 1u
-#endif
-#ifndef INTER_WB
-#define INTER_WB false
 #endif
 #ifndef INTER_DOT
 #define INTER_DOT false  // the packed filter here: no gain measured (bench step -0.25 us, k_inter +0.9 us)
@@ -1028,16 +1017,16 @@ __global__ __launch_bounds__(64 * INTER_WAVES) INTER_OCC void k_inter_mbg(p64gpu
   const int pw = pos.plane ? w >> 1 : w;
   const uint32_t ro = (uint32_t)((int64_t)pos.fi * stride) + (uint32_t)plane_offset(pos.plane, w, h) +
                       (uint32_t)mul24(pos.y, pw) + (uint32_t)pos.x;
-  // IQ + ChenIDct + reconstruction of the coded blocks, stored there
-  idct_coded_blocks<REC_LPB, INTER_WB>(ck, np, q, intra, prow, ro, pw, recon_rsrc(a, kd, nmbs), (uint32_t *)lds, lane);
+  // IQ + ChenIDct + reconstruction of the coded blocks, into their prow
+  idct_coded_blocks(ck, np, q, intra, prow, (uint32_t *)lds, lane);
   // no levels at all in the MB: the reconstruction is the new prediction
   if (repred) inter_pred(B, w, h, stride, pos, mt, mvx, mvy, prow);
   // p64.c:909-910: the record (transmitted vector only for MC types) and LastIntra
   const bool rl = b == 0 && lane < 6 * MBS_PER_WAVE && gmb0 + (unsigned)(l / 6) < nmbs;
   const uint32_t mbw = (uint32_t)(mt & 0xff) | ((uint32_t)(cbp & 0xff) << 8) |
                        (mt_mf(mt) ? ((uint32_t)(mvx & 0xff) << 16) | ((uint32_t)(mvy & 0xff) << 24) : 0u);
-  // uncoded blocks: the prediction is the reconstruction
-  mbg_store_rows(a, kd, nmbs, (ck && !INTER_WB) ? BUF_OOB : ro, pw, prow, rl, gmb, mbw,
+  // every block: the reconstruction (coded) or the prediction (uncoded)
+  mbg_store_rows(a, kd, nmbs, ro, pw, prow, rl, gmb, mbw,
                  mt_intra(mt) ? (uint8_t)0 : (uint8_t)(li + 1));
 }
 
