@@ -797,8 +797,8 @@ __device__ __forceinline__ void rec_wave_compact(int w, int h, int64_t stride, _
 #endif
 // decoder reconstruction, MB-grouped block layout (blk_pos_mb), one block per
 // lane: 10 MBs per wave, each lane loads its MB's record, then its levels and
-// prediction; uncoded blocks store the prediction, coded ones go through
-// idct_coded_blocks.  85 VGPRs: 5 waves per SIMD, which hide each other's two
+// prediction; coded blocks go through idct_coded_blocks, then every block
+// stores its rows (reconstruction or prediction) wave-wide.  87 VGPRs: 5 waves per SIMD, which hide each other's two
 // dependent load latencies (eight lanes per block: 80 VGPRs, 6 waves, but two
 // passes per wave instead of one and 1.7 us slower; a persistent
 // variant with the next block's loads in flight needed 237 VGPRs, 2 waves,
