@@ -94,8 +94,8 @@ __device__ __forceinline__ BlkPos blk_pos_mb(unsigned gmb, int b, int w, int h, 
   return p;
 }
 // ChenDct (chendct.c:97-206) on a register block given as its 8 packed pixel
-// rows (or the residual rows - prow), the row pass in packed 16-bit
-// arithmetic: the column pass (scalar) leaves each row as four (column 2j, 2j+1) int16 pairs -- its
+// rows (or the residual rows - prow), both passes in packed 16-bit
+// arithmetic: the column pass (fwd_col_pk, below) leaves each row as four (column 2j, 2j+1) int16 pairs -- its
 // outputs stay within +-5,800 for pixel or +-255 residual input -- and the
 // row pass runs the butterfly of fwd8 on pairs: v_pk_add/sub/ashr for the
 // sums, and every product pair C_a x + C_b y as ONE v_dot2_i32_i16 with the
@@ -134,6 +134,35 @@ __device__ __forceinline__ void fwd_row_pk(const s16x2 p[4], int o[8]) {
   o[3] = ms9(dot2(u12, -C5D16, C3D16));
   o[5] = ms9(dot2(u12, C3D16, C5D16));
 }
+// column pass of one column given as its packed row pairs (x0,x1), (x2,x3),
+// (x4,x5), (x6,x7): fwd8<N, 4> (chendct.c:120-159) with the pairs of butterfly
+// terms packed the way fwd_row_pk packs them -- no >>1, the <<2 input scale
+// folded into the dot-product constants (<= 4 x 502 = 2,008, int16) except
+// for d0, d3, which are added to products and shift themselves.  Pixel or
+// residual input (|x| <= 255): sums <= 1,020, u = 4d + r <= 2,462, every
+// intermediate inside int16; the products and their sums exact in 32 bits.
+__device__ __forceinline__ void fwd_col_pk(const s16x2 p[4], int o[8]) {
+  const s16x2 s01 = p[0] + p[3].yx, s23 = p[1] + p[2].yx;  // (s0,s1) (s2,s3)
+  const s16x2 d01 = p[0] - p[3].yx, d23 = p[1] - p[2].yx;  // (d0,d1) (d2,d3)
+  const s16x2 e01 = s01 + s23.yx, e32 = s01 - s23.yx;      // (e0,e1) (e3,e2)
+  o[0] = ms9(dot2(e01, 4 * C1D4, 4 * C1D4));
+  o[4] = ms9(dot2(e01, 4 * C1D4, -4 * C1D4));
+  o[2] = ms9(dot2(e32, 4 * C1D8, 4 * C3D8));   // 4 C3D8 e2 + 4 C1D8 e3
+  o[6] = ms9(dot2(e32, 4 * C3D8, -4 * C1D8));  // 4 C3D8 e3 - 4 C1D8 e2
+  const s16x2 q = __builtin_shufflevector(d01, d23, 1, 2);  // (d1, d2)
+  const int r1 = ms9(dot2(q, 4 * C1D4, 4 * C1D4)), r0 = ms9(dot2(q, 4 * C1D4, -4 * C1D4));
+  const s16x2 dd = __builtin_shufflevector(d23, d01, 1, 2) << 2;  // (4 d3, 4 d0)
+  const s16x2 rr = pk16(r0, r1);
+  const s16x2 u03 = dd + rr, u12 = dd - rr;  // (u0,u3) (u1,u2)
+  o[1] = ms9(dot2(u03, C7D16, C1D16));
+  o[7] = ms9(dot2(u03, -C1D16, C7D16));
+  o[3] = ms9(dot2(u12, -C5D16, C3D16));
+  o[5] = ms9(dot2(u12, C3D16, C5D16));
+}
+// byte b of w0 and of w1 zero-extended into the two int16 halves
+__device__ __forceinline__ s16x2 byte_pair(uint32_t w1, uint32_t w0, int b) {
+  return __builtin_bit_cast(s16x2, __builtin_amdgcn_perm(w1, w0, 0x0c000c00u | ((uint32_t)(4 + b) << 16) | (uint32_t)b));
+}
 // (the final rounding dct_final(v) reads the sign of v = X >> 9; hipcc then
 // takes it from X itself and keeps all 64 pre-shift sums alive next to the
 // shifted coefficients until quantisation -- 64 extra VGPRs.  The opaque copy
@@ -144,20 +173,21 @@ __device__ __forceinline__ void fdct_block_pk(const uint2 rows[8], int v[64], co
   s16x2 p[8][4];  // [row][column pair]
 #pragma unroll
   for (int c = 0; c < 8; c += 2) {
-    int x[8], y[8], o[8], u[8];
+    s16x2 x[4], y[4];  // columns c and c + 1 as row pairs
+    int o[8], u[8];
 #pragma unroll
-    for (int k = 0; k < 8; k++) {
-      const uint32_t wd = c < 4 ? rows[k].x : rows[k].y;
-      x[k] = (int)((wd >> (8 * (c & 3))) & 255);
-      y[k] = (int)((wd >> (8 * ((c + 1) & 3))) & 255);
+    for (int j = 0; j < 4; j++) {
+      const uint32_t w0 = c < 4 ? rows[2 * j].x : rows[2 * j].y, w1 = c < 4 ? rows[2 * j + 1].x : rows[2 * j + 1].y;
+      x[j] = byte_pair(w1, w0, c & 3);
+      y[j] = byte_pair(w1, w0, (c + 1) & 3);
       if (RES) {
-        const uint32_t pd = c < 4 ? prow[k].x : prow[k].y;
-        x[k] -= (int)((pd >> (8 * (c & 3))) & 255);
-        y[k] -= (int)((pd >> (8 * ((c + 1) & 3))) & 255);
+        const uint32_t q0 = c < 4 ? prow[2 * j].x : prow[2 * j].y, q1 = c < 4 ? prow[2 * j + 1].x : prow[2 * j + 1].y;
+        x[j] -= byte_pair(q1, q0, c & 3);
+        y[j] -= byte_pair(q1, q0, (c + 1) & 3);
       }
     }
-    fwd_col<true>(x, o);
-    fwd_col<true>(y, u);
+    fwd_col_pk(x, o);
+    fwd_col_pk(y, u);
 #pragma unroll
     for (int k = 0; k < 8; k++) p[k][c >> 1] = pk16(o[k], u[k]);
     SCHED_FENCE();
