@@ -162,8 +162,10 @@ typedef struct {
  * kernels use 16-byte vector and dword record accesses); frame_stride a
  * multiple of 16.  Otherwise P64GPU_E_INVALID.
  * Inter pictures with args->me == NULL keep their ME records in a library
- * scratch buffer private to the (device, stream) of the call; see
- * p64gpu_release_scratch. */
+ * scratch buffer private to the (device, stream) of the call -- and to the
+ * calling thread for hipStreamPerThread; see p64gpu_release_scratch.  While
+ * the stream is capturing, such a call takes the fused kernel instead (a
+ * graph never references library scratch). */
 int p64gpu_encode_frames(const p64gpu_encode_args *args, void *stream);
 /* The same for one picture (args->nframes == 1) restricted to the count
  * macroblocks listed in mb_list (device array of raster indices; entries out
@@ -175,9 +177,8 @@ int p64gpu_encode_mb_list(const p64gpu_encode_args *args, const int32_t *mb_list
 
 /* Frees the ME-record scratch buffers the library allocated for inter encodes
  * without args->me (one per device and stream; outgrown ones are kept until
- * this call, because a HIP graph captured earlier may still reference them).
- * Call only when no such encode is in flight and no graph that captured one
- * will be replayed. */
+ * this call, because work still in flight may reference them).  Call only
+ * when no such encode is in flight. */
 int p64gpu_release_scratch(void);
 
 /* ---- decoder-side reconstruction (device pointers) ---------------------- */
@@ -243,6 +244,13 @@ void p64_synth_frame(uint32_t seed, int frame, int width, int height,
 int p64gpu_synth_frames(int width, int height, uint32_t seed0, int nseeds,
                         int frame0, int nslots, int64_t frame_stride,
                         uint8_t *out, void *stream);
+
+/* Clock probe (measurement aid; no reference counterpart): runs
+ * v_sad_u8 chains on every SIMD for `microseconds`, then reports the median
+ * shader clock the waves held (s_memtime ticks / s_memrealtime ticks x
+ * 100 MHz).  Synchronises the stream.  bench.py reads the clock a timed
+ * region left the chip at with a short probe after it. */
+int p64gpu_clock_probe(int microseconds, int *mhz, void *stream);
 
 #ifdef __cplusplus
 }

@@ -118,6 +118,7 @@ def lib() -> ctypes.CDLL:
     L.p64gpu_encoder_close.argtypes = [vp]
     L.p64gpu_encoder_close.restype = None
     L.p64gpu_synth_frames.argtypes = [i32, i32, ctypes.c_uint32, i32, i32, i32, i64, vp, vp]
+    L.p64gpu_clock_probe.argtypes = [i32, ctypes.POINTER(i32), vp]
     L.p64_synth_frame.argtypes = [ctypes.c_uint32, i32, i32, i32, vp]
     L.p64_synth_frame.restype = None
     L.p64_synth_motion.argtypes = [ctypes.c_uint32, ctypes.POINTER(i32), ctypes.POINTER(i32)]
@@ -246,6 +247,16 @@ def _dev_check(t, dtype, name):
         raise P64GpuError(f"{name} must be a device tensor")
     if t.dtype != dtype or not t.is_contiguous():
         raise P64GpuError(f"{name} must be contiguous {dtype}")
+
+
+def clock_probe(microseconds: int) -> int:
+    """Median shader clock (MHz) the chip holds while every SIMD runs v_sad_u8
+    chains for `microseconds` (p64gpu_clock_probe; synchronises the current
+    stream)."""
+    torch = _torch()
+    mhz = ctypes.c_int(0)
+    _check(lib().p64gpu_clock_probe(int(microseconds), ctypes.byref(mhz), _stream(torch)))
+    return mhz.value
 
 
 def block_op(op: int, blocks, dcq: int = 8, acq: int = 8, out=None):

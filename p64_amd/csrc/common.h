@@ -13,12 +13,10 @@
 
 #include "../../include/p64gpu.h"
 
-// -DP64_SECTIONS marks kernel phases in the ISA listing (tools/section_census.py)
-#if defined(P64_SECTIONS)
-#define SECTION(name) asm volatile(";## " name)
-#else
+// phase labels of the search kernels: no code; the development tools
+// (tools/me_stamps.py, tools/me_variants.py, tools/section_census.py) rewrite
+// them in a copy of the source into timestamps or ISA markers
 #define SECTION(name)
-#endif
 
 namespace {
 
@@ -490,9 +488,8 @@ constexpr uint32_t BUF_OOB = 0x80000000u;  // >= every buffer's num_records: loa
 // MB-grouped block layout (k_block.hip): a wave takes 10 consecutive
 // macroblocks, lane 6m + b block b of its m-th MB (lanes 60..63 idle)
 constexpr int MBS_PER_WAVE = 10;
-// waves per workgroup of those kernels (each wave is independent)
-#ifndef MBG_WAVES
-#define MBG_WAVES 4u
-#endif
+// waves per workgroup of k_intra_mbg (each wave is independent; one-wave
+// groups cost it 3 us)
+constexpr unsigned MBG_WAVES = 4u;
 
 }  // namespace

@@ -114,9 +114,52 @@ __global__ __launch_bounds__(256) void k_synth(int w, int h, uint32_t seed0, int
   }
 }
 
+// Clock probe and spin-up (measurement aid, bench.py): every wave issues
+// chains of v_sad_u8 -- k_motion's dominant instruction -- until `ticks` of
+// the 100 MHz real-time counter have passed, then records how many shader
+// clock ticks (s_memtime) and real-time ticks the span took: the clock the
+// chip held over the span is their ratio x 100 MHz.  A short probe right
+// after a timed region reads the clock the workload left the chip at (the
+// chip ramps its clocks over tens of ms of load, and this dense v_sad_u8
+// load itself holds a lower clock than the search kernels do).
+// out: [waves][2] (shader ticks, real-time ticks), vector stores only.
+__global__ __launch_bounds__(256) void k_clock(uint32_t ticks, uint32_t *out) {
+  const uint64_t r0 = __builtin_amdgcn_s_memrealtime();
+  const uint64_t c0 = __builtin_amdgcn_s_memtime();
+  uint32_t a0 = threadIdx.x * 0x01010101u, a1 = a0 ^ 0x5a5a5a5au, a2 = a0 + 0x10203040u, a3 = ~a0;
+  const uint32_t b = blockIdx.x * 0x9e3779b1u;
+  uint64_t r = r0;
+  while ((uint32_t)(r - r0) < ticks) {  // uniform: a scalar loop
+#pragma unroll
+    for (int i = 0; i < 32; i++) {  // four independent chains
+      a0 = sad4(a0, b, a0);
+      a1 = sad4(a1, b, a1);
+      a2 = sad4(a2, b, a2);
+      a3 = sad4(a3, b, a3);
+    }
+    r = __builtin_amdgcn_s_memrealtime();
+  }
+  const uint64_t c1 = __builtin_amdgcn_s_memtime();
+  const unsigned wave = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if ((threadIdx.x & 63) == 0) {
+    out[2 * wave] = (uint32_t)(c1 - c0);
+    // the chains' results decide nothing but must not be optimised away: a
+    // real-time count of 0 is impossible, so the OR below never changes it
+    out[2 * wave + 1] = (uint32_t)(r - r0) | ((a0 ^ a1 ^ a2 ^ a3) == 0x7fffffffu && r == r0 ? 1u : 0u);
+  }
+}
+
 }  // namespace
 
 namespace p64k {
+
+unsigned clock_waves() { return 2048u * 4u; }
+
+hipError_t clock(uint32_t ticks, uint32_t *out, hipStream_t st) {
+  hipLaunchKernelGGL(k_clock, dim3(2048), dim3(256), 0, st, ticks, out);
+  return hipGetLastError();
+}
+
 
 hipError_t block_op(int op, const int32_t *in, int32_t *out, int64_t nblocks, int dcq, int acq,
                     hipStream_t st) {

@@ -59,6 +59,10 @@ __device__ __forceinline__ int qlevel_int(int v, const p64_qint &t) {
 // would trade registers for ILP the block layout does not need: other waves
 // hide latency)
 #define SCHED_FENCE() __builtin_amdgcn_sched_barrier(0)
+// orders a wave's LDS accesses across a lane exchange at the IR level (a
+// wave's LDS operations complete in order; the fence only stops the compiler
+// from moving them across the exchange)
+#define WAVE_FENCE() __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront")
 
 // A wave issues its loads at raised priority, so a freshly launched wave gets
 // its requests out ahead of the older waves' arithmetic
@@ -392,6 +396,7 @@ __device__ __forceinline__ void mbg_store_levels(const p64gpu_encode_args &a, co
   const __amdgpu_buffer_rsrc_t coef =
       __builtin_amdgcn_make_buffer_rsrc((void *)a.coef, (short)0, (int)(nmbs * 768u), BUF_RSRC_W3);
   const uint32_t nbytes = nvalid * 768u;
+  WAVE_FENCE();  // the staging writes (put_levels, every lane) before these reads
   __builtin_amdgcn_wave_barrier();
 #pragma unroll
   for (int k = 0; k < 8; k++) {
@@ -406,6 +411,7 @@ __device__ __forceinline__ void mbg_store_levels(const p64gpu_encode_args &a, co
     __builtin_amdgcn_raw_buffer_store_b128(d, coef, ob < nbytes ? gmb0 * 768u + ob : BUF_OOB, 0, 0);
   }
   __builtin_amdgcn_wave_barrier();
+  WAVE_FENCE();  // these reads before the staging is reused (idct_coded_blocks' slots)
 }
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t recon_rsrc(const p64gpu_encode_args &a, const BlkDiv &kd,
                                                              unsigned nmbs) {
@@ -473,10 +479,6 @@ __device__ __forceinline__ void pred_row(const PredSrc &p, int r, int s[8]) {
   unpack8(align4(p.d[r][1], p.d[r][0], p.sh), align4(p.d[r][2], p.d[r][1], p.sh), s);
 }
 // horizontal taps of the H.261 loop filter: [1 2 1], edge columns x4.
-// DOT: each tap sum one byte dot product (v_dot4_u32_u8) of the packed
-// source row with the taps as byte weights, no unpacking (decoder: -0.5 us);
-// otherwise unpacked adds (the inter encoder measured 2.7 us slower with the
-// dot products, although it issues ~90 fewer VALU per wave)
 // the horizontal taps of a row as four packed 16-bit pairs (hz_2i, hz_2i+1):
 // every tap sum is at most 4 x 255 = 1,020
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
@@ -520,21 +522,8 @@ __device__ __forceinline__ void pred_rows_filter_pk(const PredSrc &P, uint2 prow
     if (r + 2 < 8) hz_row_pk(P, r + 2, hn);
   }
 }
-template <bool DOT>
+// unpacked (k_inter_mbg: the packed form of the decoder measured no gain there)
 __device__ __forceinline__ void hz_row(const PredSrc &p, int r, int hz[8]) {
-  if (DOT) {
-    const uint32_t lo = align4(p.d[r][1], p.d[r][0], p.sh), hi = align4(p.d[r][2], p.d[r][1], p.sh);
-    const uint32_t mid = align4(hi, lo, 2);  // pixels 2..5
-    hz[0] = (int)__builtin_amdgcn_udot4(lo, 0x00000004u, 0u, false);
-    hz[1] = (int)__builtin_amdgcn_udot4(lo, 0x00010201u, 0u, false);
-    hz[2] = (int)__builtin_amdgcn_udot4(lo, 0x01020100u, 0u, false);
-    hz[3] = (int)__builtin_amdgcn_udot4(mid, 0x00010201u, 0u, false);
-    hz[4] = (int)__builtin_amdgcn_udot4(mid, 0x01020100u, 0u, false);
-    hz[5] = (int)__builtin_amdgcn_udot4(hi, 0x00010201u, 0u, false);
-    hz[6] = (int)__builtin_amdgcn_udot4(hi, 0x01020100u, 0u, false);
-    hz[7] = (int)__builtin_amdgcn_udot4(hi, 0x04000000u, 0u, false);
-    return;
-  }
   int s[8];
   pred_row(p, r, s);
   hz[0] = s[0] << 2;
@@ -652,7 +641,7 @@ __device__ __forceinline__ uint2 recon_row(const int v[8], uint2 pr) {
   }
   return make_uint2(__builtin_amdgcn_perm(o2[1], o2[0], 0x05040100u), __builtin_amdgcn_perm(o2[3], o2[2], 0x05040100u));
 }
-template <bool DOT>
+template <bool PK>
 __device__ __forceinline__ void pred_rows(const PredSrc &P, bool filter, uint2 prow[8]);
 // IQ + ChenIDct + reconstruction over a wave's CODED blocks only (decoder
 // and k_inter_mbg).  A wave holds 60 blocks, typically a quarter of them with
@@ -676,32 +665,23 @@ __device__ __forceinline__ void pred_rows(const PredSrc &P, bool filter, uint2 p
 //   q, intra UseQuant and the intra-DC rule (DC x 8, transform.c:371)
 //   prow     in: prediction rows (zeros for intra); out: the reconstruction
 //            if ck (else unchanged)
-// LPB lanes per block (8 or 4): a pass takes 64/LPB blocks, lane LPB*j+g
-// columns (rows) g, g+LPB, ... of slot j.  Slot: 64 row-major values, 16
-// prediction dwords, header; its stride keeps the row-major writes of the
-// column pass free of bank conflicts (88 = 24 mod 64 for eight lanes per block,
-// 84 = 20 mod 64 for four)
-#ifndef REC_LPB
-#define REC_LPB 4
-#endif
-constexpr int RSLOT_PRED = 64, RSLOT_HDR = 80;
-constexpr int rslot(int lpb) { return lpb == 8 ? 88 : 84; }
-#ifndef DEC_LPB
-#define DEC_LPB REC_LPB
-#endif
-constexpr int RSLOTS_BYTES = 4 * rslot(REC_LPB) * (64 / REC_LPB);
+// Four lanes per block: a pass takes 16 blocks, lane 4j+g columns (rows) g,
+// g+4 of slot j (eight lanes per block, 8 blocks a pass, measured 1.7 us
+// slower in the decoder).  Slot: 64 row-major values, 16 prediction dwords,
+// header; its stride (84 = 20 mod 64) keeps the row-major writes of the
+// column pass free of bank conflicts.
+constexpr int LPB = 4, RSLOT = 84, RSLOT_PRED = 64, RSLOT_HDR = 80;
+constexpr int RSLOTS_BYTES = 4 * RSLOT * (64 / LPB);
 static_assert(RSLOTS_BYTES <= LVL_WAVE, "k_inter_mbg's slots live in its level staging");
-#define WAVE_FENCE() __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront")
 // The row pass writes the reconstructed rows back into the slot and each
 // coded lane reads its block's rows into prow: the caller then stores every
 // block of the wave with the same wave-wide row stores (contiguous 8-byte row
 // pieces of adjacent blocks).  Stores from the pass itself (one block row per
 // lane, scattered) cost the decoder 34.3 vs 28.6 us and +14 MB of HBM writes
 // per launch, k_inter_mbg ~1.5 us.
-template <int LPB = REC_LPB>
 __device__ __forceinline__ void idct_coded_blocks(bool ck, const uint32_t np[8][4], int q, bool intra,
                                                   uint2 prow[8], uint32_t *slots, int lane) {
-  constexpr int NS = 64 / LPB, CPL = 8 / LPB, RS = rslot(LPB);
+  constexpr int NS = 64 / LPB, CPL = 8 / LPB, RS = RSLOT;
   const uint64_t cm = __builtin_amdgcn_ballot_w64(ck);
   const int n = __builtin_popcountll(cm);
   const int rank = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(cm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)cm, 0u));
@@ -792,7 +772,7 @@ __device__ __forceinline__ void rec_wave_compact(int w, int h, int64_t stride, _
     np[c][2] = pair(40 + c, 24 + c);
     np[c][3] = pair(16 + c, 48 + c);
   }
-  idct_coded_blocks<DEC_LPB>(S.ck, np, A.q, !S.inter, prow, slots, lane);
+  idct_coded_blocks(S.ck, np, A.q, !S.inter, prow, slots, lane);
   {  // every block of a coded MB, wave-wide: the reconstruction (coded blocks,
      // read back from the pass) or the prediction (uncoded blocks)
     const uint32_t uo = A.coded ? ro : BUF_OOB;
@@ -806,25 +786,11 @@ __device__ __forceinline__ void rec_wave_compact(int w, int h, int64_t stride, _
     }
   }
 }
-// occupancy targets: 4 waves per SIMD (<= 128 VGPRs)
-#define INTER_OCC __attribute__((amdgpu_waves_per_eu(4)))
-// workgroup sizes: the decoder and the inter encoder run one-wave workgroups
-// (a wave's slot and its LDS free as soon as it ends; with the priority
-// raised first, that is -1.5 us for the decoder and -1 us for k_inter_mbg);
-// k_intra_mbg keeps four (one-wave groups cost it 3 us)
-#ifndef INTER_WAVES
-#define INTER_WAVES 1u
-#endif
-#ifndef INTER_DOT
-#define INTER_DOT false  // the packed filter here: no gain measured (bench step -0.25 us, k_inter +0.9 us)
-#endif
-#ifndef RECON_WPE
-#define RECON_WPE 4
-#endif
-#define RECON_OCC __attribute__((amdgpu_waves_per_eu(RECON_WPE)))
-#ifndef REC_WAVES
-#define REC_WAVES 1u
-#endif
+// occupancy target of k_inter_mbg and k_recon_mbg: at least 4 waves per
+// SIMD (<= 128 VGPRs).  Both run one-wave workgroups: a wave's slot and its
+// LDS free as soon as it ends (with the priority raised first, -1.5 us for
+// the decoder and -1 us for k_inter_mbg); k_intra_mbg keeps four (MBG_WAVES).
+#define OCC4 __attribute__((amdgpu_waves_per_eu(4)))
 // decoder reconstruction, MB-grouped block layout (blk_pos_mb), one block per
 // lane: 10 MBs per wave, each lane loads its MB's record, then its levels and
 // prediction; coded blocks go through idct_coded_blocks, then every block
@@ -834,12 +800,12 @@ __device__ __forceinline__ void rec_wave_compact(int w, int h, int64_t stride, _
 // variant with the next block's loads in flight needed 237 VGPRs, 2 waves,
 // and was slower).  Lanes past the batch (and lanes 60..63) get coded = 0:
 // every load and store of theirs is out of range.
-__global__ __launch_bounds__(64 * REC_WAVES) RECON_OCC void k_recon_mbg(int w, int h, int64_t stride, const uint8_t *refp,
+__global__ __launch_bounds__(64) OCC4 void k_recon_mbg(int w, int h, int64_t stride, const uint8_t *refp,
                                                            uint8_t *recp, const int16_t *coef,
                                                            const p64_mb_rec *mbr, const uint8_t *quant_mb,
                                                            const uint8_t *coded_mask, BlkDiv kd, unsigned nmbs) {
   const int lane = threadIdx.x & 63;
-  const unsigned gmb0 = (xcd_remap(blockIdx.x, gridDim.x) * REC_WAVES + (threadIdx.x >> 6)) * MBS_PER_WAVE;
+  const unsigned gmb0 = xcd_remap(blockIdx.x, gridDim.x) * MBS_PER_WAVE;
   if (gmb0 >= nmbs) return;  // whole wave
   PRIO_HIGH();
   const int nmb = (w >> 4) * (h >> 4), nfr = (int)mdiv(nmbs, kd.mn, kd.sn);
@@ -862,8 +828,8 @@ __global__ __launch_bounds__(64 * REC_WAVES) RECON_OCC void k_recon_mbg(int w, i
   A.coded = __builtin_amdgcn_raw_buffer_load_b8(B.mask, valid ? gmb : BUF_OOB, 0, 0);
   const RecStageB S = rec_stage_b(B, w, h, stride, A);
   PRIO_LOW();
-  __shared__ uint32_t slots[REC_WAVES][rslot(DEC_LPB) * (64 / DEC_LPB)];
-  rec_wave_compact(w, h, stride, rec, A, S, slots[threadIdx.x >> 6], lane);
+  __shared__ uint32_t slots[RSLOT * (64 / LPB)];
+  rec_wave_compact(w, h, stride, rec, A, S, slots, lane);
 }
 
 // ---------------------------------------------------------------------------
@@ -877,7 +843,7 @@ __global__ __launch_bounds__(64 * REC_WAVES) RECON_OCC void k_recon_mbg(int w, i
 // reconstruction.  The fused one-wave-per-MB k_encode spends 40% of its time
 // in this half with 48 of 64 lanes busy on LDS-exchanged row passes; here
 // every lane holds its block in registers.
-template <bool DOT>
+template <bool PK>
 __device__ __forceinline__ void pred_rows(const PredSrc &P, bool filter, uint2 prow[8]);
 struct InterMe {  // the fields of p64_me_rec the decision needs
   int mx, my, sad, sad0, var, varor;
@@ -892,17 +858,18 @@ __device__ __forceinline__ void inter_pred(const RecBufs &B, int w, int h, int64
   A.coded = 1;
   const RecStageB S = rec_stage_b<false>(B, w, h, stride, A);  // source OOB (zeros) if intra
   PRIO_LOW();  // the loads are out: the loop filter at normal priority
-  pred_rows<INTER_DOT>(S.pred, S.filter, prow);
+  pred_rows<false>(S.pred, S.filter, prow);
 }
-// the prediction as packed rows (all zero when the source was not loaded)
-template <bool DOT>
+// the prediction as packed rows (all zero when the source was not loaded);
+// PK: the loop filter in packed 16-bit arithmetic (decoder)
+template <bool PK>
 __device__ __forceinline__ void pred_rows(const PredSrc &P, bool filter, uint2 prow[8]) {
-  if (DOT && filter) {
+  if (PK && filter) {
     pred_rows_filter_pk(P, prow);
   } else if (filter) {  // add_pred's loop filter, one packed row at a time
     int hp[8], hc[8], hn[8];
-    hz_row<DOT>(P, 0, hc);
-    hz_row<DOT>(P, 1, hn);
+    hz_row(P, 0, hc);
+    hz_row(P, 1, hn);
 #pragma unroll
     for (int r = 0; r < 8; r++) {
       int o[8];
@@ -915,7 +882,7 @@ __device__ __forceinline__ void pred_rows(const PredSrc &P, bool filter, uint2 p
         hp[k] = hc[k];
         hc[k] = hn[k];
       }
-      if (r + 2 < 8) hz_row<DOT>(P, r + 2, hn);
+      if (r + 2 < 8) hz_row(P, r + 2, hn);
     }
   } else {  // the source rows as they are
 #pragma unroll
@@ -924,12 +891,11 @@ __device__ __forceinline__ void pred_rows(const PredSrc &P, bool filter, uint2 p
   }
 }
 template <bool QMB>
-__global__ __launch_bounds__(64 * INTER_WAVES) INTER_OCC void k_inter_mbg(p64gpu_encode_args a, BlkDiv kd, unsigned nmbs,
+__global__ __launch_bounds__(64) OCC4 void k_inter_mbg(p64gpu_encode_args a, BlkDiv kd, unsigned nmbs,
                                                              const p64_me_rec *me) {
-  __shared__ __align__(16) uint8_t lvl[INTER_WAVES * LVL_WAVE];
-  const int lane = threadIdx.x & 63;
-  uint8_t *lds = lvl + (threadIdx.x >> 6) * LVL_WAVE;
-  const unsigned gmb0 = (xcd_remap(blockIdx.x, gridDim.x) * INTER_WAVES + (threadIdx.x >> 6)) * MBS_PER_WAVE;
+  __shared__ __align__(16) uint8_t lds[LVL_WAVE];
+  const int lane = threadIdx.x;
+  const unsigned gmb0 = xcd_remap(blockIdx.x, gridDim.x) * MBS_PER_WAVE;
   if (gmb0 >= nmbs) return;  // whole wave
   PRIO_HIGH();  // first: a fresh wave's loads go out before the older waves' arithmetic
   const int w = a.width, h = a.height, nfr = (int)mdiv(nmbs, kd.mn, kd.sn);
@@ -1083,10 +1049,10 @@ hipError_t intra_mbg(const p64gpu_encode_args &a, hipStream_t st) {
 hipError_t inter_mbg(const p64gpu_encode_args &a, const p64_me_rec *me, hipStream_t st) {
   const unsigned nm = (unsigned)((int64_t)a.nframes * (a.width / 16) * (a.height / 16));
   if (a.quant_mb)
-    hipLaunchKernelGGL(k_inter_mbg<true>, dim3(mbg_workgroups(nm, INTER_WAVES)), dim3(64 * INTER_WAVES), 0, st, a,
+    hipLaunchKernelGGL(k_inter_mbg<true>, dim3(mbg_workgroups(nm, 1)), dim3(64), 0, st, a,
                        blk_div(a.width, a.height), nm, me);
   else
-    hipLaunchKernelGGL(k_inter_mbg<false>, dim3(mbg_workgroups(nm, INTER_WAVES)), dim3(64 * INTER_WAVES), 0, st, a,
+    hipLaunchKernelGGL(k_inter_mbg<false>, dim3(mbg_workgroups(nm, 1)), dim3(64), 0, st, a,
                        blk_div(a.width, a.height), nm, me);
   return hipGetLastError();
 }
@@ -1095,7 +1061,7 @@ hipError_t recon_mbg(int w, int h, int nframes, int64_t stride, const uint8_t *r
                      const int16_t *coef, const p64_mb_rec *mb, const uint8_t *quant_mb,
                      const uint8_t *coded_mask, hipStream_t st) {
   const unsigned nm = (unsigned)((int64_t)nframes * (w / 16) * (h / 16));
-  hipLaunchKernelGGL(k_recon_mbg, dim3(mbg_workgroups(nm, REC_WAVES)), dim3(64 * REC_WAVES), 0, st, w, h, stride, ref, recon,
+  hipLaunchKernelGGL(k_recon_mbg, dim3(mbg_workgroups(nm, 1)), dim3(64), 0, st, w, h, stride, ref, recon,
                      coef, mb, quant_mb, coded_mask, blk_div(w, h), nm);
   return hipGetLastError();
 }

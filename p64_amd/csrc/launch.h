@@ -28,10 +28,15 @@ hipError_t recon_mbg(int w, int h, int nframes, int64_t stride, const uint8_t *r
                      const int16_t *coef, const p64_mb_rec *mb, const uint8_t *quant_mb,
                      const uint8_t *coded_mask, hipStream_t st);
 
-// k_aux.hip -- reference block routines one thread per block; synthetic input
+// k_aux.hip -- reference block routines one thread per block; synthetic input;
+// the clock probe
 hipError_t block_op(int op, const int32_t *in, int32_t *out, int64_t nblocks, int dcq, int acq,
                     hipStream_t st);
 hipError_t synth(int w, int h, uint32_t seed0, int nseeds, int frame0, int nslots, int64_t stride,
                  uint8_t *out, hipStream_t st);
+// clock probe: clock_waves() waves (8 per SIMD), each spinning `ticks` of the
+// 100 MHz counter; out [clock_waves()][2] = (shader ticks, real-time ticks)
+unsigned clock_waves();
+hipError_t clock(uint32_t ticks, uint32_t *out, hipStream_t st);
 
 }  // namespace p64k

@@ -6,12 +6,14 @@
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdarg>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
+#include <thread>
 #include <vector>
 
 #include "../../include/p64gpu.h"
@@ -70,18 +72,26 @@ bool fused_forced() {
 }
 
 // Device scratch for the ME records of the split inter encoder when the
-// caller does not ask for them (args.me == NULL): one buffer per (device,
-// stream), so encodes on different streams never share records, and work on
-// one stream is ordered by the stream itself.  A buffer that is outgrown is
-// retired, not freed: a HIP graph captured earlier (or work still in flight)
-// may reference it; p64gpu_release_scratch() frees everything when the
-// caller knows no such work or graph remains.  No device synchronisation
-// here, so another thread's capture is never disturbed.  During a capture
-// that would need a larger buffer the allocation is not attempted (NULL: the
-// caller takes the fused kernel, which needs no scratch).
+// caller does not ask for them (args.me == NULL).
+//  * One buffer per (device, stream), and per calling thread for
+//    hipStreamPerThread (a sentinel that stands for each thread's own stream).
+//  * The lock is held from the lookup until both kernels of the call are
+//    enqueued, so calls from several threads on one shared stream (the NULL
+//    stream, say) cannot interleave their k_motion / k_inter_mbg pairs: the
+//    stream then orders them pair by pair.
+//  * Never during stream capture: a captured graph would keep the buffer's
+//    pointer and could race an eager call (or another graph replayed on
+//    another stream) that uses it.  A capturing caller gets NULL and the
+//    call takes the fused kernel, which needs no scratch.
+//  * A buffer that is outgrown is retired, not freed (work still in flight
+//    may reference it); p64gpu_release_scratch() frees everything when the
+//    caller knows no such work remains.  The allocation runs in relaxed
+//    capture mode, so it cannot invalidate another thread's global-mode
+//    capture.
 struct MeScratch {
   int dev;
   hipStream_t st;
+  std::thread::id tid;
   p64_me_rec *buf;
   size_t cap;
 };
@@ -89,20 +99,29 @@ std::mutex g_scr_mu;
 std::vector<MeScratch> g_scr;
 std::vector<void *> g_retired;
 
-p64_me_rec *me_scratch(size_t n, hipStream_t st) {
-  int dev = -1;
-  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
-  std::lock_guard<std::mutex> lk(g_scr_mu);
-  MeScratch *e = nullptr;
-  for (auto &s : g_scr)
-    if (s.dev == dev && s.st == st) e = &s;
-  if (e && n <= e->cap) return e->buf;
+// returns the buffer with `lk` holding g_scr_mu, or NULL (lock not held)
+p64_me_rec *me_scratch(size_t n, hipStream_t st, std::unique_lock<std::mutex> &lk) {
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
   if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
+  int dev = -1;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  const std::thread::id tid = st == hipStreamPerThread ? std::this_thread::get_id() : std::thread::id();
+  lk = std::unique_lock<std::mutex>(g_scr_mu);
+  MeScratch *e = nullptr;
+  for (auto &s : g_scr)
+    if (s.dev == dev && s.st == st && s.tid == tid) e = &s;
+  if (e && n <= e->cap) return e->buf;
   void *p = nullptr;
-  if (hipMalloc(&p, n * sizeof(p64_me_rec)) != hipSuccess) return nullptr;
+  hipStreamCaptureMode mode = hipStreamCaptureModeRelaxed;
+  (void)hipThreadExchangeStreamCaptureMode(&mode);
+  const hipError_t me = hipMalloc(&p, n * sizeof(p64_me_rec));
+  (void)hipThreadExchangeStreamCaptureMode(&mode);
+  if (me != hipSuccess) {
+    lk.unlock();
+    return nullptr;
+  }
   if (!e) {
-    g_scr.push_back(MeScratch{dev, st, nullptr, 0});
+    g_scr.push_back(MeScratch{dev, st, tid, nullptr, 0});
     e = &g_scr.back();
   }
   if (e->buf) g_retired.push_back(e->buf);
@@ -169,7 +188,8 @@ int encode_launch(const p64gpu_encode_args *a, const int32_t *mb_list, int count
     const int nmb = (a->width / 16) * (a->height / 16);
     // inter: ME for the whole batch into the caller's records or the scratch
     p64_me_rec *me = nullptr;
-    if (!a->intra) me = a->me ? a->me : me_scratch((size_t)a->nframes * nmb, st);
+    std::unique_lock<std::mutex> lk;  // held while the scratch is in use (me_scratch)
+    if (!a->intra) me = a->me ? a->me : me_scratch((size_t)a->nframes * nmb, st, lk);
     if (a->intra || me) {
       if (!a->intra)
         HIP_TRY(p64k::motion(mode, a->width, a->height, a->nframes, a->frame_stride, a->ref, a->cur,
@@ -357,6 +377,29 @@ int p64gpu_synth_frames(int w, int h, uint32_t seed0, int nseeds, int frame0, in
     return fail(P64GPU_E_INVALID, "synth: out=%p nseeds=%d nslots=%d frame0=%d", (void *)out,
                 nseeds, nslots, frame0);
   HIP_TRY(p64k::synth(w, h, seed0, nseeds, frame0, nslots, stride, out, (hipStream_t)stream));
+  return P64GPU_OK;
+}
+
+int p64gpu_clock_probe(int microseconds, int *mhz, void *stream) {
+  if (!mhz || microseconds < 1 || microseconds > 10000000)
+    return fail(P64GPU_E_INVALID, "clock probe: mhz=%p microseconds=%d", (void *)mhz, microseconds);
+  *mhz = 0;
+  hipStream_t st = (hipStream_t)stream;
+  const unsigned n = p64k::clock_waves();
+  uint32_t *d = nullptr;
+  HIP_TRY(hipMalloc(&d, (size_t)n * 2 * sizeof(uint32_t)));
+  std::vector<uint32_t> h((size_t)n * 2);
+  hipError_t e = p64k::clock((uint32_t)microseconds * 100u, d, st);  // 100 ticks per us
+  if (e == hipSuccess) e = hipMemcpyAsync(h.data(), d, h.size() * sizeof(uint32_t), hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  (void)hipFree(d);
+  if (e != hipSuccess) return fail(P64GPU_E_HIP, "clock probe: %s", hipGetErrorString(e));
+  std::vector<double> f;
+  for (unsigned i = 0; i < n; i++)
+    if (h[2 * i + 1]) f.push_back(100.0 * h[2 * i] / h[2 * i + 1]);
+  if (f.empty()) return fail(P64GPU_E_HIP, "clock probe: no samples");
+  std::nth_element(f.begin(), f.begin() + f.size() / 2, f.end());
+  *mhz = (int)(f[f.size() / 2] + 0.5);
   return P64GPU_OK;
 }
 

@@ -18,7 +18,7 @@
 #include "../../include/p64gpu.h"
 #include "../../include/p64prog.h"
 
-int p64gpu_fail_(int status, const char *msg); /* p64gpu.hip: sets last error */
+int p64gpu_fail_(int status, const char *msg); /* p64gpu_abi.hip: sets last error */
 
 /* reserved words, lexer.l:27-79, in token order 1..52 */
 static const char *const WORDS[] = {

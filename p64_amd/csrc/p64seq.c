@@ -15,7 +15,7 @@
 #include "../../include/p64prog.h"
 #include "../../include/p64seq.h"
 
-int p64gpu_fail_(int status, const char *msg); /* p64gpu.hip: sets last error */
+int p64gpu_fail_(int status, const char *msg); /* p64gpu_abi.hip: sets last error */
 
 static int fail(int status, const char *fmt, ...) __attribute__((format(printf, 2, 3)));
 static int fail(int status, const char *fmt, ...) {

@@ -1,6 +1,6 @@
 /*
  * synth_impl.h -- per-pixel body of the deterministic synthetic video source.
- * Included by synth.c (host, gcc) and p64gpu.hip (device generator); the
+ * Included by synth.c (host, gcc) and k_aux.hip (device generator); the
  * includer defines SYNTH_FN (`static inline` or `__host__ __device__ static
  * inline`).  Integer arithmetic only, so every includer produces the same bytes.
  */

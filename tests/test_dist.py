@@ -162,6 +162,39 @@ def test_bench_launcher_spawns_ranks():
     assert d["seed_ranges"] == [[1, 8], [9, 16]]
     assert d["elapsed_max_s"] >= 20 * 0.002  # rank 1's 2 ms steps bound the MAX
     assert abs(d["value"] - 2 * 8 * 396 * 20 / d["elapsed_max_s"]) < 1e-6 * d["value"]
+    # who ran it: the process group's size and one entry per rank (device
+    # fields null without a device; on a GPU node each rank's PCI bus id)
+    rk = d["ranks"]
+    assert rk["world_size"] == 2 and rk["backend"] == "gloo"
+    assert [r["rank"] for r in rk["ranks"]] == [0, 1]
+    assert [r["local_rank"] for r in rk["ranks"]] == [0, 1]
+    assert all(set(r) == {"rank", "local_rank", "host", "pci_bus_id", "device"} for r in rk["ranks"])
+
+
+def test_bench_n1_launcher_line_shape_matches_plain():
+    """The N=1 line under torch.distributed.run (WORLD_SIZE=1 from the
+    launcher) has exactly the keys, and ranks block, of a plain N=1 run."""
+    import subprocess
+    import sys
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    args = ["--dry", "--gpus", "1", "--steps", "3", "--streams", "4"]
+    plain = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), *args],
+                           capture_output=True, text=True, timeout=120, env=env)
+    assert plain.returncode == 0, plain.stderr[-2000:]
+    launched = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                               "--nproc-per-node=1", "--master-addr=127.0.0.1",
+                               f"--master-port={free_port()}", os.path.join(REPO, "bench.py"), *args],
+                              capture_output=True, text=True, timeout=240, env=env)
+    assert launched.returncode == 0, launched.stderr[-2000:]
+    a, b = _bench_json(plain.stdout), _bench_json(launched.stdout)
+    assert set(a) == set(b)
+    assert set(a["config"]) == set(b["config"])
+    for d in (a, b):
+        assert d["n_gpus"] == 1 and d["ranks"]["world_size"] == 1
+        assert len(d["ranks"]["ranks"]) == 1 and d["ranks"]["distinct_devices"] == 1
+        for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+                  "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config"):
+            assert k in d
 
 
 def test_bench_refuses_world_mismatch():

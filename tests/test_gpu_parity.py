@@ -362,9 +362,10 @@ def _raw_encode(p64, torch, cur, ref, recon, li, coef, mb, *, w, h, stream, me=N
 def test_library_me_scratch_per_stream_and_graph_safe(p64, torch_dev):
     """Inter encodes without an ME-record output (args.me == NULL) keep their
     records in a library scratch private to the calling stream: two batches
-    encoded concurrently on two streams give their own results, and a graph
-    captured before the scratch grows still replays correctly afterwards (the
-    outgrown buffer is retired, not freed).  ADVICE r02 (high)."""
+    encoded concurrently on two streams give their own results; a graph
+    captured on a stream with a scratch takes the fused kernel (a graph never
+    points at library scratch) and replays the same results after the
+    scratch has grown.  ADVICE r02 (high), r03 (medium)."""
     torch = torch_dev
     w, h = 352, 288
     nmb, pic = (w // 16) * (h // 16), w * h * 3 // 2
@@ -441,6 +442,79 @@ def test_library_me_scratch_per_stream_and_graph_safe(p64, torch_dev):
         np.testing.assert_array_equal(got, want)
     del g
     torch.cuda.synchronize()
+    assert p64.lib().p64gpu_release_scratch() == 0
+
+
+def test_library_me_scratch_per_thread_stream(p64, torch_dev):
+    """hipStreamPerThread stands for each calling thread's own stream: two
+    threads encoding without an ME-record output on it, at the same time,
+    get scratch buffers of their own and their own results; and so do two
+    threads sharing the NULL stream (the library holds its lock until both
+    kernels of a call are enqueued).  ADVICE r03 (medium)."""
+    import threading
+    torch = torch_dev
+    w, h, S = 352, 288, 4
+    nmb, pic = (w // 16) * (h // 16), w * h * 3 // 2
+
+    class Raw:  # a raw stream handle for _raw_encode
+        def __init__(self, v):
+            self.cuda_stream = v
+
+    jobs = []
+    for seed in (303, 404):
+        f = [dev(torch, np.stack([p64.synth_frame(seed + s, t, w, h) for s in range(S)])).reshape(-1)
+             for t in range(2)]
+        li = torch.zeros(S * nmb, dtype=torch.uint8, device="cuda")
+        r0 = torch.zeros(S * pic, dtype=torch.uint8, device="cuda")
+        p64.encode_frames(f[0], None, r0, li, width=w, height=h, intra=True, quant=8)
+        jobs.append((f[1], r0, li))
+    torch.cuda.synchronize()
+
+    def outputs():
+        return (torch.empty(S * pic, dtype=torch.uint8, device="cuda"),
+                torch.zeros(S * nmb, dtype=torch.uint8, device="cuda"),
+                torch.empty((S, nmb, 6, 64), dtype=torch.int16, device="cuda"),
+                torch.empty((S, nmb, 4), dtype=torch.int8, device="cuda"))
+
+    want = []
+    for cur, ref, li in jobs:
+        o = outputs()
+        o[1].copy_(li)
+        me = torch.empty((S, nmb, 7), dtype=torch.int32, device="cuda")
+        _raw_encode(p64, torch, cur, ref, o[0], o[1], o[2], o[3], w=w, h=h,
+                    stream=torch.cuda.current_stream(), me=me)
+        torch.cuda.synchronize()
+        want.append(tuple(host(x) for x in (o[0], o[2], o[3])))
+
+    for handle in (2, 0):  # hipStreamPerThread, the NULL stream
+        outs = [outputs() for _ in jobs]
+        for (cur, ref, li), o in zip(jobs, outs):
+            o[1].copy_(li)
+        torch.cuda.synchronize()
+        errs = []
+
+        def work(i):
+            try:
+                cur, ref, li = jobs[i]
+                o = outs[i]
+                for _ in range(4):  # the same picture again: same results every time
+                    _raw_encode(p64, torch, cur, ref, o[0], o[1], o[2], o[3], w=w, h=h,
+                                stream=Raw(handle))
+                    torch.cuda.synchronize()
+                    o[1].copy_(li)  # LastIntra back for the next round
+                    torch.cuda.synchronize()
+            except Exception as e:  # noqa: BLE001
+                errs.append(e)
+        ts = [threading.Thread(target=work, args=(i,)) for i in range(len(jobs))]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+        torch.cuda.synchronize()
+        assert not errs, errs
+        for o, e in zip(outs, want):
+            for got, exp in zip((host(o[0]), host(o[2]), host(o[3])), e):
+                np.testing.assert_array_equal(got, exp, err_msg=f"stream handle {handle}")
     assert p64.lib().p64gpu_release_scratch() == 0
 
 

@@ -1,4 +1,4 @@
-"""The fused kernels divide by 2q with a binary32 reciprocal (p64gpu.hip
+"""The fused kernels divide by 2q with a binary32 reciprocal (common.h
 c_qrecip: 1/(2q) rounded to float, then raised one ulp, so that exact
 multiples never fall short).  Check it exhaustively against C truncating
 division for every step the encoder can use (q = 1..31) and every value the

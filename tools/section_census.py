@@ -1,7 +1,8 @@
 """Instruction census per SECTION() phase of one kernel (development aid).
 
-Compiles p64gpu.hip with -DP64_SECTIONS to an ISA listing and counts VALU /
-SALU / LDS instructions between the ";## name" markers.  Static counts: loop
+Compiles a copy of k_search.hip whose SECTION() labels (no code in the
+product) become ";## name" asm markers to an ISA listing and counts VALU /
+SALU / LDS instructions between the markers.  Static counts: loop
 bodies count once, both sides of a branch count.
 usage: python tools/section_census.py [kernel-substring] [extra hipcc flags...]
 """
@@ -13,9 +14,15 @@ import sys
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 kern = sys.argv[1] if len(sys.argv) > 1 else "k_motionILi2"
 out = "/tmp/p64_sections.s"
-subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-DP64_SECTIONS",
-                *sys.argv[2:], "-S", "--cuda-device-only", "-o", out,
-                os.path.join(REPO, "p64_amd/csrc/k_search.hip")], check=True)
+src = open(os.path.join(REPO, "p64_amd/csrc/k_search.hip")).read().replace(
+    '#include "launch.h"\n', '#include "launch.h"\n#undef SECTION\n#define SECTION(name) asm volatile(";## " name)\n', 1)
+tmp = os.path.join(REPO, "p64_amd/csrc/_census_tmp.hip")
+open(tmp, "w").write(src)
+try:
+    subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17",
+                    *sys.argv[2:], "-S", "--cuda-device-only", "-o", out, tmp], check=True)
+finally:
+    os.remove(tmp)
 s = open(out).read()
 start = next(i for i in range(len(s)) if s.startswith("_Z", i) and kern in s[i:s.find(":", i)]
              and s[s.find(":", i) + 1:s.find(":", i) + 4].strip().startswith(";"))
