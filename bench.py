@@ -79,8 +79,12 @@ SAD_PEAK = 256 * 4 * 16 * 4 * 2.4e9
 BYTES_PER_MB = 384 + 384 + 1 + 768 + 384 + 4 + 28 + 1
 READ_BYTES_PER_MB = 384 + 384 + 1
 INTRA_BYTES_PER_MB = 384 + 768 + 384 + 4 + 1
-# rocprofv3 --kernel-trace --stats summary of the default bench command (this round)
-PROFILE_STATS = "profiles/r03_kernel_stats.csv"
+# per-kernel means over the timed region of the driver's command (rocprofv3
+# --kernel-trace of `bench.py --steps 20 --warmup 5 --no-cpu`, reduced by
+# tools/timed_region.py --json; the spin-up's replays are outside the region)
+PROFILE_TIMED = "profiles/r04_timed_region.json"
+# executed v_sad_u8 work of k_motion per launch (tools/sad_count.py side build)
+PROFILE_SAD = "profiles/sad_executed.json"
 MAX_SLOTS = 256  # distinct input pictures per sequence kept resident (~10 GB at S=256 CIF)
 
 
@@ -479,15 +483,19 @@ def timed_region(torch, dist, world, steps, t_first, launch, pre=None, post=None
     Steady state: the chip raises its clocks over tens of ms of load and drops
     them when idle (the capture and the verification snapshot before the
     region leave it idle for ~12 ms); a 20-step region (3.6 ms) measured from
-    there ran 10% slower than the same kernels after ~20 ms of load
-    (profiles/r04_clock.txt).  So, when spin = (init, launch_s) is given,
-    init() copies the closed-loop state into scratch buffers and launch_s(t)
-    issues step t exactly as launch(t) does but into those scratch buffers
-    (same inputs, outputs discarded); the K scratch launches are replayed
-    back to back for >= spinup_ms, and the timed region follows at once.
-    Nothing the timed steps read is produced by the spin-up, and no work is
-    dropped from them.  A 50-us clock probe after the region reads the clock
-    the chip was left at (box-to-box spread).
+    there ran 12% slower than the same kernels after ~25 ms of load
+    (profiles/r04a_clock_sweep.txt).  So, when spin is given (dict: init()
+    allocates scratch outputs, reset() copies the closed-loop state into
+    scratch, launch(t) issues step t exactly as launch does but into the
+    scratch), [reset + the K scratch steps] is replayed back to back for >=
+    spinup_ms -- every replay the same work as the timed one, outputs
+    discarded -- and the timed region follows.  Nothing the timed steps read
+    is produced by the spin-up, and no work is dropped from them.
+    spin["split"](t), if given, returns the step as its separate launches
+    [(kernel name, fn)]: one more reset + eager pass times each with HIP
+    events (the live per-kernel split of the step, e.g. k_motion alone).
+    A 50-us clock probe after the region reads the clock the chip was left
+    at (box-to-box spread).
     Returns (wall seconds of the timed region, mean kernel seconds per step,
     steady-state record)."""
     import p64_amd
@@ -495,10 +503,12 @@ def timed_region(torch, dist, world, steps, t_first, launch, pre=None, post=None
         graph = False
     st = {"spinup_ms": spinup_ms if spin else 0, "spinup_replays": 0}
 
-    def capture(fn):
+    def capture(fn, first=None):
         torch.cuda.synchronize()
         gr = torch.cuda.CUDAGraph()
         with torch.cuda.graph(gr):
+            if first is not None:
+                first()
             for k in range(steps):
                 fn(t_first + k)
         torch.cuda.synchronize()
@@ -506,10 +516,16 @@ def timed_region(torch, dist, world, steps, t_first, launch, pre=None, post=None
 
     g = capture(launch) if graph else None
     if spin is not None and spinup_ms > 0:
-        init, launch_s = spin
-        init()
-        gs = capture(launch_s) if graph else None
-        run = gs.replay if graph else (lambda: [launch_s(t_first + k) for k in range(steps)])
+        spin["init"]()
+        gs = capture(spin["launch"], spin["reset"]) if graph else None
+
+        def run():
+            if graph:
+                gs.replay()
+            else:
+                spin["reset"]()
+                for k in range(steps):
+                    spin["launch"](t_first + k)
         t0 = time.perf_counter()
         run()
         torch.cuda.synchronize()
@@ -517,8 +533,25 @@ def timed_region(torch, dist, world, steps, t_first, launch, pre=None, post=None
         n = max(0, int(spinup_ms * 1e-3 / max(one, 1e-6) + 0.999) - 1)
         for _ in range(n):  # back to back, no host synchronisation between them
             run()
+        torch.cuda.synchronize()
         st["spinup_replays"] = 1 + n
         st["spinup_ms_actual"] = round((time.perf_counter() - t0) * 1e3, 1)
+        if spin.get("split"):  # the split again, now at steady clocks
+            spin["reset"]()
+            evs = {}
+            for k in range(steps):
+                for nm, fn in spin["split"](t_first + k):
+                    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    a.record()
+                    fn()
+                    b.record()
+                    evs.setdefault(nm, []).append((a, b))
+            torch.cuda.synchronize()
+            st["kernels_us_live"] = {nm: round(sum(a.elapsed_time(b) for a, b in v) * 1e3 / len(v), 2)
+                                     for nm, v in evs.items()}
+            st["kernels_us_live_note"] = ("each kernel of the step launched on its own (eager, HIP events "
+                                          "around each launch), same steps and state as the timed region, "
+                                          "right after the spin-up")
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
           for _ in range(1 if graph else steps)]
     torch.cuda.synchronize()
@@ -657,18 +690,31 @@ def main(argv=None):
                 post(t)
 
         # steady-state spin-up (timed_region): the same launches into scratch
+        kme, kin = "k_motion<%d>" % (2 if args.mode == "full" else 1), "k_inter_mbg<false>"
         sp = {}
 
         def spin_init():
-            sp["rec"] = [r.clone() for r in rec]
-            sp["li"] = li.clone()
+            sp["rec"] = [torch.empty_like(r) for r in rec]
+            sp["li"] = torch.empty_like(li)
             sp["out"] = p64_amd.FrameBatchOut(coef=torch.empty_like(coef_all[0]),
                                               mb=torch.empty_like(mb_all[0]), me=torch.empty_like(me))
 
-        def spin_launch(t):
+        def spin_reset():
+            for a, b in zip(sp["rec"], rec):
+                a.copy_(b)
+            sp["li"].copy_(li)
+
+        def spin_launch(t, me_given=False):
             p64_amd.encode_frames(frames[slot(t)].reshape(-1), sp["rec"][(t + 1) % 2], sp["rec"][t % 2],
                                   sp["li"], width=w, height=h, intra=False, quant=args.quant,
-                                  me_mode=mode, search_limit=args.search_limit, out=sp["out"])
+                                  me_mode=mode, search_limit=args.search_limit, out=sp["out"],
+                                  me_given=me_given)
+
+        def spin_split(t):  # the step as its two kernels: the search, then the rest
+            return [(kme, lambda: p64_amd.MotionEstimation(
+                        sp["rec"][t % 2], frames[slot(t)].reshape(-1), w, h, mode=mode,
+                        search_limit=args.search_limit, out=sp["out"].me)),
+                    (kin, lambda: spin_launch(t, me_given=True))]
 
         for t in range(1 + args.warmup):  # intra picture + warmup, untimed
             step(t)
@@ -683,7 +729,8 @@ def main(argv=None):
         elapsed, kavg, clk = timed_region(torch, dist, world, args.steps, t_first, launch,
                                           pre if root else None, post if root else None,
                                           graph=not args.eager, spinup_ms=args.spinup_ms,
-                                          spin=(spin_init, spin_launch))
+                                          spin={"init": spin_init, "reset": spin_reset,
+                                                "launch": spin_launch, "split": spin_split})
         sp.clear()
         tmax = max_over_ranks(elapsed, world, device="cuda")
         last = t_first + args.steps - 1
@@ -743,18 +790,19 @@ def main(argv=None):
         key = f"{w}x{h}_{args.mode}{args.search_limit}_q{args.quant}_S{S}" + \
             ("" if args.content == "synth" else f"_{args.content}")
         pmc = load_pmc(args.pmc_json, key)
-        kme, kin = "k_motion<%d>" % (2 if args.mode == "full" else 1), "k_inter_mbg<false>"
         pmc_me, pmc_in = load_pmc(args.pmc_json, key + "_me"), load_pmc(args.pmc_json, key + "_inter")
         if os.environ.get("P64GPU_FUSED", "0") in ("", "0"):  # split: k_motion, k_inter_mbg
             kernel = f"{kme} + {kin} (one step)"
-            prof = os.path.join(REPO, PROFILE_STATS)
+            prof = load_json(os.path.join(REPO, PROFILE_TIMED)) or {}
             split = {"dominant": kme,
-                     "dominant_note": "k_motion is VALU-bound (roofline_sad, valu_busy); the HBM "
-                                      "roofline is taken over the whole step, both kernels",
-                     "kernels_us_rocprof": rocprof_avg_us(prof, (kme, kin)) if key.endswith(
-                         "S256") else None,
-                     "kernels_us_source": f"{PROFILE_STATS} (rocprofv3 --kernel-trace "
-                                          "--stats of this default bench command)"}
+                     "dominant_note": "k_motion is VALU-bound (roofline_sad_executed, valu_busy); the "
+                                      "HBM roofline is taken over the whole step, both kernels",
+                     "kernels_us_live": clk.get("kernels_us_live"),
+                     "kernels_us_rocprof": ({k: prof[k] for k in (kme, kin)} if key.endswith("S256") and
+                                            all(k in prof for k in (kme, kin)) else None),
+                     "kernels_us_rocprof_source": f"{PROFILE_TIMED} (rocprofv3 --kernel-trace of "
+                                                  "`bench.py --steps 20 --warmup 5 --no-cpu`, timed "
+                                                  "region only: tools/timed_region.py)"}
             pmc = None  # (an entry under `key` would be the fused kernel's)
             if pmc_me and pmc_in:
                 pmc = {"hbm_bytes_per_launch": pmc_me["hbm_bytes_per_launch"] +
@@ -786,13 +834,14 @@ def main(argv=None):
                 "note": "the north_star's HBM-read roofline: the bytes a step must read (current "
                         "picture 384 + previous reconstruction 384 + LastIntra 1 per MB) over the "
                         "step time"},
-            "roofline_sad": {"bound": "valu", "achieved": round(sad_rate / 1e12, 3),
-                             "peak": round(SAD_PEAK / 1e12, 3), "unit": "T byte-absdiff/s",
-                             "frac": round(sad_rate / SAD_PEAK, 4), "candidates_per_mb": cand,
-                             "note": "exhaustive-search equivalent: candidates x 256 "
-                                     "byte-absdiffs per MB; the FULL kernel executes far fewer "
-                                     "(exact pruning by a 4x4-average lower bound, DESIGN.md "
-                                     "section 5); executed VALU work: valu_busy"},
+            "roofline_sad_exhaustive_equivalent": {
+                "bound": "valu", "achieved": round(sad_rate / 1e12, 3),
+                "peak": round(SAD_PEAK / 1e12, 3), "unit": "T byte-absdiff/s",
+                "frac": round(sad_rate / SAD_PEAK, 4), "candidates_per_mb": cand,
+                "note": "NOT a utilisation: the exhaustive search's candidates x 256 byte-absdiffs "
+                        "per MB over the whole step time; the FULL kernel executes far fewer "
+                        "(exact pruning, DESIGN.md 5): see roofline_sad_executed"},
+            "roofline_sad_executed": sad_executed(args, key, kme, clk, mbs_launch),
             "valu_busy": (pmc or {}).get("valu_busy"),
             "steady_state": clk,
             "with_vlc": with_vlc,
@@ -829,25 +878,42 @@ def main(argv=None):
     print(json.dumps(line), flush=True)
 
 
+def load_json(path):
+    try:
+        with open(path) as f:
+            return json.load(f)
+    except (OSError, ValueError):
+        return None
+
+
+def sad_executed(args, key, kme, clk, mbs):
+    """k_motion's executed v_sad_u8 work against the instruction's peak: the
+    byte-absolute-differences one launch executes on this workload (counted
+    side build, profiles/sad_executed.json) over k_motion's own launch time
+    (live: kernels_us_live, each kernel timed alone right after the spin-up;
+    else the committed rocprof timed-region mean)."""
+    cnt = (load_json(os.path.join(REPO, PROFILE_SAD)) or {}).get(key)
+    us = (clk.get("kernels_us_live") or {}).get(kme)
+    src = "live"
+    if us is None:
+        us = (load_json(os.path.join(REPO, PROFILE_TIMED)) or {}).get(kme)
+        src = PROFILE_TIMED
+    if not cnt or not us or args.mode != "full":
+        return None
+    per_launch = cnt["byte_absdiff_per_mb"] * mbs
+    rate = per_launch / (us * 1e-6)
+    return {"bound": "valu", "kernel": kme, "achieved": round(rate / 1e12, 3),
+            "peak": round(SAD_PEAK / 1e12, 3), "unit": "T byte-absdiff/s", "frac": round(rate / SAD_PEAK, 4),
+            "executed_byte_absdiff_per_mb": round(cnt["byte_absdiff_per_mb"], 1),
+            "kernel_us": us, "kernel_us_source": src,
+            "note": "executed v_sad_u8 lane-instructions x 4 (counted by tools/sad_count.py on this "
+                    "workload, profiles/sad_executed.json) over k_motion's launch time; the rest of "
+                    "k_motion's issue is the bound map, addressing and reductions (valu_busy)"}
+
+
 def strip(r):
     """A nested config line: everything but the top-level contract keys."""
     return {k: v for k, v in r.items() if k not in ("with_vlc",)}
-
-
-def rocprof_avg_us(path, names):
-    """Average launch duration (us) of the named kernels in a committed
-    rocprofv3 --kernel-trace --stats summary (profiles/), or None."""
-    try:
-        import csv
-        out = {}
-        with open(path) as f:
-            for r in csv.DictReader(f):
-                n = r["Name"].replace("(anonymous namespace)::", "").replace("void ", "").split("(")[0]
-                if n in names:
-                    out[n] = round(float(r["AverageNs"]) / 1e3, 2)
-        return out if len(out) == len(names) else None
-    except (OSError, KeyError, ValueError):
-        return None
 
 
 def measure_vlc(args, torch, p64_amd, step, out_of, S, nmb, w, h):
@@ -900,8 +966,11 @@ def run_intra(args, torch, dist, np, p64_amd, world, frames, S, nmb, pic, nslots
     sp = {}
 
     def spin_init():
-        sp["rec"], sp["li"] = torch.empty_like(rec), li.clone()
+        sp["rec"], sp["li"] = torch.empty_like(rec), torch.empty_like(li)
         sp["out"] = p64_amd.FrameBatchOut(coef=torch.empty_like(out.coef), mb=torch.empty_like(out.mb), me=None)
+
+    def spin_reset():
+        sp["li"].copy_(li)
 
     def spin_step(t):
         p64_amd.encode_frames(frames[t % nslots].reshape(-1), None, sp["rec"], sp["li"], width=w, height=h,
@@ -911,7 +980,7 @@ def run_intra(args, torch, dist, np, p64_amd, world, frames, S, nmb, pic, nslots
         step(t)
     elapsed, kavg, clk = timed_region(torch, dist, world, args.steps, args.warmup, step,
                                       graph=not args.eager, spinup_ms=args.spinup_ms,
-                                      spin=(spin_init, spin_step))
+                                      spin={"init": spin_init, "reset": spin_reset, "launch": spin_step})
     sp.clear()
     tmax = max_over_ranks(elapsed, world, device="cuda")
     last = args.warmup + args.steps - 1
@@ -987,14 +1056,19 @@ def run_decode(args, torch, dist, np, p64_amd, world, enc, S, nmb, pic):
     sp = {}
 
     def spin_init():
-        sp["dec"] = [d.clone() for d in dec]
+        sp["dec"] = [torch.empty_like(d) for d in dec]
+
+    def spin_reset():
+        for a, b in zip(sp["dec"], dec):
+            a.copy_(b)
 
     def spin_step(t):
         p64_amd.decode_recon(sp["dec"][(t + 1) % 2], sp["dec"][t % 2], enc["coef"][t], enc["mb"][t], qmb,
                              mask, width=w, height=h)
 
     elapsed, kavg, clk = timed_region(torch, dist, world, args.steps, first, step, graph=not args.eager,
-                                      spinup_ms=args.spinup_ms, spin=(spin_init, spin_step))
+                                      spinup_ms=args.spinup_ms,
+                                      spin={"init": spin_init, "reset": spin_reset, "launch": spin_step})
     sp.clear()
     tmax = max_over_ranks(elapsed, world, device="cuda")
     ok = bool(torch.equal(dec[last % 2], enc["recon_last"]))

@@ -134,6 +134,13 @@ int p64gpu_motion_estimation(int width, int height, int nframes,
                              p64_me_rec *out, void *stream);
 
 /* ---- the fused per-macroblock encode (device pointers) ------------------ */
+/* flags: P64GPU_FLAG_ME_GIVEN -- inter pictures only: args->me already holds
+ * this batch's ME records (p64gpu_motion_estimation over the same ref/cur
+ * luma, mode and search limit), so the search is not run again; the rest of
+ * the encode reads them.  The reference's own order: MotionEstimation() for
+ * the picture first (p64.c:652, me.c:340), then the MDU loop reads MeVAR,
+ * MeVAROR, MeX/MeY... (p64.c:734-756). */
+enum { P64GPU_FLAG_ME_GIVEN = 1 };
 typedef struct {
   int32_t width, height;  /* picture size, multiples of 16, 32..4096         */
   int32_t nframes;        /* independent pictures in this launch (>= 1)      */
@@ -142,7 +149,7 @@ typedef struct {
   int32_t quant;          /* GQuant 1..31 (UseQuant without -r)              */
   int32_t me_mode;        /* P64GPU_ME_TSS | P64GPU_ME_FULL                  */
   int32_t search_limit;   /* FULL: 1..31 (SearchLimit, me.c:62, -i flag)     */
-  int32_t reserved;       /* must be 0                                       */
+  int32_t flags;          /* 0 or P64GPU_FLAG_ME_GIVEN                       */
   int64_t frame_stride;   /* bytes between pictures in cur/ref/recon        */
   const uint8_t *cur;     /* [nframes] current pictures                       */
   const uint8_t *ref;     /* [nframes] previous reconstructions (CFS);

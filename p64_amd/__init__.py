@@ -68,7 +68,7 @@ class EncodeArgs(ctypes.Structure):
     _fields_ = [
         ("width", ctypes.c_int32), ("height", ctypes.c_int32), ("nframes", ctypes.c_int32),
         ("intra", ctypes.c_int32), ("quant", ctypes.c_int32), ("me_mode", ctypes.c_int32),
-        ("search_limit", ctypes.c_int32), ("reserved", ctypes.c_int32),
+        ("search_limit", ctypes.c_int32), ("flags", ctypes.c_int32),
         ("frame_stride", ctypes.c_int64),
         ("cur", ctypes.c_void_p), ("ref", ctypes.c_void_p), ("recon", ctypes.c_void_p),
         ("last_intra", ctypes.c_void_p), ("quant_mb", ctypes.c_void_p),
@@ -78,6 +78,7 @@ class EncodeArgs(ctypes.Structure):
 
 
 # numpy views of the record arrays (field order matches include/p64gpu.h)
+P64GPU_FLAG_ME_GIVEN = 1  # include/p64gpu.h
 ME_DTYPE = np.dtype([(n, "<i4") for n in ("mx", "my", "sad", "sad0", "var", "varor", "mwor")])
 MB_DTYPE = np.dtype([(n, "i1") for n in ("mtype", "cbp", "mvx", "mvy")])
 
@@ -321,10 +322,11 @@ def IZigzagMatrix(m):  # transform.c:546
 
 
 def MotionEstimation(ref, cur, width: int, height: int, mode: int = ME_TSS,
-                     search_limit: int = 15, frame_stride: int | None = None):
+                     search_limit: int = 15, frame_stride: int | None = None, out=None):
     """me.c:340 over a batch: ref/cur are uint8 device tensors holding nframes
     pictures (or luma planes) `frame_stride` bytes apart.  Returns an int32
-    tensor [nframes, nmb, 7] = (MeX, MeY, MeVal, MeOVal, MeVAR, MeVAROR, MeMWOR)."""
+    tensor [nframes, nmb, 7] = (MeX, MeY, MeVal, MeOVal, MeVAR, MeVAROR, MeMWOR)
+    (written into `out` when given)."""
     torch = _torch()
     _dev_check(ref, torch.uint8, "ref")
     _dev_check(cur, torch.uint8, "cur")
@@ -333,7 +335,12 @@ def MotionEstimation(ref, cur, width: int, height: int, mode: int = ME_TSS,
     if nframes < 1 or ref.numel() < (nframes - 1) * stride + width * height:
         raise P64GpuError("ref/cur hold fewer pictures than the geometry needs")
     nmb = (width // 16) * (height // 16)
-    out = torch.empty((nframes, nmb, 7), dtype=torch.int32, device=cur.device)
+    if out is None:
+        out = torch.empty((nframes, nmb, 7), dtype=torch.int32, device=cur.device)
+    else:
+        _dev_check(out, torch.int32, "out")
+        if out.numel() < nframes * nmb * 7:
+            raise P64GpuError("out smaller than nframes x nmb records")
     _check(lib().p64gpu_motion_estimation(width, height, nframes, stride, ref.data_ptr(),
                                           cur.data_ptr(), mode, search_limit, out.data_ptr(),
                                           _stream(torch)))
@@ -350,8 +357,11 @@ class FrameBatchOut:
 def encode_frames(cur, ref, recon, last_intra, *, width: int, height: int, intra: bool,
                   quant: int = 8, me_mode: int = ME_TSS, search_limit: int = 15,
                   quant_mb=None, mtype_override=None, out: FrameBatchOut | None = None,
-                  want_me: bool = True) -> FrameBatchOut:
-    """One picture of each of `nframes` independent sequences (p64.c:622-1013)."""
+                  want_me: bool = True, me_given: bool = False) -> FrameBatchOut:
+    """One picture of each of `nframes` independent sequences (p64.c:622-1013).
+    me_given: out.me already holds the batch's ME records (MotionEstimation
+    over the same pictures, search mode and limit): the search is not run
+    again (P64GPU_FLAG_ME_GIVEN)."""
     torch = _torch()
     stride = picture_bytes(width, height)
     nframes = cur.numel() // stride
@@ -391,10 +401,13 @@ def encode_frames(cur, ref, recon, last_intra, *, width: int, height: int, intra
     # allocation is stream- and graph-safe (the caching allocator), so the
     # library's own per-stream scratch is never needed from Python
     me = out.me
+    if me_given and (intra or me is None):
+        raise P64GpuError("me_given needs an inter batch and out.me holding its records")
     if me is None and not intra:
         me = torch.empty((nframes, nmb, 7), dtype=torch.int32, device=dev)
     a = EncodeArgs(width=width, height=height, nframes=nframes, intra=int(bool(intra)),
-                   quant=quant, me_mode=me_mode, search_limit=search_limit, reserved=0,
+                   quant=quant, me_mode=me_mode, search_limit=search_limit,
+                   flags=P64GPU_FLAG_ME_GIVEN if me_given else 0,
                    frame_stride=stride, cur=cur.data_ptr(),
                    ref=(ref.data_ptr() if ref is not None else None), recon=recon.data_ptr(),
                    last_intra=last_intra.data_ptr(),

@@ -181,17 +181,20 @@ int encode_launch(const p64gpu_encode_args *a, const int32_t *mb_list, int count
     return fail(P64GPU_E_INVALID, "me mode %d", a->me_mode);
   if (a->search_limit < 1 || a->search_limit > 31)
     return fail(P64GPU_E_INVALID, "search_limit %d not in 1..31", a->search_limit);
-  if (a->reserved != 0) return fail(P64GPU_E_INVALID, "reserved must be 0");
+  if (a->flags & ~P64GPU_FLAG_ME_GIVEN) return fail(P64GPU_E_INVALID, "flags 0x%x: unknown bits", a->flags);
+  const bool me_given = (a->flags & P64GPU_FLAG_ME_GIVEN) != 0;
+  if (me_given && (a->intra || !a->me || mb_list))
+    return fail(P64GPU_E_INVALID, "P64GPU_FLAG_ME_GIVEN needs an inter picture batch with args->me");
   hipStream_t st = (hipStream_t)stream;
   const int mode = a->intra ? 0 : (a->me_mode == P64GPU_ME_FULL ? 2 : 1);
-  if (!mb_list && !fused_forced()) {
+  if (!mb_list && (!fused_forced() || me_given)) {
     const int nmb = (a->width / 16) * (a->height / 16);
     // inter: ME for the whole batch into the caller's records or the scratch
     p64_me_rec *me = nullptr;
     std::unique_lock<std::mutex> lk;  // held while the scratch is in use (me_scratch)
     if (!a->intra) me = a->me ? a->me : me_scratch((size_t)a->nframes * nmb, st, lk);
     if (a->intra || me) {
-      if (!a->intra)
+      if (!a->intra && !me_given)
         HIP_TRY(p64k::motion(mode, a->width, a->height, a->nframes, a->frame_stride, a->ref, a->cur,
                              a->search_limit, me, st));
       const int chunk = pictures_per_launch(a->width, a->height, a->frame_stride);

@@ -59,7 +59,7 @@ int main(void) {
   printf("sizeof_args %zu\nsizeof_me %zu\nsizeof_mb %zu\n", sizeof(p64gpu_encode_args),
          sizeof(p64_me_rec), sizeof(p64_mb_rec));
   O(width); O(height); O(nframes); O(intra); O(quant); O(me_mode); O(search_limit);
-  O(reserved); O(frame_stride); O(cur); O(ref); O(recon); O(last_intra); O(quant_mb);
+  O(flags); O(frame_stride); O(cur); O(ref); O(recon); O(last_intra); O(quant_mb);
   O(mtype_override); O(coef); O(mb); O(me);
   return 0;
 }''')
@@ -84,6 +84,18 @@ def test_invalid_arguments_rejected_without_device(p64):
                        cur=16, recon=16, last_intra=16, coef=16, mb=16, intra=1)
     assert L.p64gpu_encode_frames(ctypes.byref(a), None) == -1
     assert b"quant" in L.p64gpu_last_error()
+    # flags: unknown bits, and P64GPU_FLAG_ME_GIVEN without an inter batch with records
+    a = p64.EncodeArgs(width=176, height=144, nframes=1, quant=8, frame_stride=38016, me_mode=1,
+                       search_limit=31, cur=16, ref=16, recon=16, last_intra=16, coef=16, mb=16,
+                       flags=2)
+    assert L.p64gpu_encode_frames(ctypes.byref(a), None) == -1
+    assert b"flags" in L.p64gpu_last_error()
+    a.flags = p64.P64GPU_FLAG_ME_GIVEN  # args.me is NULL
+    assert L.p64gpu_encode_frames(ctypes.byref(a), None) == -1
+    assert b"ME_GIVEN" in L.p64gpu_last_error()
+    a.me, a.intra = 16, 1
+    assert L.p64gpu_encode_frames(ctypes.byref(a), None) == -1
+    assert b"ME_GIVEN" in L.p64gpu_last_error()
     assert L.p64gpu_block_op(99, 16, 16, 1, 8, 8, None) == -1
     assert L.p64gpu_block_op(2, 16, 16, 1, 8, 0, None) == -1  # acq 0
     assert L.p64gpu_block_op(0, None, None, 0, 8, 8, None) == 0  # empty batch is a no-op

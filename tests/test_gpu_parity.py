@@ -345,12 +345,47 @@ def test_split_encoder_without_me_output_and_in_graph(p64, torch_dev):
         np.testing.assert_array_equal(rec, ref_rec)
 
 
+@pytest.mark.parametrize("mode,sl", [(1, 31), (1, 15), (0, 15)])
+def test_encode_with_given_me_records(p64, torch_dev, mode, sl):
+    """P64GPU_FLAG_ME_GIVEN: the reference's own order -- MotionEstimation
+    for the picture (me.c:340) as its own call, then the MDU loop reading the
+    records (p64.c:734-756) -- gives the same levels, records and
+    reconstructions as the encode that runs the search itself."""
+    torch = torch_dev
+    w, h, S, T = 352, 288, 3, 4
+    nmb, pic = (w // 16) * (h // 16), w * h * 3 // 2
+    frames = [dev(torch, np.stack([p64.synth_frame(21 + s, t, w, h) for s in range(S)])).reshape(-1)
+              for t in range(T)]
+
+    def run(given):
+        li = torch.zeros(S * nmb, dtype=torch.uint8, device="cuda")
+        bufs = [torch.zeros(S * pic, dtype=torch.uint8, device="cuda") for _ in range(2)]
+        got = []
+        for t in range(T):
+            ref, rec = bufs[t % 2], bufs[(t + 1) % 2]
+            o = p64.FrameBatchOut(coef=torch.empty((S, nmb, 6, 64), dtype=torch.int16, device="cuda"),
+                                  mb=torch.empty((S, nmb, 4), dtype=torch.int8, device="cuda"),
+                                  me=torch.empty((S, nmb, 7), dtype=torch.int32, device="cuda"))
+            if given and t > 0:
+                o.me.copy_(p64.MotionEstimation(ref, frames[t], w, h, mode=mode, search_limit=sl))
+            p64.encode_frames(frames[t], ref, rec, li, width=w, height=h, intra=(t == 0), quant=8,
+                              me_mode=mode, search_limit=sl, out=o, me_given=given and t > 0)
+            torch.cuda.synchronize()
+            got.append((host(o.coef), host(o.mb), host(o.me) if t > 0 else None, host(rec)))
+        return got
+
+    for t, (a, b) in enumerate(zip(run(False), run(True))):
+        for x, y in zip(a, b):
+            if x is not None:
+                np.testing.assert_array_equal(x, y, err_msg=f"picture {t}")
+
+
 def _raw_encode(p64, torch, cur, ref, recon, li, coef, mb, *, w, h, stream, me=None):
     """p64gpu_encode_frames straight through the C ABI (me = NULL unless given)."""
     import ctypes
     nframes = cur.numel() // p64.picture_bytes(w, h)
     a = p64.EncodeArgs(width=w, height=h, nframes=nframes, intra=0, quant=8, me_mode=p64.ME_FULL,
-                       search_limit=31, reserved=0, frame_stride=p64.picture_bytes(w, h),
+                       search_limit=31, flags=0, frame_stride=p64.picture_bytes(w, h),
                        cur=cur.data_ptr(), ref=ref.data_ptr(), recon=recon.data_ptr(),
                        last_intra=li.data_ptr(), quant_mb=None, mtype_override=None,
                        coef=coef.data_ptr(), mb=mb.data_ptr(),
