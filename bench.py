@@ -491,9 +491,11 @@ def timed_region(torch, dist, world, steps, t_first, launch, pre=None, post=None
     spinup_ms -- every replay the same work as the timed one, outputs
     discarded -- and the timed region follows.  Nothing the timed steps read
     is produced by the spin-up, and no work is dropped from them.
-    spin["split"](t), if given, returns the step as its separate launches
-    [(kernel name, fn)]: one more reset + eager pass times each with HIP
-    events (the live per-kernel split of the step, e.g. k_motion alone).
+    spin["split"](t, k), if given, returns step t (the k-th) as its separate
+    launches [(kernel name, fn)], in order: each part's K launches are
+    captured into a graph of their own and replayed once after the spin-up
+    (reset first), timed with HIP events -- the live per-kernel split of the
+    step (k_motion alone, then the rest from its records).
     A 50-us clock probe after the region reads the clock the chip was left
     at (box-to-box spread).
     Returns (wall seconds of the timed region, mean kernel seconds per step,
@@ -536,22 +538,23 @@ def timed_region(torch, dist, world, steps, t_first, launch, pre=None, post=None
         torch.cuda.synchronize()
         st["spinup_replays"] = 1 + n
         st["spinup_ms_actual"] = round((time.perf_counter() - t0) * 1e3, 1)
-        if spin.get("split"):  # the split again, now at steady clocks
-            spin["reset"]()
-            evs = {}
-            for k in range(steps):
-                for nm, fn in spin["split"](t_first + k):
-                    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                    a.record()
-                    fn()
-                    b.record()
-                    evs.setdefault(nm, []).append((a, b))
-            torch.cuda.synchronize()
-            st["kernels_us_live"] = {nm: round(sum(a.elapsed_time(b) for a, b in v) * 1e3 / len(v), 2)
-                                     for nm, v in evs.items()}
-            st["kernels_us_live_note"] = ("each kernel of the step launched on its own (eager, HIP events "
-                                          "around each launch), same steps and state as the timed region, "
-                                          "right after the spin-up")
+        if spin.get("split") and graph:  # each kernel of the step on its own, at steady clocks
+            parts = spin["split"](t_first, 0)
+            live = {}
+            for p, (nm, _) in enumerate(parts):
+                gp = capture(lambda t, p=p: spin["split"](t, t - t_first)[p][1]())
+                spin["reset"]()
+                a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                a.record()
+                gp.replay()
+                b.record()
+                torch.cuda.synchronize()
+                live[nm] = round(a.elapsed_time(b) * 1e3 / steps, 2)
+                del gp
+            st["kernels_us_live"] = live
+            st["kernels_us_live_note"] = ("each kernel of the step alone: a graph of its K launches (same "
+                                          "steps and state as the timed region) replayed right after the "
+                                          "spin-up, HIP events around the replay, / K")
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
           for _ in range(1 if graph else steps)]
     torch.cuda.synchronize()
@@ -704,17 +707,22 @@ def main(argv=None):
                 a.copy_(b)
             sp["li"].copy_(li)
 
-        def spin_launch(t, me_given=False):
+        def spin_launch(t):
             p64_amd.encode_frames(frames[slot(t)].reshape(-1), sp["rec"][(t + 1) % 2], sp["rec"][t % 2],
                                   sp["li"], width=w, height=h, intra=False, quant=args.quant,
-                                  me_mode=mode, search_limit=args.search_limit, out=sp["out"],
-                                  me_given=me_given)
+                                  me_mode=mode, search_limit=args.search_limit, out=sp["out"])
 
-        def spin_split(t):  # the step as its two kernels: the search, then the rest
+        def spin_split(t, k):  # step t as its two kernels: the search, then the rest from its records
+            if "mes" not in sp:
+                sp["mes"] = [torch.empty_like(me) for _ in range(args.steps)]
+            o = p64_amd.FrameBatchOut(coef=sp["out"].coef, mb=sp["out"].mb, me=sp["mes"][k])
             return [(kme, lambda: p64_amd.MotionEstimation(
                         sp["rec"][t % 2], frames[slot(t)].reshape(-1), w, h, mode=mode,
-                        search_limit=args.search_limit, out=sp["out"].me)),
-                    (kin, lambda: spin_launch(t, me_given=True))]
+                        search_limit=args.search_limit, out=sp["mes"][k])),
+                    (kin, lambda: p64_amd.encode_frames(
+                        frames[slot(t)].reshape(-1), sp["rec"][(t + 1) % 2], sp["rec"][t % 2], sp["li"],
+                        width=w, height=h, intra=False, quant=args.quant, me_mode=mode,
+                        search_limit=args.search_limit, out=o, me_given=True))]
 
         for t in range(1 + args.warmup):  # intra picture + warmup, untimed
             step(t)
