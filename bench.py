@@ -491,11 +491,11 @@ def timed_region(torch, dist, world, steps, t_first, launch, pre=None, post=None
     spinup_ms -- every replay the same work as the timed one, outputs
     discarded -- and the timed region follows.  Nothing the timed steps read
     is produced by the spin-up, and no work is dropped from them.
-    spin["split"](t, k), if given, returns step t (the k-th) as its separate
-    launches [(kernel name, fn)], in order: each part's K launches are
-    captured into a graph of their own and replayed once after the spin-up
-    (reset first), timed with HIP events -- the live per-kernel split of the
-    step (k_motion alone, then the rest from its records).
+    spin["split"] = (first, rest, full(t, k), part(t, k)), if given, splits
+    the step's time between its two kernels: a graph of the K full steps
+    (full: step t, the k-th, keeping what the second kernel needs) and one
+    of the second kernels alone (part), each replayed once after a reset and
+    timed with HIP events; the first kernel's time is the difference.
     A 50-us clock probe after the region reads the clock the chip was left
     at (box-to-box spread).
     Returns (wall seconds of the timed region, mean kernel seconds per step,
@@ -538,23 +538,25 @@ def timed_region(torch, dist, world, steps, t_first, launch, pre=None, post=None
         torch.cuda.synchronize()
         st["spinup_replays"] = 1 + n
         st["spinup_ms_actual"] = round((time.perf_counter() - t0) * 1e3, 1)
-        if spin.get("split") and graph:  # each kernel of the step on its own, at steady clocks
-            parts = spin["split"](t_first, 0)
-            live = {}
-            for p, (nm, _) in enumerate(parts):
-                gp = capture(lambda t, p=p: spin["split"](t, t - t_first)[p][1]())
+        if spin.get("split") and graph:  # the step's kernels apart, at steady clocks
+            first, rest, full, part = spin["split"]
+            times = {}
+            for nm, fn in (("step", full), (rest, part)):
+                gp = capture(lambda t, fn=fn: fn(t, t - t_first))
                 spin["reset"]()
                 a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 a.record()
                 gp.replay()
                 b.record()
                 torch.cuda.synchronize()
-                live[nm] = round(a.elapsed_time(b) * 1e3 / steps, 2)
+                times[nm] = a.elapsed_time(b) * 1e3 / steps
                 del gp
-            st["kernels_us_live"] = live
-            st["kernels_us_live_note"] = ("each kernel of the step alone: a graph of its K launches (same "
-                                          "steps and state as the timed region) replayed right after the "
-                                          "spin-up, HIP events around the replay, / K")
+            st["kernels_us_live"] = {first: round(times["step"] - times[rest], 2), rest: round(times[rest], 2)}
+            st["kernels_us_live_note"] = (
+                f"graphs of the K steps right after the spin-up (same steps and state as the timed "
+                f"region), HIP events around each replay, / K: the whole step ({times['step']:.2f} us) "
+                f"recording each step's ME records, then {rest} alone from those records "
+                f"(P64GPU_FLAG_ME_GIVEN); {first} = the difference")
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
           for _ in range(1 if graph else steps)]
     torch.cuda.synchronize()
@@ -712,17 +714,21 @@ def main(argv=None):
                                   sp["li"], width=w, height=h, intra=False, quant=args.quant,
                                   me_mode=mode, search_limit=args.search_limit, out=sp["out"])
 
-        def spin_split(t, k):  # step t as its two kernels: the search, then the rest from its records
+        def spin_out(k):  # scratch outputs with step k's own ME records
             if "mes" not in sp:
                 sp["mes"] = [torch.empty_like(me) for _ in range(args.steps)]
-            o = p64_amd.FrameBatchOut(coef=sp["out"].coef, mb=sp["out"].mb, me=sp["mes"][k])
-            return [(kme, lambda: p64_amd.MotionEstimation(
-                        sp["rec"][t % 2], frames[slot(t)].reshape(-1), w, h, mode=mode,
-                        search_limit=args.search_limit, out=sp["mes"][k])),
-                    (kin, lambda: p64_amd.encode_frames(
-                        frames[slot(t)].reshape(-1), sp["rec"][(t + 1) % 2], sp["rec"][t % 2], sp["li"],
-                        width=w, height=h, intra=False, quant=args.quant, me_mode=mode,
-                        search_limit=args.search_limit, out=o, me_given=True))]
+            return p64_amd.FrameBatchOut(coef=sp["out"].coef, mb=sp["out"].mb, me=sp["mes"][k])
+
+        def spin_full(t, k):  # the whole step, its ME records kept
+            p64_amd.encode_frames(frames[slot(t)].reshape(-1), sp["rec"][(t + 1) % 2], sp["rec"][t % 2],
+                                  sp["li"], width=w, height=h, intra=False, quant=args.quant,
+                                  me_mode=mode, search_limit=args.search_limit, out=spin_out(k))
+
+        def spin_rest(t, k):  # the step after the search, from those records
+            p64_amd.encode_frames(frames[slot(t)].reshape(-1), sp["rec"][(t + 1) % 2], sp["rec"][t % 2],
+                                  sp["li"], width=w, height=h, intra=False, quant=args.quant,
+                                  me_mode=mode, search_limit=args.search_limit, out=spin_out(k),
+                                  me_given=True)
 
         for t in range(1 + args.warmup):  # intra picture + warmup, untimed
             step(t)
@@ -738,7 +744,8 @@ def main(argv=None):
                                           pre if root else None, post if root else None,
                                           graph=not args.eager, spinup_ms=args.spinup_ms,
                                           spin={"init": spin_init, "reset": spin_reset,
-                                                "launch": spin_launch, "split": spin_split})
+                                                "launch": spin_launch,
+                                                "split": (kme, kin, spin_full, spin_rest)})
         sp.clear()
         tmax = max_over_ranks(elapsed, world, device="cuda")
         last = t_first + args.steps - 1
