@@ -377,11 +377,26 @@ class VlcArgs(ctypes.Structure):
                 ("bits", ctypes.c_void_p), ("scratch", ctypes.c_void_p)]
 
 
-def vlc_pictures(mb, coef, gquant, tr, *, width: int, height: int, phase=None, mquant=None):
+def vlc_buffers(n: int, width: int, height: int):
+    """Device buffers for vlc_pictures over n pictures: (out, bits, scratch)."""
+    import torch
+
+    _, _, ngob = geometry(format_of(width, height))
+    nmb = ngob * 33
+    stride = (int(lib().p64gpu_vlc_max_bytes(width, height)) + 3) // 4 * 4
+    return (torch.empty((n, stride), dtype=torch.uint8, device="cuda"),
+            torch.empty(n, dtype=torch.int32, device="cuda"),
+            torch.empty(2 * n * nmb, dtype=torch.int32, device="cuda"))
+
+
+def vlc_pictures(mb, coef, gquant, tr, *, width: int, height: int, phase=None, mquant=None,
+                 buffers=None, host_bits: bool = True):
     """H.261 bits of a batch of pictures on the GPU.  All inputs are CUDA(HIP)
     tensors: mb [n, nmb, 4] int8, coef [n, nmb, 6, 64] int16, gquant [n, ngob]
     uint8, tr [n] int32, phase [n] uint8 or None, mquant [n, nmb] uint8 or None.
-    Returns (out [n, stride] uint8 tensor, bits [n] list of ints)."""
+    buffers: (out, bits, scratch) from vlc_buffers, reused across calls.
+    Returns (out [n, stride] uint8 tensor, bits [n] list of ints) -- or, with
+    host_bits=False, the device bits tensor (no synchronisation)."""
     import torch
 
     from . import _stream, _torch
@@ -392,18 +407,20 @@ def vlc_pictures(mb, coef, gquant, tr, *, width: int, height: int, phase=None, m
     nmb = ngob * 33
     if mb.numel() != n * nmb * 4 or coef.numel() != n * nmb * 384 or gquant.numel() != n * ngob:
         raise P64GpuError("vlc_pictures: buffer sizes do not match the picture format")
-    stride = int(L.p64gpu_vlc_max_bytes(width, height))
-    stride = (stride + 3) // 4 * 4
-    out = torch.empty((n, stride), dtype=torch.uint8, device="cuda")
-    bits = torch.empty(n, dtype=torch.int32, device="cuda")
-    scratch = torch.empty(2 * n * nmb, dtype=torch.int32, device="cuda")
+    out, bits, scratch = buffers if buffers is not None else vlc_buffers(n, width, height)
+    stride = int(out.shape[1])
+    if out.shape[0] < n or bits.numel() < n or scratch.numel() < 2 * n * nmb or \
+            stride < int(L.p64gpu_vlc_max_bytes(width, height)):
+        raise P64GpuError("vlc_pictures: buffers smaller than the batch")
     a = VlcArgs(width=width, height=height, nframes=n, reserved=0, mb=mb.data_ptr(),
                 coef=coef.data_ptr(), gquant=gquant.data_ptr(),
                 mquant=mquant.data_ptr() if mquant is not None else None, tr=tr.data_ptr(),
                 phase=phase.data_ptr() if phase is not None else None, out=out.data_ptr(),
                 out_stride=stride, bits=bits.data_ptr(), scratch=scratch.data_ptr())
     _check(L.p64gpu_vlc_pictures(ctypes.byref(a), _stream(torch)))
-    b = [int(x) & 0xFFFFFFFF for x in bits.cpu().tolist()]
+    if not host_bits:
+        return out, bits[:n]
+    b = [int(x) & 0xFFFFFFFF for x in bits[:n].cpu().tolist()]
     if any(x == 0xFFFFFFFF for x in b):
         raise P64GpuError("vlc_pictures: invalid macroblock record or buffer overflow")
     return out, b
