@@ -475,12 +475,9 @@ struct PredSrc {
   uint32_t d[8][3];
   int sh;
 };
-__device__ __forceinline__ void pred_row(const PredSrc &p, int r, int s[8]) {
-  unpack8(align4(p.d[r][1], p.d[r][0], p.sh), align4(p.d[r][2], p.d[r][1], p.sh), s);
-}
-// horizontal taps of the H.261 loop filter: [1 2 1], edge columns x4.
-// the horizontal taps of a row as four packed 16-bit pairs (hz_2i, hz_2i+1):
-// every tap sum is at most 4 x 255 = 1,020
+// the horizontal taps of the H.261 loop filter ([1 2 1], edge columns x4) of
+// a row as four packed 16-bit pairs (hz_2i, hz_2i+1), each tap sum one byte
+// dot product of the packed source row: at most 4 x 255 = 1,020
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ void hz_row_pk(const PredSrc &p, int r, u16x2 hz[4]) {
   const uint32_t lo = align4(p.d[r][1], p.d[r][0], p.sh), hi = align4(p.d[r][2], p.d[r][1], p.sh);
@@ -496,7 +493,7 @@ __device__ __forceinline__ void hz_row_pk(const PredSrc &p, int r, u16x2 hz[4]) 
 #pragma unroll
   for (int i = 0; i < 4; i++) hz[i] = __builtin_bit_cast(u16x2, (w[2 * i + 1] << 16) | w[2 * i]);
 }
-// pred_rows' loop filter in packed 16-bit arithmetic (decoder): the vertical
+// pred_rows' loop filter in packed 16-bit arithmetic: the vertical
 // [1 2 1] + 8 >> 4 of the tap pairs (at most 4 x 1,020 + 8 = 4,088) as
 // v_pk_ operations, half the registers of the unpacked rows
 __device__ __forceinline__ void pred_rows_filter_pk(const PredSrc &P, uint2 prow[8]) {
@@ -521,15 +518,6 @@ __device__ __forceinline__ void pred_rows_filter_pk(const PredSrc &P, uint2 prow
     }
     if (r + 2 < 8) hz_row_pk(P, r + 2, hn);
   }
-}
-// unpacked (k_inter_mbg: the packed form of the decoder measured no gain there)
-__device__ __forceinline__ void hz_row(const PredSrc &p, int r, int hz[8]) {
-  int s[8];
-  pred_row(p, r, s);
-  hz[0] = s[0] << 2;
-#pragma unroll
-  for (int k = 1; k < 7; k++) hz[k] = s[k - 1] + 2 * s[k] + s[k + 1];
-  hz[7] = s[7] << 2;
 }
 // decoder reconstruction (DecompressMDU p64.c:1179-1237 + DecodeSaveMDU
 // p64.c:971-1013), block layout: a lane loads its MB's record, then its
@@ -641,7 +629,6 @@ __device__ __forceinline__ uint2 recon_row(const int v[8], uint2 pr) {
   }
   return make_uint2(__builtin_amdgcn_perm(o2[1], o2[0], 0x05040100u), __builtin_amdgcn_perm(o2[3], o2[2], 0x05040100u));
 }
-template <bool PK>
 __device__ __forceinline__ void pred_rows(const PredSrc &P, bool filter, uint2 prow[8]);
 // IQ + ChenIDct + reconstruction over a wave's CODED blocks only (decoder
 // and k_inter_mbg).  A wave holds 60 blocks, typically a quarter of them with
@@ -754,7 +741,7 @@ __device__ __forceinline__ void rec_wave_compact(int w, int h, int64_t stride, _
                                                  int lane) {
   const BlkPos &p = A.p;
   uint2 prow[8];
-  pred_rows<true>(S.pred, S.filter && S.inter, prow);  // zeros for intra (source not loaded)
+  pred_rows(S.pred, S.filter && S.inter, prow);  // zeros for intra (source not loaded)
   const int pw = p.plane ? w >> 1 : w;
   const uint32_t ro = (uint32_t)((int64_t)p.fi * stride) + (uint32_t)plane_offset(p.plane, w, h) +
                       (uint32_t)(mul24(p.y, pw) + p.x);
@@ -843,7 +830,6 @@ __global__ __launch_bounds__(64) OCC4 void k_recon_mbg(int w, int h, int64_t str
 // reconstruction.  The fused one-wave-per-MB k_encode spends 40% of its time
 // in this half with 48 of 64 lanes busy on LDS-exchanged row passes; here
 // every lane holds its block in registers.
-template <bool PK>
 __device__ __forceinline__ void pred_rows(const PredSrc &P, bool filter, uint2 prow[8]);
 struct InterMe {  // the fields of p64_me_rec the decision needs
   int mx, my, sad, sad0, var, varor;
@@ -858,32 +844,15 @@ __device__ __forceinline__ void inter_pred(const RecBufs &B, int w, int h, int64
   A.coded = 1;
   const RecStageB S = rec_stage_b<false>(B, w, h, stride, A);  // source OOB (zeros) if intra
   PRIO_LOW();  // the loads are out: the loop filter at normal priority
-  pred_rows<false>(S.pred, S.filter, prow);
+  pred_rows(S.pred, S.filter, prow);
 }
-// the prediction as packed rows (all zero when the source was not loaded);
-// PK: the loop filter in packed 16-bit arithmetic (decoder)
-template <bool PK>
+// the prediction as packed rows (all zero when the source was not loaded),
+// the H.261 loop filter in packed 16-bit arithmetic (pred_rows_filter_pk;
+// k_inter_mbg -0.45 us and the step -1.5 us against the unpacked adds,
+// A/B x2 in round 4)
 __device__ __forceinline__ void pred_rows(const PredSrc &P, bool filter, uint2 prow[8]) {
-  if (PK && filter) {
+  if (filter) {
     pred_rows_filter_pk(P, prow);
-  } else if (filter) {  // add_pred's loop filter, one packed row at a time
-    int hp[8], hc[8], hn[8];
-    hz_row(P, 0, hc);
-    hz_row(P, 1, hn);
-#pragma unroll
-    for (int r = 0; r < 8; r++) {
-      int o[8];
-#pragma unroll
-      for (int k = 0; k < 8; k++)
-        o[k] = (r == 0 || r == 7) ? ((hc[k] << 2) + 8) >> 4 : (hp[k] + 2 * hc[k] + hn[k] + 8) >> 4;
-      prow[r] = pack8(o);
-#pragma unroll
-      for (int k = 0; k < 8; k++) {
-        hp[k] = hc[k];
-        hc[k] = hn[k];
-      }
-      if (r + 2 < 8) hz_row(P, r + 2, hn);
-    }
   } else {  // the source rows as they are
 #pragma unroll
     for (int r = 0; r < 8; r++)
