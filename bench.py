@@ -937,9 +937,9 @@ def measure_vlc(args, torch, p64_amd, step, out_of, S, nmb, w, h):
     """The encode steps followed by entropy coding on the device (p64vlc.hip):
     the whole-encoder rate to .p64 bits, measured after the metric (it re-runs
     steps, so the closed-loop state is not reused).  Per step: the encode
-    launches, the three VLC launches and an asynchronous copy of every
-    picture's bit count to pinned host memory; one synchronisation at the end
-    (a host encoder pipeline keeps the device busy the same way)."""
+    launches, the three VLC launches and a copy of every picture's bit count
+    to pinned host memory, the steps captured in one HIP graph (as the
+    metric's steps are) and replayed once, wall-clock timed."""
     try:
         from p64_amd import stream as p64s
         ngob = nmb // 33
@@ -953,18 +953,34 @@ def measure_vlc(args, torch, p64_amd, step, out_of, S, nmb, w, h):
                           buffers=bufs)  # first call: table upload
         torch.cuda.synchronize()
         vlc_ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
-        t1 = time.perf_counter()
-        for k in range(vsteps):
+        bits_dev = [None] * vsteps
+
+        def vstep(k, ev=False):
             t = 1 + args.warmup + k
             step(t)
             o = out_of(t)
-            vlc_ev[0].record()
-            _, bits = p64s.vlc_pictures(o.mb, o.coef, gq, trs[k], width=w, height=h, buffers=bufs,
-                                        host_bits=False)
-            vlc_ev[1].record()
-            host[k].copy_(bits, non_blocking=True)
+            if ev:
+                vlc_ev[0].record()
+            _, bits_dev[k] = p64s.vlc_pictures(o.mb, o.coef, gq, trs[k], width=w, height=h, buffers=bufs,
+                                               host_bits=False)
+            if ev:
+                vlc_ev[1].record()
+            host[k].copy_(bits_dev[k], non_blocking=True)
+
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            for k in range(vsteps):
+                vstep(k)
+        torch.cuda.synchronize()
+        g.replay()  # the first replay uploads the graph; the second is timed (its first
+        torch.cuda.synchronize()  # step predicts from the first replay's last picture)
+        t1 = time.perf_counter()
+        g.replay()
         torch.cuda.synchronize()
         dt = time.perf_counter() - t1
+        del g
+        vstep(vsteps - 1, ev=True)  # the VLC launches of one step alone, eagerly (vlc_ms_last_step)
+        torch.cuda.synchronize()
         hb = host.numpy().astype(np.int64) & 0xFFFFFFFF
         if (hb == 0xFFFFFFFF).any():
             return {"error": "vlc: invalid record or overflow"}
@@ -973,7 +989,8 @@ def measure_vlc(args, torch, p64_amd, step, out_of, S, nmb, w, h):
                 "vlc_ms_last_step": round(vlc_ev[0].elapsed_time(vlc_ev[1]), 4),
                 "avg_bits_per_mb": round(float(hb.sum()) / (S * nmb * vsteps), 2),
                 "note": "encode launches + GPU entropy coding (count, scan, emit) per step, every "
-                        "picture's bit count copied to the host asynchronously; not part of `value`"}
+                        "picture's bit count copied to pinned host memory, the steps replayed as one "
+                        "HIP graph; not part of `value`"}
     except Exception as e:  # never let the extra measurement cost the bench line
         return {"error": str(e)[:200]}
 

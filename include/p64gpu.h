@@ -210,7 +210,7 @@ int p64gpu_decode_recon(int width, int height, int nframes, int64_t frame_stride
  * byte -- the bit position the sequence's stream has reached -- so the host
  * appends it by OR-ing the first byte into its pending byte.  bits[i] receives
  * the bit count including the phase, or 0xFFFFFFFF if a record was invalid.
- * All pointers are device pointers; scratch holds 2*nframes*nmb uint32. */
+ * All pointers are device pointers; scratch holds 6*nframes*nmb uint32. */
 typedef struct {
   int width, height, nframes, reserved;
   const p64_mb_rec *mb;     /* [nframes][nmb] raster order (encoder output)   */
@@ -222,7 +222,7 @@ typedef struct {
   uint8_t *out;             /* [nframes][out_stride], zeroed by the call      */
   int64_t out_stride;       /* >= p64gpu_vlc_max_bytes, multiple of 4         */
   uint32_t *bits;           /* [nframes]                                      */
-  uint32_t *scratch;        /* [2][nframes][nmb]                              */
+  uint32_t *scratch;        /* [6][nframes][nmb]                              */
 } p64gpu_vlc_args;
 int64_t p64gpu_vlc_max_bytes(int width, int height);
 int p64gpu_vlc_pictures(const p64gpu_vlc_args *args, void *stream);

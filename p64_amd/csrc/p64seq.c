@@ -168,7 +168,7 @@ int p64seq_open(const p64seq_config *cfg, p64seq **out) {
     if ((st = p64gpu_alloc((void **)&s->d_vout, (size_t)s->vstride)) ||
         (st = p64gpu_alloc((void **)&s->d_vgq, 12)) || (st = p64gpu_alloc((void **)&s->d_vphase, 1)) ||
         (st = p64gpu_alloc((void **)&s->d_vbits, 4)) || (st = p64gpu_alloc((void **)&s->d_vtr, 4)) ||
-        (st = p64gpu_alloc((void **)&s->d_vscratch, 2 * nmb * sizeof(uint32_t))))
+        (st = p64gpu_alloc((void **)&s->d_vscratch, 6 * nmb * sizeof(uint32_t))))
       goto bad;
     if (!(s->h_vout = (uint8_t *)malloc((size_t)s->vstride))) {
       st = fail(P64GPU_E_NOMEM, "p64seq: host buffers");

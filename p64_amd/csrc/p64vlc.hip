@@ -48,6 +48,7 @@ struct VlcArgs {
   uint32_t *bits;     // [nframes]
   uint32_t *mb_bits;  // [nframes][nmb], stream order
   uint32_t *mb_off;   // [nframes][nmb], stream order
+  uint16_t *blk_bits; // [nframes][nmb][8], raster order: header bits, the six blocks' bits
 };
 
 __device__ __forceinline__ bool mt_quant(int m) { return m == 1 || m == 3 || m == 6 || m == 9; }
@@ -77,11 +78,10 @@ struct Header {
   int bits;
   bool bad;
 };
-__device__ __forceinline__ Header header_codes(const VlcTables &T, const VlcArgs &a, int fi, int g,
-                                               int m) {
+// r: the MB's record, rp: the previous MB's (the MVD predictor; MDUs 0, 11
+// and 22 reset it, marker.c:311-327), mq: its MQUANT, m: its MDU
+__device__ __forceinline__ Header header_codes(const VlcTables &T, p64_mb_rec r, p64_mb_rec rp, int mq, int m) {
   Header h;
-  const size_t base = (size_t)fi * a.nmb;
-  const p64_mb_rec r = a.mb[base + raster(a.format, g, m)];
   const int mt = r.mtype;
   h.bad = mt < 0 || mt > 9 || (mt_cbp(mt) && (r.cbp < 1 || r.cbp > 63));
 #pragma unroll
@@ -90,14 +90,13 @@ __device__ __forceinline__ Header header_codes(const VlcTables &T, const VlcArgs
   if (h.bad) return h;
   h.c[0] = Code{1u, 1};  // MBA = 1: every MDU is coded (p64.c:922)
   h.c[1] = tab(T, T_MTYPE + mt);
-  if (mt_quant(mt)) h.c[2] = Code{a.mquant ? (uint32_t)(a.mquant[base + raster(a.format, g, m)] & 31) : 0u, 5};
+  if (mt_quant(mt)) h.c[2] = Code{(uint32_t)(mq & 31), 5};
   if (mt_mf(mt)) {
     int dh = r.mvx, dv = r.mvy;
     if (m != 0 && m != 11 && m != 22) {
-      const p64_mb_rec p = a.mb[base + raster(a.format, g, m - 1)];
-      if (p.mtype >= 4 && p.mtype <= 9) {  // differential to the previous MC macroblock
-        dh -= p.mvx;
-        dv -= p.mvy;
+      if (rp.mtype >= 4 && rp.mtype <= 9) {  // differential to the previous MC macroblock
+        dh -= rp.mvx;
+        dv -= rp.mvy;
         dh += dh < -16 ? 32 : (dh > 15 ? -32 : 0);
         dv += dv < -16 ? 32 : (dv > 15 ? -32 : 0);
       }
@@ -109,29 +108,6 @@ __device__ __forceinline__ Header header_codes(const VlcTables &T, const VlcArgs
 #pragma unroll
   for (int i = 0; i < 6; i++) h.bits += h.c[i].len;
   return h;
-}
-
-// the code of this lane's level in block c (EncodeAC codec.c:96 / CBPEncodeAC
-// codec.c:141); len 0 for no code
-__device__ __forceinline__ Code level_code(const VlcTables &T, int lane, int lev, uint64_t nz,
-                                           bool cbp_block) {
-  if (!((nz >> lane) & 1)) return Code{0, 0};
-  const uint64_t below = nz & ((1ull << lane) - 1ull);
-  const int start = cbp_block ? 0 : 1;
-  const int prev = below ? 63 - __clzll(below) : start - 1;
-  const int run = lane - prev - 1;
-  const int al = lev < 0 ? -lev : lev;
-  const bool first = cbp_block && !below;
-  if (first && run == 0 && al == 1) {
-    const Code f = tab(T, T_FIRST01);
-    return Code{(f.v << 1) | (lev < 0), f.len + 1};
-  }
-  if (run < 27 && al < 16) {
-    const Code e = tab(T, T_TC + run * 16 + al);
-    if (e.len) return Code{(e.v << 1) | (lev < 0), e.len + 1};
-  }
-  const Code esc = tab(T, T_ESC);  // ESCAPE, 6-bit run, 8-bit level
-  return Code{(esc.v << 14) | ((uint32_t)run << 8) | ((uint32_t)lev & 0xffu), esc.len + 14};
 }
 
 // wave64 inclusive prefix sum in DPP steps (row_shr 1/2/4/8 inside each
@@ -150,129 +126,202 @@ __device__ __forceinline__ int wave_sum_i(int v) {
 }
 __device__ __forceinline__ int wave_excl_scan(int v, int) { return wave_incl_scan(v) - v; }
 
-// bits of `c` at bit position `pos` of a word buffer (MSB-first bytes,
-// little-endian words: bswap per word); LDS atomics in the emit kernel
-__device__ __forceinline__ void put_bits(uint32_t *out, int pos, Code c) {
-  if (!c.len) return;
-  const int w = pos >> 5;
-  const int sh = pos & 31;
-  const uint64_t x = (uint64_t)c.v << (64 - c.len - sh);  // big-endian within 64 bits
-  const uint32_t hi = (uint32_t)(x >> 32), lo = (uint32_t)x;
-  if (hi) atomicOr(out + w, __builtin_bswap32(hi));
-  if (lo) atomicOr(out + w + 1, __builtin_bswap32(lo));
+constexpr int VLC_WAVES = 4;  // waves per workgroup
+constexpr int VLC_MBS = 10;   // macroblocks per wave: lane 6m + b codes block b of MB m
+
+// raster macroblock k -> stream position j = 33 g + m (GOB g, MDU m; the
+// inverse of raster(): GOBs of 11 x 3 MBs, two per GOB row except in QCIF)
+__device__ __forceinline__ int stream_pos(int format, int k) {
+  const int mbw = format == P64S_QCIF ? 11 : 22;
+  const int mby = k / mbw, mbx = k - mby * mbw;
+  const int g = format == P64S_QCIF ? mby / 3 : (mby / 3) * 2 + mbx / 11;
+  return 33 * g + (mby % 3) * 11 + mbx % 11;
 }
 
-constexpr int SEG_WORDS = 256;  // >= (8192 bits) one macroblock's segment + headers
-constexpr int VLC_WAVES = 4;    // waves per workgroup
-constexpr int VLC_MBS = 1;      // consecutive stream-order macroblocks per wave
-
-// one macroblock (wave-wide); EMIT places its segment's bits into seg
-template <bool EMIT>
-__device__ __forceinline__ int code_mb(const VlcTables &T, const VlcArgs &a, int fi, int j,
-                                       int lane, uint32_t *seg, int64_t *seg_first) {
-  const int g = j / 33, m = j - g * 33;
-  const size_t base = (size_t)fi * a.nmb;
-  const int k = raster(a.format, g, m);
-  const p64_mb_rec r = a.mb[base + k];
-  const Header hd = header_codes(T, a, fi, g, m);
-  if (hd.bad) return -1;
-  const int mt = r.mtype;
-  const bool cbpt = mt_cbp(mt);
-  const int cbp = cbpt ? r.cbp : 0x3f;
-  // this macroblock's segment of the picture: [s0, off + bits), s0 including
-  // the GOB header before MDU 0 and the picture header before GOB 0
-  int64_t off = 0, s0 = 0, sbase = 0;
-  if (EMIT) {
-    off = a.mb_off[base + j];
-    s0 = j == 0 ? (a.phase ? a.phase[fi] : 0) : (m == 0 ? off - 26 : off);
-    sbase = s0 & ~(int64_t)31;  // seg[0] <-> picture word s0 >> 5
-    *seg_first = s0;
-    if (lane == 0) {
-      if (j == 0) {  // picture header (WritePictureHeader marker.c:103-135)
-        const int p0 = (int)(s0 - sbase);
-        put_bits(seg, p0, Code{0x10u, 20});
-        put_bits(seg, p0 + 20, Code{(uint32_t)a.tr[fi] & 31u, 5});
-        put_bits(seg, p0 + 25, Code{a.format == P64S_QCIF ? 0u : 4u, 6});
-        if (a.format == P64S_NTSC) put_bits(seg, p0 + 31, Code{0x18cu, 9});  // PSPARE 0x8c
-      }
-      if (m == 0) {  // GOB header (WriteGOBHeader marker.c:171-198)
-        const uint32_t gn = a.format == P64S_QCIF ? 2 * g + 1 : g + 1;
-        const uint32_t gq = a.gquant[(size_t)fi * a.ngob + g] & 31u;
-        put_bits(seg, (int)(off - 26 - sbase), Code{(1u << 10) | (gn << 6) | (gq << 1), 26});
-      }
-      int p = (int)(off - sbase);
-#pragma unroll
-      for (int i = 0; i < 6; i++) {
-        put_bits(seg, p, hd.c[i]);
-        p += hd.c[i].len;
-      }
+// The bit writer of one lane: a segment of the picture's bits starting at
+// bit `pos`, MSB first, big-endian bytes in little-endian words (one bswap
+// per word).  A word wholly inside the segment is stored; the first and the
+// last, which neighbouring segments share, are ORed in (k_vlc_scan zeroed
+// every word of the picture).
+struct BitWriter {
+  uint64_t acc;  // the pending bits, right-aligned
+  int nacc;      // how many (< 32 between appends)
+  int64_t w;     // picture word the pending bits start in
+  bool first;    // that word is the segment's first (shared)
+  uint32_t *out;
+  __device__ __forceinline__ void start(uint32_t *o, int64_t pos) {
+    out = o;
+    w = pos >> 5;
+    nacc = (int)(pos & 31);  // the bits before the segment, as zeros
+    acc = 0;
+    first = true;
+  }
+  __device__ __forceinline__ void put(uint32_t v, int n) {  // n <= 32
+    acc = (acc << n) | v;
+    nacc += n;
+    if (nacc >= 32) {
+      const uint32_t word = __builtin_bswap32((uint32_t)(acc >> (nacc - 32)));
+      if (first)
+        atomicOr(out + w, word);
+      else
+        out[w] = word;
+      first = false;
+      w++;
+      nacc -= 32;
     }
   }
-  int bits = hd.bits;
-  if (mt_tc(mt)) {
-    int levs[6];  // all six blocks' levels in flight at once (latency, not bandwidth, binds)
+  __device__ __forceinline__ void finish() {  // the last, partial word
+    if (nacc > 0) atomicOr(out + w, __builtin_bswap32((uint32_t)(acc << (32 - nacc))));
+  }
+};
+
+// the codes of one block's levels (EncodeAC codec.c:96 / CBPEncodeAC
+// codec.c:141), scan positions from `s0` (1 for intra blocks: the DC is
+// coded alone); EMIT: into the writer, else only counted.  Returns the
+// bits, EOB included (0 for a CBP-type block without a level: nothing is
+// written, codec.c:151).
+template <bool EMIT>
+__device__ __forceinline__ int block_codes(const VlcTables &T, const uint32_t lv[32], bool cbpt, BitWriter &bw) {
+  int bits = 0, run = 0;
+  bool first = cbpt, any = false;
 #pragma unroll
-    for (int c = 0; c < 6; c++) levs[c] = a.coef[(base + k) * 384 + c * 64 + lane];
-#pragma unroll
-    for (int c = 0; c < 6; c++) {
-      if (!((cbp >> (5 - c)) & 1)) continue;
-      const int lev = levs[c];
-      const uint64_t nz = __ballot(lev != 0 && (cbpt || lane > 0));
-      if (cbpt && !nz) continue;  // CBPEncodeAC: no level, nothing written
-      const Code lc = level_code(T, lane, lev, nz, cbpt);
-      const int dcbits = cbpt ? 0 : 8;
-      if (EMIT) {
-        const int b0 = (int)(off - sbase) + bits;
-        if (!cbpt && lane == 0) {  // EncodeDC codec.c:343-352
-          const int dc = lev < 1 ? 1 : (lev > 254 ? 254 : lev);
-          put_bits(seg, b0, Code{(uint32_t)(dc == 128 ? 255 : dc), 8});
-        }
-        const int pre = wave_excl_scan(lc.len, lane);
-        put_bits(seg, b0 + dcbits + pre, lc);
-        const int tot = __shfl(pre + lc.len, 63);
-        if (lane == 0) put_bits(seg, b0 + dcbits + tot, tab(T, T_EOB));
-        bits += dcbits + tot + 2;
+  for (int sp = 0; sp < 64; sp++) {
+    if (!cbpt && sp == 0) continue;
+    const int l = (int)(int16_t)((lv[sp >> 1] >> (16 * (sp & 1))) & 0xffffu);
+    if (l != 0) {
+      const int al = l < 0 ? -l : l;
+      uint32_t v;
+      int n;
+      if (first && run == 0 && al == 1) {
+        const Code f = tab(T, T_FIRST01);
+        v = (f.v << 1) | (uint32_t)(l < 0);
+        n = f.len + 1;
       } else {
-        bits += dcbits + wave_sum_i(lc.len) + 2;
+        const Code e = (run < 27 && al < 16) ? tab(T, T_TC + run * 16 + al) : Code{0u, 0};
+        if (e.len) {
+          v = (e.v << 1) | (uint32_t)(l < 0);
+          n = e.len + 1;
+        } else {  // ESCAPE, 6-bit run, 8-bit level
+          const Code esc = tab(T, T_ESC);
+          v = (esc.v << 14) | ((uint32_t)run << 8) | ((uint32_t)l & 0xffu);
+          n = esc.len + 14;
+        }
       }
+      if (EMIT) bw.put(v, n);
+      bits += n;
+      first = false;
+      any = true;
+      run = 0;
+    } else {
+      run++;
     }
   }
-  return bits;
+  if (cbpt && !any) return 0;
+  const Code eob = tab(T, T_EOB);
+  if (EMIT) bw.put(eob.v, eob.len);
+  return bits + eob.len;
 }
 
+// Lane-per-block entropy coding: a wave takes 10 raster macroblocks, lane
+// 6m + b block b of the m-th (the encoder's layout), lane b = 0 also the MB
+// header (and the GOB / picture header before MDU 0 / GOB 0).  Every lane
+// runs its own block's scan serially (no cross-lane step per code), with the
+// block's 64 levels in registers (8 x 16-byte loads; none for blocks the
+// record leaves uncoded).
+//   count (EMIT false): header and block bits into blk_bits, the MB's total
+//     into mb_bits[stream position]
+//   emit  (EMIT true):  each block's codes from its bit offset: the MB's
+//     offset (k_vlc_scan) + its header + the blocks before it
 template <bool EMIT>
-__global__ __launch_bounds__(64 * VLC_WAVES) void k_vlc_mb(VlcArgs a, VlcTables Tg) {
+__global__ __launch_bounds__(64 * VLC_WAVES) void k_vlc_blk(VlcArgs a, VlcTables Tg) {
   __shared__ VlcTables T;  // per-lane table lookups from LDS, loaded once per workgroup
-  __shared__ uint32_t segs[VLC_WAVES][SEG_WORDS + 2];
   for (int i = threadIdx.x; i < T_N; i += 64 * VLC_WAVES) T.t[i] = Tg.t[i];
   __syncthreads();
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int fi = blockIdx.y;
-  const int j0 = (blockIdx.x * VLC_WAVES + wv) * VLC_MBS;
-  uint32_t *seg = segs[wv];
-  const size_t base = (size_t)fi * a.nmb;
+  const int mb0 = (blockIdx.x * VLC_WAVES + wv) * VLC_MBS;
+  if (mb0 >= a.nmb) return;  // whole wave (after the only barrier)
   if (EMIT && a.bits[fi] == 0xFFFFFFFFu) return;  // invalid record or no room: nothing written
-  uint32_t *out = a.out + (size_t)fi * a.out_words;
-  for (int j = j0; j < min(j0 + VLC_MBS, a.nmb); j++) {
-    if (EMIT)
-      for (int i = lane; i < SEG_WORDS + 2; i += 64) seg[i] = 0;
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    int64_t s0 = 0;
-    const int bits = code_mb<EMIT>(T, a, fi, j, lane, seg, &s0);
-    if (!EMIT) {
-      if (lane == 0) a.mb_bits[base + j] = bits < 0 ? 0x80000000u : (uint32_t)bits;
-      continue;
+  const int l = min(lane, 6 * VLC_MBS - 1), b = l % 6;
+  const int k = min(mb0 + l / 6, a.nmb - 1);  // raster MB (tail lanes repeat the last)
+  const bool act = lane < 6 * VLC_MBS && mb0 + l / 6 < a.nmb;
+  const size_t base = (size_t)fi * a.nmb;
+  const p64_mb_rec r = a.mb[base + k];
+  const int j = stream_pos(a.format, k), g = j / 33, m = j - g * 33;
+  const p64_mb_rec rp = a.mb[base + (m % 11 ? k - 1 : k)];  // MVD predictor (same GOB row)
+  const int mq = a.mquant ? (int)a.mquant[base + k] : 0;
+  const int mt = r.mtype;
+  const bool valid = mt >= 0 && mt <= 9;
+  const bool cbpt = valid && mt_cbp(mt);
+  const int cbp = cbpt ? r.cbp : 0x3f;
+  const bool coded = act && valid && mt_tc(mt) && ((cbp >> (5 - b)) & 1);
+  uint32_t lv[32];
+  {
+    const __amdgpu_buffer_rsrc_t cr = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)a.coef, (short)0, (int)min((size_t)a.nframes * a.nmb * 768, (size_t)0x7fffffff), 0x00020000);
+    const uint32_t co = coded ? (uint32_t)(((base + k) * 6 + b) * 128) : 0x80000000u;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      const auto v = __builtin_amdgcn_raw_buffer_load_b128(cr, co + 16 * i, 0, 0);
+      lv[4 * i] = v[0];
+      lv[4 * i + 1] = v[1];
+      lv[4 * i + 2] = v[2];
+      lv[4 * i + 3] = v[3];
     }
-    // copy the segment out: words strictly inside it are this wave's alone; the
-    // first and last word are shared with the neighbouring segments
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    const int64_t w0 = s0 >> 5, w1 = ((int64_t)a.mb_off[base + j] + bits - 1) >> 5;
-    for (int64_t w = w0 + lane; w <= w1; w += 64) {
-      const uint32_t v = seg[w - w0];
-      if (w == w0 || w == w1)
-        atomicOr(out + w, v);
-      else
-        out[w] = v;
+  }
+  BitWriter bw;
+  uint32_t *out = a.out + (size_t)fi * a.out_words;
+  if (!EMIT) {
+    const Header hd = header_codes(T, r, rp, mq, m);
+    int bb = coded ? block_codes<false>(T, lv, cbpt, bw) + (cbpt ? 0 : 8) : 0;  // (intra: + DC)
+    // the MB's six lanes: header and block bits into blk_bits, the total
+    uint16_t *bk = a.blk_bits + (base + k) * 8;
+    if (act) bk[1 + b] = (uint16_t)bb;
+    if (act && b == 0) bk[0] = (uint16_t)hd.bits;
+    int tot = bb;
+#pragma unroll
+    for (int d = 1; d < 6; d++) tot += __shfl(bb, min(lane + d, 63));
+    if (act && b == 0) a.mb_bits[base + j] = hd.bad ? 0x80000000u : (uint32_t)(hd.bits + tot);
+  } else {
+    if (!act) return;
+    // (8-byte loads: blk_bits is 8-byte aligned, 2 nframes nmb words into scratch)
+    const uint2 *bp = reinterpret_cast<const uint2 *>(a.blk_bits + (base + k) * 8);
+    const uint2 b01 = bp[0], b23 = bp[1];
+    const uint32_t bw4[4] = {b01.x, b01.y, b23.x, b23.y};
+    const uint16_t *bh = reinterpret_cast<const uint16_t *>(bw4);
+    int64_t pos = (int64_t)a.mb_off[base + j] + bh[0];
+#pragma unroll
+    for (int d = 0; d < 5; d++) pos += d < b ? bh[1 + d] : 0;
+    if (b == 0) {  // headers: picture (MDU 0 of GOB 0), GOB (MDU 0), MB
+      const int64_t off = a.mb_off[base + j];
+      const Header hd = header_codes(T, r, rp, mq, m);
+      const int64_t s0 = j == 0 ? (a.phase ? a.phase[fi] : 0) : (m == 0 ? off - 26 : off);
+      bw.start(out, s0);
+      if (j == 0) {  // WritePictureHeader marker.c:103-135
+        bw.put(0x10u, 20);
+        bw.put((uint32_t)a.tr[fi] & 31u, 5);
+        bw.put(a.format == P64S_QCIF ? 0u : 4u, 6);
+        if (a.format == P64S_NTSC) bw.put(0x18cu, 9);  // PEI 1, PSPARE 0x8c
+        bw.put(0u, 1);                                   // PEI 0
+      }
+      if (m == 0) {  // WriteGOBHeader marker.c:171-198
+        const uint32_t gn = a.format == P64S_QCIF ? 2 * g + 1 : g + 1;
+        bw.put((1u << 10) | (gn << 6) | ((a.gquant[(size_t)fi * a.ngob + g] & 31u) << 1), 26);
+      }
+#pragma unroll
+      for (int i = 0; i < 6; i++)
+        if (hd.c[i].len) bw.put(hd.c[i].v, hd.c[i].len);
+      bw.finish();
+    }
+    if (coded) {
+      bw.start(out, pos);
+      if (!cbpt) {  // EncodeDC codec.c:343-352
+        const int dc0 = (int)(int16_t)(lv[0] & 0xffffu);
+        const int dc = dc0 < 1 ? 1 : (dc0 > 254 ? 254 : dc0);
+        bw.put((uint32_t)(dc == 128 ? 255 : dc), 8);
+      }
+      block_codes<true>(T, lv, cbpt, bw);
+      bw.finish();
     }
   }
 }
@@ -357,9 +406,10 @@ int p64gpu_vlc_pictures(const p64gpu_vlc_args *x, void *stream) {
   hipStream_t st = (hipStream_t)stream;
   const dim3 grid((unsigned)((a.nmb + VLC_WAVES * VLC_MBS - 1) / (VLC_WAVES * VLC_MBS)),
                   (unsigned)a.nframes);
-  hipLaunchKernelGGL(k_vlc_mb<false>, grid, dim3(64 * VLC_WAVES), 0, st, a, g_tab);
+  a.blk_bits = reinterpret_cast<uint16_t *>(x->scratch + 2 * (size_t)x->nframes * a.nmb);
+  hipLaunchKernelGGL(k_vlc_blk<false>, grid, dim3(64 * VLC_WAVES), 0, st, a, g_tab);
   hipLaunchKernelGGL(k_vlc_scan, dim3((unsigned)a.nframes), dim3(64), 0, st, a);
-  hipLaunchKernelGGL(k_vlc_mb<true>, grid, dim3(64 * VLC_WAVES), 0, st, a, g_tab);
+  hipLaunchKernelGGL(k_vlc_blk<true>, grid, dim3(64 * VLC_WAVES), 0, st, a, g_tab);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return p64gpu_fail_(P64GPU_E_HIP, hipGetErrorString(e));
   return P64GPU_OK;

@@ -386,7 +386,7 @@ def vlc_buffers(n: int, width: int, height: int):
     stride = (int(lib().p64gpu_vlc_max_bytes(width, height)) + 3) // 4 * 4
     return (torch.empty((n, stride), dtype=torch.uint8, device="cuda"),
             torch.empty(n, dtype=torch.int32, device="cuda"),
-            torch.empty(2 * n * nmb, dtype=torch.int32, device="cuda"))
+            torch.empty(6 * n * nmb, dtype=torch.int32, device="cuda"))
 
 
 def vlc_pictures(mb, coef, gquant, tr, *, width: int, height: int, phase=None, mquant=None,
@@ -409,7 +409,7 @@ def vlc_pictures(mb, coef, gquant, tr, *, width: int, height: int, phase=None, m
         raise P64GpuError("vlc_pictures: buffer sizes do not match the picture format")
     out, bits, scratch = buffers if buffers is not None else vlc_buffers(n, width, height)
     stride = int(out.shape[1])
-    if out.shape[0] < n or bits.numel() < n or scratch.numel() < 2 * n * nmb or \
+    if out.shape[0] < n or bits.numel() < n or scratch.numel() < 6 * n * nmb or \
             stride < int(L.p64gpu_vlc_max_bytes(width, height)):
         raise P64GpuError("vlc_pictures: buffers smaller than the batch")
     a = VlcArgs(width=width, height=height, nframes=n, reserved=0, mb=mb.data_ptr(),
