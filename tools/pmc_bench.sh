@@ -20,7 +20,7 @@ run() {  # tag, program args...
   done
   echo "pmc $tag done"
 }
-B="$R/bench.py --steps 10 --warmup 2 --no-cpu --no-verify --no-vlc --eager"
+B="$R/bench.py --steps 10 --warmup 2 --no-cpu --no-verify --no-vlc --eager --spinup-ms 0"
 for t in calib synth noise pan15 flat; do mkdir -p $OUT/$t; done
 run calib $R/tools/ubench_valu new
 run synth python3 $B
