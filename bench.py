@@ -1045,7 +1045,8 @@ def run_intra(args, torch, dist, np, p64_amd, world, frames, S, nmb, pic, nslots
             "config": {"workload": f"{w}x{h} intra pictures, q={args.quant}, content {args.content}, "
                                    f"{S} pictures/step/GPU", "macroblocks_per_step_per_gpu": mbs,
                        "distinct_input_pictures": nslots},
-            "roofline": roofline(mbs * INTRA_BYTES_PER_MB, kavg, "k_intra_mbg<false>",
+            "roofline": roofline(mbs * INTRA_BYTES_PER_MB, kavg,
+                                 "k_intra_mbg<false, %s>" % ("false" if args.quant >= 5 else "true"),
                                  load_pmc(args.pmc_json, key),
                                  algorithmic_bytes_per_mb=INTRA_BYTES_PER_MB, timing=timing_note(args)),
             "valu_busy": (load_pmc(args.pmc_json, key) or {}).get("valu_busy"),
