@@ -124,6 +124,24 @@ __device__ __forceinline__ int dot2(s16x2 a, short ca, short cb) {
   asm("v_dot2_i32_i16 %0, %1, %2, 0" : "=v"(r) : "v"(a), "s"(c));
   return r;
 }
+// the same with a VGPR accumulator (acc + C_a x + C_b y in one instruction)
+__device__ __forceinline__ int dot2acc(s16x2 a, short ca, short cb, int acc) {
+  const uint32_t c = (uint32_t)(uint16_t)ca | ((uint32_t)(uint16_t)cb << 16);
+  int r;
+  asm("v_dot2_i32_i16 %0, %1, %2, %3" : "=v"(r) : "v"(a), "s"(c), "v"(acc));
+  return r;
+}
+// (ms9(A), ms9(B)) as one int16 pair when A = 2a, B = 2b are given with halved
+// constants: floor(a / 512) = floor(A / 256) = A >> 8, whose low 16 bits are
+// bytes 1 and 2 of A -- one v_perm instead of two shifts and a v_bfi.  The
+// constants of the forward column pass (4 C_k; the odd part's C_k1D16..C7D16,
+// all even) and C1D4 halve exactly, so the halved products are the same
+// rationals.
+__device__ __forceinline__ s16x2 pk_ms8(int A, int B) {
+  return __builtin_bit_cast(s16x2, __builtin_amdgcn_perm((uint32_t)B, (uint32_t)A, 0x06050201u));
+}
+static_assert(C1D4 % 2 == 0 && C1D16 % 2 == 0 && C3D16 % 2 == 0 && C5D16 % 2 == 0 && C7D16 % 2 == 0,
+              "halved constants");
 // row pass of one row given as (x0,x1), (x2,x3), (x4,x5), (x6,x7)
 __device__ __forceinline__ void fwd_row_pk(const s16x2 p[4], int o[8]) {
   const s16x2 s01 = (p[0] + p[3].yx) >> 1, s23 = (p[1] + p[2].yx) >> 1;  // (s0,s1) (s2,s3)
@@ -134,9 +152,8 @@ __device__ __forceinline__ void fwd_row_pk(const s16x2 p[4], int o[8]) {
   o[2] = ms9(dot2(e32, C1D8, C3D8));   // C3D8 e2 + C1D8 e3
   o[6] = ms9(dot2(e32, C3D8, -C1D8));  // C3D8 e3 - C1D8 e2
   const s16x2 q = __builtin_shufflevector(d01, d23, 1, 2);   // (d1, d2)
-  const int r1 = ms9(dot2(q, C1D4, C1D4)), r0 = ms9(dot2(q, C1D4, -C1D4));
   const s16x2 dd = __builtin_shufflevector(d23, d01, 1, 2);  // (d3, d0)
-  const s16x2 rr = pk16(r0, r1);
+  const s16x2 rr = pk_ms8(dot2(q, C1D4 / 2, -C1D4 / 2), dot2(q, C1D4 / 2, C1D4 / 2));  // (r0, r1)
   const s16x2 u03 = dd + rr, u12 = dd - rr;                   // (u0,u3) (u1,u2)
   o[1] = ms9(dot2(u03, C7D16, C1D16));
   o[7] = ms9(dot2(u03, -C1D16, C7D16));
@@ -150,23 +167,24 @@ __device__ __forceinline__ void fwd_row_pk(const s16x2 p[4], int o[8]) {
 // for d0, d3, which are added to products and shift themselves.  Pixel or
 // residual input (|x| <= 255): sums <= 1,020, u = 4d + r <= 2,462, every
 // intermediate inside int16; the products and their sums exact in 32 bits.
+// The outputs are left as 2 x the pre-shift sums (halved constants, A above):
+// the caller packs two columns' outputs with pk_ms8.
 __device__ __forceinline__ void fwd_col_pk(const s16x2 p[4], int o[8]) {
   const s16x2 s01 = p[0] + p[3].yx, s23 = p[1] + p[2].yx;  // (s0,s1) (s2,s3)
   const s16x2 d01 = p[0] - p[3].yx, d23 = p[1] - p[2].yx;  // (d0,d1) (d2,d3)
   const s16x2 e01 = s01 + s23.yx, e32 = s01 - s23.yx;      // (e0,e1) (e3,e2)
-  o[0] = ms9(dot2(e01, 4 * C1D4, 4 * C1D4));
-  o[4] = ms9(dot2(e01, 4 * C1D4, -4 * C1D4));
-  o[2] = ms9(dot2(e32, 4 * C1D8, 4 * C3D8));   // 4 C3D8 e2 + 4 C1D8 e3
-  o[6] = ms9(dot2(e32, 4 * C3D8, -4 * C1D8));  // 4 C3D8 e3 - 4 C1D8 e2
+  o[0] = dot2(e01, 2 * C1D4, 2 * C1D4);
+  o[4] = dot2(e01, 2 * C1D4, -2 * C1D4);
+  o[2] = dot2(e32, 2 * C1D8, 2 * C3D8);   // (4 C3D8 e2 + 4 C1D8 e3) / 2
+  o[6] = dot2(e32, 2 * C3D8, -2 * C1D8);  // (4 C3D8 e3 - 4 C1D8 e2) / 2
   const s16x2 q = __builtin_shufflevector(d01, d23, 1, 2);  // (d1, d2)
-  const int r1 = ms9(dot2(q, 4 * C1D4, 4 * C1D4)), r0 = ms9(dot2(q, 4 * C1D4, -4 * C1D4));
+  const s16x2 rr = pk_ms8(dot2(q, 2 * C1D4, -2 * C1D4), dot2(q, 2 * C1D4, 2 * C1D4));  // (r0, r1)
   const s16x2 dd = __builtin_shufflevector(d23, d01, 1, 2) << 2;  // (4 d3, 4 d0)
-  const s16x2 rr = pk16(r0, r1);
   const s16x2 u03 = dd + rr, u12 = dd - rr;  // (u0,u3) (u1,u2)
-  o[1] = ms9(dot2(u03, C7D16, C1D16));
-  o[7] = ms9(dot2(u03, -C1D16, C7D16));
-  o[3] = ms9(dot2(u12, -C5D16, C3D16));
-  o[5] = ms9(dot2(u12, C3D16, C5D16));
+  o[1] = dot2(u03, C7D16 / 2, C1D16 / 2);
+  o[7] = dot2(u03, -C1D16 / 2, C7D16 / 2);
+  o[3] = dot2(u12, -C5D16 / 2, C3D16 / 2);
+  o[5] = dot2(u12, C3D16 / 2, C5D16 / 2);
 }
 // byte b of w0 and of w1 zero-extended into the two int16 halves
 __device__ __forceinline__ s16x2 byte_pair(uint32_t w1, uint32_t w0, int b) {
@@ -198,7 +216,7 @@ __device__ __forceinline__ void fdct_block_pk(const uint2 rows[8], int v[64], co
     fwd_col_pk(x, o);
     fwd_col_pk(y, u);
 #pragma unroll
-    for (int k = 0; k < 8; k++) p[k][c >> 1] = pk16(o[k], u[k]);
+    for (int k = 0; k < 8; k++) p[k][c >> 1] = pk_ms8(o[k], u[k]);
     SCHED_FENCE();
   }
 #pragma unroll
@@ -224,11 +242,23 @@ __device__ __forceinline__ uint32_t sat4(const int x[4]) {
   asm("v_sat_pk_u8_i16 %0, %1" : "=v"(s23) : "v"(p23));
   return __builtin_amdgcn_perm(s23, s01, 0x05040100u);
 }
-__device__ __forceinline__ uint2 final_clamp_pack8(const int o[8]) {
-  int x[8];
-#pragma unroll
-  for (int k = 0; k < 8; k++) x[k] = (o[k] + 8) >> 4;
-  return make_uint2(sat4(x), sat4(x + 4));
+// The same from o8 = o + 8 (the +8 folded into the row pass): the pairs
+// saturated to int16 first (v_cvt_pk_i16_i32), then >> 4 in packed 16-bit
+// arithmetic and v_sat_pk_u8_i16: 16 instructions a row instead of 26.  The
+// saturation changes nothing: o8 > 32,767 gives >= 2,047 and o8 < -32,768
+// gives <= -2,048 either way, both clamped to 255 / 0 after.
+__device__ __forceinline__ uint32_t sat4_shr4(const int x[4]) {
+  uint32_t p01, p23, s01, s23;
+  asm("v_cvt_pk_i16_i32 %0, %1, %2" : "=v"(p01) : "v"(x[0]), "v"(x[1]));
+  asm("v_cvt_pk_i16_i32 %0, %1, %2" : "=v"(p23) : "v"(x[2]), "v"(x[3]));
+  const s16x2 h01 = __builtin_bit_cast(s16x2, p01) >> (s16x2){4, 4};
+  const s16x2 h23 = __builtin_bit_cast(s16x2, p23) >> (s16x2){4, 4};
+  asm("v_sat_pk_u8_i16 %0, %1" : "=v"(s01) : "v"(h01));
+  asm("v_sat_pk_u8_i16 %0, %1" : "=v"(s23) : "v"(h23));
+  return __builtin_amdgcn_perm(s23, s01, 0x05040100u);
+}
+__device__ __forceinline__ uint2 final_clamp_pack8_o8(const int o8[8]) {
+  return make_uint2(sat4_shr4(o8), sat4_shr4(o8 + 4));
 }
 // ICCITTFlatQuantize + ChenIDct + BoundIDctMatrix of an intra block from its
 // levels (natural order in v; the DC dequantised as DC x 8): the dequantiser
@@ -288,9 +318,13 @@ __device__ __forceinline__ void iq_idct_cols(PairFn pair, uint32_t q2, uint32_t 
 // 1,054, DC <= 254 x 8 = 2,032), which bounds the column-pass outputs by
 // 25,062 (every sign pattern at those magnitudes) < 2^15; a decoder or an
 // inter residual may exceed that (up to 167,072), so only here.
+// The final rounding's +8 rides in the accumulators of q0 and q1 (8 x 512:
+// ms9(x + 4,096) = ms9(x) + 8, and every output is e_i +- f with e_i built
+// from q0 or q1), then final_clamp_pack8_o8.
 __device__ __forceinline__ void iq_idct_intra_rec(int v[64], int q, uint2 rec[8]) {
   const uint32_t q2 = 0x20002u * (uint32_t)q, qq = 0x10001u * (uint32_t)(q - (int)!(q & 1));
   iq_idct_cols([&](int e, int f) { return pk2(v[e], v[f]); }, q2, qq, true, v[0] * 8, v);
+  const int r8 = opaque(8 << 9);  // one VGPR for every row (not rematerialised per use)
 #pragma unroll
   for (int r = 0; r < 8; r++) {
     const int *x = v + 8 * r;
@@ -298,13 +332,13 @@ __device__ __forceinline__ void iq_idct_intra_rec(int v[64], int q, uint2 rec[8]
     const s16x2 a53 = __builtin_bit_cast(s16x2, pk2(x[5], x[3])), a26 = __builtin_bit_cast(s16x2, pk2(x[2], x[6]));
     const int p0 = ms9(dot2(a17, C7D16, -C1D16)), p3 = ms9(dot2(a17, C1D16, C7D16));
     const int p1 = ms9(dot2(a53, C3D16, -C5D16)), p2 = ms9(dot2(a53, C5D16, C3D16));
-    const int q0 = ms9(dot2(a04, C1D4, C1D4)), q1 = ms9(dot2(a04, C1D4, -C1D4));
+    const int q0 = ms9(dot2acc(a04, C1D4, C1D4, r8)), q1 = ms9(dot2acc(a04, C1D4, -C1D4, r8));
     const int q2_ = ms9(dot2(a26, C3D8, -C1D8)), q3 = ms9(dot2(a26, C1D8, C3D8));
     const int e0 = q0 + q3, e1 = q1 + q2_, e2 = q1 - q2_, e3 = q0 - q3;
     const int f0 = p0 + p1, f1 = p0 - p1, f2 = p3 - p2, f3 = p3 + p2;
     const int g1 = ms9(kmul<true>(C1D4, f2 - f1)), g2 = ms9(kmul<true>(C1D4, f2 + f1));
-    const int o[8] = {e0 + f3, e1 + g2, e2 + g1, e3 + f0, e3 - f0, e2 - g1, e1 - g2, e0 - f3};
-    rec[r] = final_clamp_pack8(o);
+    const int o8[8] = {e0 + f3, e1 + g2, e2 + g1, e3 + f0, e3 - f0, e2 - g1, e1 - g2, e0 - f3};
+    rec[r] = final_clamp_pack8_o8(o8);
     SCHED_FENCE();
   }
 }
