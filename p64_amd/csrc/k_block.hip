@@ -195,9 +195,9 @@ __device__ __forceinline__ s16x2 byte_pair(uint32_t w1, uint32_t w0, int b) {
 // shifted coefficients until quantisation -- 64 extra VGPRs.  The opaque copy
 // ends X's life at the shift.)
 // RES: the input is the residual rows - prow (both packed pixel rows)
+// column pass: p[row][column pair]
 template <bool RES = false>
-__device__ __forceinline__ void fdct_block_pk(const uint2 rows[8], int v[64], const uint2 *prow = nullptr) {
-  s16x2 p[8][4];  // [row][column pair]
+__device__ __forceinline__ void fdct_cols_pk(const uint2 rows[8], s16x2 p[8][4], const uint2 *prow = nullptr) {
 #pragma unroll
   for (int c = 0; c < 8; c += 2) {
     s16x2 x[4], y[4];  // columns c and c + 1 as row pairs
@@ -219,6 +219,11 @@ __device__ __forceinline__ void fdct_block_pk(const uint2 rows[8], int v[64], co
     for (int k = 0; k < 8; k++) p[k][c >> 1] = pk_ms8(o[k], u[k]);
     SCHED_FENCE();
   }
+}
+template <bool RES = false>
+__device__ __forceinline__ void fdct_block_pk(const uint2 rows[8], int v[64], const uint2 *prow = nullptr) {
+  s16x2 p[8][4];  // [row][column pair]
+  fdct_cols_pk<RES>(rows, p, prow);
 #pragma unroll
   for (int r = 0; r < 8; r++) {
     fwd_row_pk(p[r], v + 8 * r);
@@ -964,37 +969,55 @@ __global__ __launch_bounds__(64) OCC4 void k_inter_mbg(p64gpu_encode_args a, Blk
   const p64_qint qt = c_qint.ac[q], qd = c_qint.dc[q];
   // levels & tcm: 0 when the MB type carries no coefficients (through an
   // opaque mask: as a select hipcc branches around every quantisation)
-  const int tcm = opaque(tc ? -1 : 0);
-  int v[64];
-  fdct_block_pk<true>(f.rows, v, prow);
-  // quantise in scan order into the LDS staging (levels of a block whose MB
-  // type carries no coefficients are 0); Σ l^2 for the CBP decision:
-  // Σ|l| > 1 <=> Σ l^2 > 1 and Σ|l| > 0 <=> Σ l^2 > 0 for integers
+  const uint32_t tcm = (uint32_t)opaque(tc ? -1 : 0);
+  // ChenDct of the residual, each row quantised right after its row pass and
+  // kept as natural int16 level pairs L[r][j] = (x_r,2j, x_r,2j+1): 32
+  // registers instead of 64 ints for the levels
+  uint32_t L[8][4];
+  {
+    s16x2 p[8][4];
+    fdct_cols_pk<true>(f.rows, p, prow);
+#pragma unroll
+    for (int r = 0; r < 8; r++) {
+      int o[8];
+      fwd_row_pk(p[r], o);
+#pragma unroll
+      for (int k = 0; k < 8; k++) o[k] = opaque(o[k]);
+      int l[8];
+#pragma unroll
+      for (int k = 0; k < 8; k++) {
+        if (r == 0 && k == 0)  // DC: intra (DC +- 4) / 8 in 1..254, inter as AC with DC bounds
+          l[k] = intra ? clampi(dct_final(min(dct_final(o[0]), 2047)), 1, 254) : qlevel_int(o[0], qd);
+        else
+          l[k] = qlevel_int(o[k], qt);
+      }
+#pragma unroll
+      for (int j = 0; j < 4; j++) L[r][j] = pk2(l[2 * j], l[2 * j + 1]);
+      SCHED_FENCE();
+    }
+  }
+  // natural positions e (low half) and f (high half) as one pair
+  auto lpair = [&](int e, int f) {
+    const uint32_t sel = (uint32_t)(2 * (e & 1)) | ((uint32_t)(2 * (e & 1) + 1) << 8) |
+                         ((uint32_t)(4 + 2 * (f & 1)) << 16) | ((uint32_t)(5 + 2 * (f & 1)) << 24);
+    return __builtin_amdgcn_perm(L[f >> 3][(f & 7) >> 1], L[e >> 3][(e & 7) >> 1], sel);
+  };
+  // in scan order into the LDS staging (levels of a block whose MB type
+  // carries no coefficients are 0); sum of l^2 for the CBP decision:
+  // sum|l| > 1 <=> sum l^2 > 1 and sum|l| > 0 <=> sum l^2 > 0 for integers
   int ss = 0;
 #pragma unroll
   for (int k = 0; k < 8; k++) {
     uint32_t pk[4];
 #pragma unroll
     for (int j = 0; j < 4; j++) {
-      int l2[2];
-#pragma unroll
-      for (int i = 0; i < 2; i++) {
-        const int e = k_zz.inv[8 * k + 2 * j + i];
-        if (e == 0)  // DC: intra (DC +- 4) / 8 in 1..254, inter as AC with DC bounds
-          l2[i] = intra ? clampi(dct_final(min(dct_final(v[0]), 2047)), 1, 254) : qlevel_int(v[0], qd);
-        else
-          l2[i] = qlevel_int(v[e], qt);
-        l2[i] &= tcm;
-      }
-      pk[j] = __builtin_amdgcn_perm((uint32_t)l2[1], (uint32_t)l2[0], 0x05040100u);
+      pk[j] = lpair(k_zz.inv[8 * k + 2 * j], k_zz.inv[8 * k + 2 * j + 1]) & tcm;
       ss = __builtin_amdgcn_sdot2(__builtin_bit_cast(s16x2, pk[j]), __builtin_bit_cast(s16x2, pk[j]), ss, false);
-      v[k_zz.inv[8 * k + 2 * j]] = l2[0];
-      v[k_zz.inv[8 * k + 2 * j + 1]] = l2[1];
     }
     put_levels(lds, lane, k, make_uint4(pk[0], pk[1], pk[2], pk[3]));
     SCHED_FENCE();
   }
-  // CBP (p64.c:887-908): block coded if Σ|l| > 1; none such -> the first
+  // CBP (p64.c:887-908): block coded if sum|l| > 1; none such -> the first
   // block with a nonzero level; no nonzero level at all -> MC without
   // coefficients (MTYPE 4 / 7), vector kept, CBP 0x3f
   const int sh = 6 * (l / 6);
@@ -1011,14 +1034,15 @@ __global__ __launch_bounds__(64) OCC4 void k_inter_mbg(p64gpu_encode_args a, Blk
     }
   }
   const bool ck = mt_tcoeff(mt) && ((cbp >> (5 - b)) & 1);
-  // the levels as natural column pairs (the 64 level registers die here)
+  // the levels as natural column pairs (unmasked: only coded blocks, whose MB
+  // type carries coefficients, use them)
   uint32_t np[8][4];
 #pragma unroll
   for (int c = 0; c < 8; c++) {
-    np[c][0] = pk2(v[c], v[32 + c]);
-    np[c][1] = pk2(v[8 + c], v[56 + c]);
-    np[c][2] = pk2(v[40 + c], v[24 + c]);
-    np[c][3] = pk2(v[16 + c], v[48 + c]);
+    np[c][0] = lpair(c, 32 + c);
+    np[c][1] = lpair(8 + c, 56 + c);
+    np[c][2] = lpair(40 + c, 24 + c);
+    np[c][3] = lpair(16 + c, 48 + c);
   }
   // the levels leave first: the staging then holds idct_coded_blocks' slots
   const uint32_t nvalid = min((unsigned)MBS_PER_WAVE, nmbs - gmb0);
