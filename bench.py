@@ -697,7 +697,7 @@ def main(argv=None):
                 post(t)
 
         # steady-state spin-up (timed_region): the same launches into scratch
-        kme, kin = "k_motion<%d>" % (2 if args.mode == "full" else 1), "k_inter_mbg<false>"
+        kme, kin = "k_motion<%d>" % (2 if args.mode == "full" else 1), "k_inter_mbg<false, false>"
         sp = {}
 
         def spin_init():

@@ -440,11 +440,13 @@ __device__ __forceinline__ void intra_block(const p64gpu_encode_args &a, const I
 // (nvalid MBs x 768 bytes at coef + gmb0 x 768) from the LDS staging, the
 // lane's 8 reconstructed rows (rec_off, plane width pw), and from the record
 // lanes (rl) the MB record dword and the LastIntra byte of MB gmb
-__device__ __forceinline__ void mbg_store_levels(const p64gpu_encode_args &a, const uint8_t *lds, int lane,
-                                                 unsigned nmbs, unsigned gmb0, uint32_t nvalid) {
+// (block form: the wave's blocks g0 .. g0 + nblk - 1 of the launch, 128 bytes
+// of levels each, from lane b's staging)
+__device__ __forceinline__ void blk_store_levels(const p64gpu_encode_args &a, const uint8_t *lds, int lane,
+                                                 unsigned nmbs, unsigned g0, uint32_t nblk) {
   const __amdgpu_buffer_rsrc_t coef =
       __builtin_amdgcn_make_buffer_rsrc((void *)a.coef, (short)0, (int)(nmbs * 768u), BUF_RSRC_W3);
-  const uint32_t nbytes = nvalid * 768u;
+  const uint32_t nbytes = nblk * 128u;
   WAVE_FENCE();  // the staging writes (put_levels, every lane) before these reads
   __builtin_amdgcn_wave_barrier();
 #pragma unroll
@@ -457,10 +459,14 @@ __device__ __forceinline__ void mbg_store_levels(const p64gpu_encode_args &a, co
     d[1] = v.y;
     d[2] = v.z;
     d[3] = v.w;
-    __builtin_amdgcn_raw_buffer_store_b128(d, coef, ob < nbytes ? gmb0 * 768u + ob : BUF_OOB, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b128(d, coef, ob < nbytes ? g0 * 128u + ob : BUF_OOB, 0, 0);
   }
   __builtin_amdgcn_wave_barrier();
   WAVE_FENCE();  // these reads before the staging is reused (idct_coded_blocks' slots)
+}
+__device__ __forceinline__ void mbg_store_levels(const p64gpu_encode_args &a, const uint8_t *lds, int lane,
+                                                 unsigned nmbs, unsigned gmb0, uint32_t nvalid) {
+  blk_store_levels(a, lds, lane, nmbs, 6u * gmb0, 6u * nvalid);
 }
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t recon_rsrc(const p64gpu_encode_args &a, const BlkDiv &kd,
                                                              unsigned nmbs) {
@@ -495,27 +501,33 @@ __device__ __forceinline__ void mbg_store(const p64gpu_encode_args &a, const Blk
   mbg_store_rows(a, kd, nmbs, rec_off, pw, rows, rl, gmb, mbw, li);
 }
 
-// intra picture, MB-grouped block layout (blk_pos_mb): one wave = 10 MBs, a
-// lane per block; levels leave as one contiguous 7,680-byte run per wave
+// intra picture, block layout over all 64 lanes: wave w takes the launch's
+// blocks 64 w .. 64 w + 63 in MB-major order (blk_pos_mb of block g: MB g / 6,
+// block g % 6), so an MB may straddle two waves -- nothing in an intra block
+// looks at its MB's other blocks; levels leave as one contiguous 8-KB run per
+// wave.  (Ten whole MBs per wave, as the inter kernel needs for its CBP
+// ballots, leave lanes 60..63 idle: 6.25% more waves.)
 template <bool QMB, bool CLAMP>
 __global__ __launch_bounds__(64 * MBG_WAVES) void k_intra_mbg(p64gpu_encode_args a, BlkDiv kd, unsigned nmbs) {
   __shared__ __align__(16) uint8_t lvl[MBG_WAVES * LVL_WAVE];
   const int lane = threadIdx.x & 63;
   uint8_t *lds = lvl + (threadIdx.x >> 6) * LVL_WAVE;
-  const unsigned gmb0 = (xcd_remap(blockIdx.x, gridDim.x) * MBG_WAVES + (threadIdx.x >> 6)) * MBS_PER_WAVE;
-  if (gmb0 >= nmbs) return;  // whole wave
+  const unsigned nblk = 6u * nmbs;
+  const unsigned g0 = (xcd_remap(blockIdx.x, gridDim.x) * MBG_WAVES + (threadIdx.x >> 6)) * 64u;
+  if (g0 >= nblk) return;  // whole wave
   PRIO_HIGH();
-  const int l = min(lane, 6 * MBS_PER_WAVE - 1);
-  const unsigned gmb = min(gmb0 + (unsigned)(l / 6), nmbs - 1);  // tail lanes repeat the last MB
-  const IntraFetch f = intra_fetch_at<QMB>(a, blk_pos_mb(gmb, l % 6, a.width, a.height, kd));
+  const unsigned g = min(g0 + (unsigned)lane, nblk - 1);  // tail lanes repeat the last block
+  const unsigned gmb = __umulhi(g, 0xAAAAAAABu) >> 2;      // g / 6
+  const int b = (int)(g - 6u * gmb);
+  const IntraFetch f = intra_fetch_at<QMB>(a, blk_pos_mb(gmb, b, a.width, a.height, kd));
   PRIO_LOW();
   IntraOut o;
-  const uint32_t nvalid = min((unsigned)MBS_PER_WAVE, nmbs - gmb0);
   intra_block<CLAMP>(a, f, lds, lane, o);
   // the MB's record and LastIntra (p64.c:909-910: MTYPE 0, CBP 0x3f, LastIntra
-  // reset) from lane b = 0 of each MB
-  const bool rl = l % 6 == 0 && lane < 6 * MBS_PER_WAVE && gmb0 + (unsigned)(l / 6) < nmbs;
-  mbg_store(a, kd, lds, lane, nmbs, gmb0, nvalid, o.rec_off, o.pw, o.rec, rl, gmb, 0x3f00u, 0);
+  // reset) from the lane of its block 0
+  const bool rl = b == 0 && g0 + (unsigned)lane < nblk;
+  blk_store_levels(a, lds, lane, nmbs, g0, min(64u, nblk - g0));
+  mbg_store_rows(a, kd, nmbs, o.rec_off, o.pw, o.rec, rl, gmb, 0x3f00u, 0);
 }
 // The source of an 8x8 prediction at (x, y) of a plane (any byte alignment):
 // three aligned dwords per row (the third only matters when the row is
@@ -827,22 +839,24 @@ __device__ __forceinline__ void rec_wave_compact(int w, int h, int64_t stride, _
 // LDS free as soon as it ends (with the priority raised first, -1.5 us for
 // the decoder and -1 us for k_inter_mbg); k_intra_mbg keeps four (MBG_WAVES).
 #define OCC4 __attribute__((amdgpu_waves_per_eu(4)))
-// decoder reconstruction, MB-grouped block layout (blk_pos_mb), one block per
-// lane: 10 MBs per wave, each lane loads its MB's record, then its levels and
+// decoder reconstruction, block layout over all 64 lanes (as k_intra_mbg: wave
+// w takes blocks 64 w .. 64 w + 63, an MB may straddle two waves), one block
+// per lane: each lane loads its MB's record, then its levels and
 // prediction; coded blocks go through idct_coded_blocks, then every block
 // stores its rows (reconstruction or prediction) wave-wide.  87 VGPRs: 5 waves per SIMD, which hide each other's two
 // dependent load latencies (eight lanes per block: 80 VGPRs, 6 waves, but two
 // passes per wave instead of one and 1.7 us slower; a persistent
 // variant with the next block's loads in flight needed 237 VGPRs, 2 waves,
-// and was slower).  Lanes past the batch (and lanes 60..63) get coded = 0:
+// and was slower).  Lanes past the batch get coded = 0:
 // every load and store of theirs is out of range.
 __global__ __launch_bounds__(64) OCC4 void k_recon_mbg(int w, int h, int64_t stride, const uint8_t *refp,
                                                            uint8_t *recp, const int16_t *coef,
                                                            const p64_mb_rec *mbr, const uint8_t *quant_mb,
                                                            const uint8_t *coded_mask, BlkDiv kd, unsigned nmbs) {
   const int lane = threadIdx.x & 63;
-  const unsigned gmb0 = xcd_remap(blockIdx.x, gridDim.x) * MBS_PER_WAVE;
-  if (gmb0 >= nmbs) return;  // whole wave
+  const unsigned nblk = 6u * nmbs;
+  const unsigned g0 = xcd_remap(blockIdx.x, gridDim.x) * 64u;  // the wave's first block
+  if (g0 >= nblk) return;  // whole wave
   PRIO_HIGH();
   const int nmb = (w >> 4) * (h >> 4), nfr = (int)mdiv(nmbs, kd.mn, kd.sn);
   RecBufs B;
@@ -853,12 +867,11 @@ __global__ __launch_bounds__(64) OCC4 void k_recon_mbg(int w, int h, int64_t str
   B.mask = __builtin_amdgcn_make_buffer_rsrc((void *)coded_mask, (short)0, nfr * nmb, BUF_RSRC_W3);
   const __amdgpu_buffer_rsrc_t rec =
       __builtin_amdgcn_make_buffer_rsrc((void *)recp, (short)0, (int)(nfr * stride), BUF_RSRC_W3);
-  const int l = min(lane, 6 * MBS_PER_WAVE - 1);
-  const unsigned g = gmb0 + (unsigned)(l / 6);
-  const bool valid = lane < 6 * MBS_PER_WAVE && g < nmbs;
-  const unsigned gmb = min(g, nmbs - 1);
+  const bool valid = g0 + (unsigned)lane < nblk;
+  const unsigned g = min(g0 + (unsigned)lane, nblk - 1);
+  const unsigned gmb = __umulhi(g, 0xAAAAAAABu) >> 2;  // g / 6
   RecStageA A;
-  A.p = blk_pos_mb(gmb, l % 6, w, h, kd);
+  A.p = blk_pos_mb(gmb, (int)(g - 6u * gmb), w, h, kd);
   A.m = __builtin_amdgcn_raw_buffer_load_b32(B.mb, 4 * gmb, 0, 0);
   A.q = __builtin_amdgcn_raw_buffer_load_b8(B.q, gmb, 0, 0);
   A.coded = __builtin_amdgcn_raw_buffer_load_b8(B.mask, valid ? gmb : BUF_OOB, 0, 0);
@@ -908,7 +921,10 @@ __device__ __forceinline__ void pred_rows(const PredSrc &P, bool filter, uint2 p
       prow[r] = make_uint2(align4(P.d[r][1], P.d[r][0], P.sh), align4(P.d[r][2], P.d[r][1], P.sh));
   }
 }
-template <bool QMB>
+// OVR: an -o MTYPE override array is given.  Without one every MTYPE the
+// decision can return (0, 2, 5, 8: decide_mtype) carries coefficients, so
+// the level mask for MC-only types (4, 7) is left out.
+template <bool QMB, bool OVR>
 __global__ __launch_bounds__(64) OCC4 void k_inter_mbg(p64gpu_encode_args a, BlkDiv kd, unsigned nmbs,
                                                              const p64_me_rec *me) {
   __shared__ __align__(16) uint8_t lds[LVL_WAVE];
@@ -944,8 +960,7 @@ __global__ __launch_bounds__(64) OCC4 void k_inter_mbg(p64gpu_encode_args a, Blk
   const __amdgpu_buffer_rsrc_t ovr = __builtin_amdgcn_make_buffer_rsrc(
       (void *)a.mtype_override, (short)0, a.mtype_override ? (int)nmbs : 0, BUF_RSRC_W3);
   const int li = __builtin_amdgcn_raw_buffer_load_b8(lir, gmb, 0, 0);
-  const int ovl = (int)(int8_t)__builtin_amdgcn_raw_buffer_load_b8(ovr, a.mtype_override ? gmb : BUF_OOB, 0, 0);
-  const int ov = a.mtype_override ? ovl : -1;
+  const int ov = OVR ? (int)(int8_t)__builtin_amdgcn_raw_buffer_load_b8(ovr, gmb, 0, 0) : -1;
   const IntraFetch f = intra_fetch_at<QMB>(a, pos);  // current rows, q
 
   // MTYPE (p64.c:734-772): the decision, the -o override, the intra refresh
@@ -969,7 +984,7 @@ __global__ __launch_bounds__(64) OCC4 void k_inter_mbg(p64gpu_encode_args a, Blk
   const p64_qint qt = c_qint.ac[q], qd = c_qint.dc[q];
   // levels & tcm: 0 when the MB type carries no coefficients (through an
   // opaque mask: as a select hipcc branches around every quantisation)
-  const uint32_t tcm = (uint32_t)opaque(tc ? -1 : 0);
+  const uint32_t tcm = OVR ? (uint32_t)opaque(tc ? -1 : 0) : ~0u;
   // ChenDct of the residual, each row quantised right after its row pass and
   // kept as natural int16 level pairs L[r][j] = (x_r,2j, x_r,2j+1): 32
   // registers instead of 64 ints for the levels
@@ -1011,7 +1026,8 @@ __global__ __launch_bounds__(64) OCC4 void k_inter_mbg(p64gpu_encode_args a, Blk
     uint32_t pk[4];
 #pragma unroll
     for (int j = 0; j < 4; j++) {
-      pk[j] = lpair(k_zz.inv[8 * k + 2 * j], k_zz.inv[8 * k + 2 * j + 1]) & tcm;
+      pk[j] = lpair(k_zz.inv[8 * k + 2 * j], k_zz.inv[8 * k + 2 * j + 1]);
+      if (OVR) pk[j] &= tcm;
       ss = __builtin_amdgcn_sdot2(__builtin_bit_cast(s16x2, pk[j]), __builtin_bit_cast(s16x2, pk[j]), ss, false);
     }
     put_levels(lds, lane, k, make_uint4(pk[0], pk[1], pk[2], pk[3]));
@@ -1074,7 +1090,8 @@ static unsigned mbg_workgroups(unsigned nmbs, unsigned per = MBG_WAVES) {
 
 hipError_t intra_mbg(const p64gpu_encode_args &a, hipStream_t st) {
   const unsigned nm = (unsigned)((int64_t)a.nframes * (a.width / 16) * (a.height / 16));
-  const dim3 grid(mbg_workgroups(nm)), block(64 * MBG_WAVES);
+  const unsigned waves = (6u * nm + 63u) / 64u;  // 64 blocks a wave
+  const dim3 grid((waves + MBG_WAVES - 1) / MBG_WAVES), block(64 * MBG_WAVES);
   const BlkDiv kd = blk_div(a.width, a.height);
   if (a.quant_mb)
     hipLaunchKernelGGL((k_intra_mbg<true, true>), grid, block, 0, st, a, kd, nm);
@@ -1087,12 +1104,17 @@ hipError_t intra_mbg(const p64gpu_encode_args &a, hipStream_t st) {
 
 hipError_t inter_mbg(const p64gpu_encode_args &a, const p64_me_rec *me, hipStream_t st) {
   const unsigned nm = (unsigned)((int64_t)a.nframes * (a.width / 16) * (a.height / 16));
-  if (a.quant_mb)
-    hipLaunchKernelGGL(k_inter_mbg<true>, dim3(mbg_workgroups(nm, 1)), dim3(64), 0, st, a,
-                       blk_div(a.width, a.height), nm, me);
+  const dim3 grid(mbg_workgroups(nm, 1)), block(64);
+  const BlkDiv kd = blk_div(a.width, a.height);
+  const bool ovr = a.mtype_override != nullptr;
+  if (a.quant_mb && ovr)
+    hipLaunchKernelGGL((k_inter_mbg<true, true>), grid, block, 0, st, a, kd, nm, me);
+  else if (a.quant_mb)
+    hipLaunchKernelGGL((k_inter_mbg<true, false>), grid, block, 0, st, a, kd, nm, me);
+  else if (ovr)
+    hipLaunchKernelGGL((k_inter_mbg<false, true>), grid, block, 0, st, a, kd, nm, me);
   else
-    hipLaunchKernelGGL(k_inter_mbg<false>, dim3(mbg_workgroups(nm, 1)), dim3(64), 0, st, a,
-                       blk_div(a.width, a.height), nm, me);
+    hipLaunchKernelGGL((k_inter_mbg<false, false>), grid, block, 0, st, a, kd, nm, me);
   return hipGetLastError();
 }
 
@@ -1100,7 +1122,7 @@ hipError_t recon_mbg(int w, int h, int nframes, int64_t stride, const uint8_t *r
                      const int16_t *coef, const p64_mb_rec *mb, const uint8_t *quant_mb,
                      const uint8_t *coded_mask, hipStream_t st) {
   const unsigned nm = (unsigned)((int64_t)nframes * (w / 16) * (h / 16));
-  hipLaunchKernelGGL(k_recon_mbg, dim3(mbg_workgroups(nm, 1)), dim3(64), 0, st, w, h, stride, ref, recon,
+  hipLaunchKernelGGL(k_recon_mbg, dim3((6u * nm + 63u) / 64u), dim3(64), 0, st, w, h, stride, ref, recon,
                      coef, mb, quant_mb, coded_mask, blk_div(w, h), nm);
   return hipGetLastError();
 }
