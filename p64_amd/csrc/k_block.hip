@@ -538,37 +538,45 @@ struct PredSrc {
 };
 // the horizontal taps of the H.261 loop filter ([1 2 1], edge columns x4) of
 // a row as four packed 16-bit pairs (hz_2i, hz_2i+1), each tap sum one byte
-// dot product of the packed source row: at most 4 x 255 = 1,020
+// dot product of the packed source row, biased by 2 in its accumulator (the
+// vertical pass's +8 rounding, spread over its weights 1 + 2 + 1 or 4): at
+// most 4 x 255 + 2 = 1,022
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ void hz_row_pk(const PredSrc &p, int r, u16x2 hz[4]) {
   const uint32_t lo = align4(p.d[r][1], p.d[r][0], p.sh), hi = align4(p.d[r][2], p.d[r][1], p.sh);
   const uint32_t mid = align4(hi, lo, 2);  // pixels 2..5
-  const uint32_t w[8] = {__builtin_amdgcn_udot4(lo, 0x00000004u, 0u, false),
-                         __builtin_amdgcn_udot4(lo, 0x00010201u, 0u, false),
-                         __builtin_amdgcn_udot4(lo, 0x01020100u, 0u, false),
-                         __builtin_amdgcn_udot4(mid, 0x00010201u, 0u, false),
-                         __builtin_amdgcn_udot4(mid, 0x01020100u, 0u, false),
-                         __builtin_amdgcn_udot4(hi, 0x00010201u, 0u, false),
-                         __builtin_amdgcn_udot4(hi, 0x01020100u, 0u, false),
-                         __builtin_amdgcn_udot4(hi, 0x04000000u, 0u, false)};
+  const uint32_t w[8] = {__builtin_amdgcn_udot4(lo, 0x00000004u, 2u, false),
+                         __builtin_amdgcn_udot4(lo, 0x00010201u, 2u, false),
+                         __builtin_amdgcn_udot4(lo, 0x01020100u, 2u, false),
+                         __builtin_amdgcn_udot4(mid, 0x00010201u, 2u, false),
+                         __builtin_amdgcn_udot4(mid, 0x01020100u, 2u, false),
+                         __builtin_amdgcn_udot4(hi, 0x00010201u, 2u, false),
+                         __builtin_amdgcn_udot4(hi, 0x01020100u, 2u, false),
+                         __builtin_amdgcn_udot4(hi, 0x04000000u, 2u, false)};
 #pragma unroll
   for (int i = 0; i < 4; i++) hz[i] = __builtin_bit_cast(u16x2, (w[2 * i + 1] << 16) | w[2 * i]);
 }
 // pred_rows' loop filter in packed 16-bit arithmetic: the vertical
-// [1 2 1] + 8 >> 4 of the tap pairs (at most 4 x 1,020 + 8 = 4,088) as
-// v_pk_ operations, half the registers of the unpacked rows
+// [1 2 1] + 8 >> 4 of the tap pairs (at most 4 x 1,022 = 4,088; the +8 is in
+// the taps' bias) as v_pk_ operations, half the registers of the unpacked
+// rows: edge rows (4 hz + 8) >> 4 = hz' >> 2
 __device__ __forceinline__ void pred_rows_filter_pk(const PredSrc &P, uint2 prow[8]) {
   u16x2 hp[4], hc[4], hn[4];
   hz_row_pk(P, 0, hc);
   hz_row_pk(P, 1, hn);
-  const u16x2 c8 = {8, 8};
 #pragma unroll
   for (int r = 0; r < 8; r++) {
     uint32_t t[4];
 #pragma unroll
     for (int i = 0; i < 4; i++) {
-      const u16x2 v = (r == 0 || r == 7) ? (u16x2)((hc[i] << (u16x2){2, 2}) + c8) >> (u16x2){4, 4}
-                                         : (u16x2)(hp[i] + (hc[i] << (u16x2){1, 1}) + hn[i] + c8) >> (u16x2){4, 4};
+      u16x2 v;
+      if (r == 0 || r == 7) {
+        v = hc[i] >> (u16x2){2, 2};
+      } else {  // 2 hc + hp as one v_pk_mad_u16 (hipcc: a shift and an add)
+        u16x2 m;
+        asm("v_pk_mad_u16 %0, %1, 2, %2 op_sel_hi:[1,0,1]" : "=v"(m) : "v"(hc[i]), "v"(hp[i]));
+        v = (u16x2)(m + hn[i]) >> (u16x2){4, 4};
+      }
       t[i] = __builtin_bit_cast(uint32_t, v);
     }
     prow[r] = make_uint2(__builtin_amdgcn_perm(t[1], t[0], 0x06040200u), __builtin_amdgcn_perm(t[3], t[2], 0x06040200u));
