@@ -97,6 +97,9 @@ __device__ __forceinline__ LumaFetch fetch_luma(const uint8_t *ref_y, const uint
   const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc((void *)ref_y, (short)0, w * h, BUF_RSRC_W3);
   const int base = (y0 - WIN_OY + R0) * w + x0 - WIN_OX;  // (negative above the picture: out of range)
   LumaFetch f;
+  // the current block first: k_motion builds its sub-block map while the
+  // window is still in flight (wait counts are in issue order)
+  f.c = *reinterpret_cast<const uint32_t *>(cur_y + (uint32_t)(mul24(y0 + (lane >> 2), w) + x0 + 4 * (lane & 3)));
 #pragma unroll
   for (int i = 0; i < NIT; i++) {
     const int t = lane + 64 * i, row = t / 3, seg = t - row * 3;
@@ -104,17 +107,20 @@ __device__ __forceinline__ LumaFetch fetch_luma(const uint8_t *ref_y, const uint
     const auto v = __builtin_amdgcn_raw_buffer_load_b128(rr, off, 0, 0);
     f.v[i] = make_uint4(v[0], v[1], v[2], v[3]);
   }
-  f.c = *reinterpret_cast<const uint32_t *>(cur_y + (uint32_t)(mul24(y0 + (lane >> 2), w) + x0 + 4 * (lane & 3)));
   return f;
 }
 template <int R0 = 0, int NR = WIN_ROWS>
-__device__ __forceinline__ void put_luma(MbLds &L, const LumaFetch &f, int lane) {
+__device__ __forceinline__ void put_win(MbLds &L, const LumaFetch &f, int lane) {
   constexpr int SEGS = NR * 3, NIT = (SEGS + 63) / 64;
 #pragma unroll
   for (int i = 0; i < NIT; i++) {
     const int t = lane + 64 * i;
     if (64 * i + 63 < SEGS || t < SEGS) reinterpret_cast<uint4 *>(L.win)[3 * R0 + t] = f.v[i];
   }
+}
+template <int R0 = 0, int NR = WIN_ROWS>
+__device__ __forceinline__ void put_luma(MbLds &L, const LumaFetch &f, int lane) {
+  put_win<R0, NR>(L, f, lane);
   L.cur[lane] = f.c;
 }
 // the rows the SL <= 15 search reads: its candidates' rows 8..36 (dy in
@@ -422,10 +428,16 @@ struct MeLayout {
 using MeLay31 = MeLayout<32, 30, 15, -15>;
 using MeLay15 = MeLayout<16, 14, 4, -7>;
 
-template <class G, class LY>
+// the current block's sub-block averages and their range (cur_lb_map), when
+// the caller built them before the window arrived (k_motion)
+struct CurMap {
+  uint32_t cm[4];
+  int range;
+};
+template <class G, class LY, bool PRE = false>
 __device__ __forceinline__ void me_full(const Sx &S, const uint8_t *cur_blk, int w, int h, int x0,
                                         int y0, int sl, int lane, int &sad0_out, int &mx, int &my,
-                                        int &best) {
+                                        int &best, const CurMap &pre = CurMap{}) {
   constexpr int ND = LY::ND;
   const int q = lane / LY::DXL, dxi = lane % LY::DXL;
   const bool lane_ok = dxi < LY::NDX;
@@ -461,7 +473,14 @@ __device__ __forceinline__ void me_full(const Sx &S, const uint8_t *cur_blk, int
 
   SECTION("cur_map");
   uint32_t cm[4];
-  const int range = uni(cur_lb_map(S, lane, cm));
+  int range;
+  if (PRE) {
+#pragma unroll
+    for (int j = 0; j < 4; j++) cm[j] = pre.cm[j];
+    range = pre.range;
+  } else {
+    range = uni(cur_lb_map(S, lane, cm));
+  }
   int sad0, ehf;
   sad_zero_hf<G>(S, lane, sad0, ehf);
   sad0 = uni(sad0);
@@ -668,15 +687,17 @@ __device__ __forceinline__ void me_stats(const Sx &S, int lane, MeOut &o) {
 }
 
 
-template <class G, int MODE>  // MODE 1 = TSS, 2 = FULL
+template <class G, int MODE, bool PRE = false>  // MODE 1 = TSS, 2 = FULL
 __device__ __forceinline__ MeOut motion_estimate(const Sx &S, const uint8_t *cur_y, int w, int h,
-                                                 int x0, int y0, int sl, int lane) {
+                                                 int x0, int y0, int sl, int lane, const CurMap &pre = CurMap{}) {
   MeOut o;
   if (MODE == 2) {
     if (sl <= 15)  // (uniform: one search limit per launch)
-      me_full<G, MeLay15>(S, cur_y + (size_t)y0 * w + x0, w, h, x0, y0, sl, lane, o.sad0, o.mx, o.my, o.sad);
+      me_full<G, MeLay15, PRE>(S, cur_y + (size_t)y0 * w + x0, w, h, x0, y0, sl, lane, o.sad0, o.mx, o.my,
+                               o.sad, pre);
     else
-      me_full<G, MeLay31>(S, cur_y + (size_t)y0 * w + x0, w, h, x0, y0, sl, lane, o.sad0, o.mx, o.my, o.sad);
+      me_full<G, MeLay31, PRE>(S, cur_y + (size_t)y0 * w + x0, w, h, x0, y0, sl, lane, o.sad0, o.mx, o.my,
+                               o.sad, pre);
   } else {
     o.sad0 = uni(sad_zero<G>(S, lane));
     me_tss<G>(S, w, h, x0, y0, lane, o.sad0, o.mx, o.my, o.sad);
@@ -1043,15 +1064,30 @@ __global__ __launch_bounds__(64, 1) void k_motion(int w, int h, int64_t stride, 
   const unsigned gid = xcd_remap(blockIdx.x, gridDim.x);
   const MbPos ps = mb_pos(gid, nmb, mbw, kd);
   const int fi = ps.fi, x0 = 16 * ps.mbx, y0 = 16 * ps.mby;
-  if (MODE == 2 && sl <= 15)  // (the SL <= 15 layout reads window rows 8..38 only)
-    put_luma<WIN15_R0, WIN15_NR>(
-        L, fetch_luma<WIN15_R0, WIN15_NR>(ref_y + (size_t)fi * stride, cur_y + (size_t)fi * stride, w, h, x0, y0, lane),
-        lane);
-  else
-    put_luma(L, fetch_luma(ref_y + (size_t)fi * stride, cur_y + (size_t)fi * stride, w, h, x0, y0, lane), lane);
+  // FULL: the current block's sub-block map (cur_lb_map) while the window is
+  // in flight, then the window
+  CurMap cmap;
+  auto cur_first = [&](const LumaFetch &f) {
+    L.cur[lane] = f.c;
+    if (MODE == 2) {
+      wsync();
+      cmap.range = uni(cur_lb_map(sx_of(L), lane, cmap.cm));
+    }
+  };
+  if (MODE == 2 && sl <= 15) {  // (the SL <= 15 layout reads window rows 8..38 only)
+    const LumaFetch f = fetch_luma<WIN15_R0, WIN15_NR>(ref_y + (size_t)fi * stride, cur_y + (size_t)fi * stride,
+                                                       w, h, x0, y0, lane);
+    cur_first(f);
+    put_win<WIN15_R0, WIN15_NR>(L, f, lane);
+  } else {
+    const LumaFetch f = fetch_luma(ref_y + (size_t)fi * stride, cur_y + (size_t)fi * stride, w, h, x0, y0, lane);
+    cur_first(f);
+    put_win(L, f, lane);
+  }
   __syncthreads();
   SECTION("m_fetched");
-  const MeOut me = motion_estimate<Geo1, MODE>(sx_of(L), cur_y + (size_t)fi * stride, w, h, x0, y0, sl, lane);
+  const MeOut me = motion_estimate<Geo1, MODE, MODE == 2>(sx_of(L), cur_y + (size_t)fi * stride, w, h, x0, y0,
+                                                          sl, lane, cmap);
   SECTION("m_me_done");
   if (lane == 0) {
     p64_me_rec o;
