@@ -428,40 +428,60 @@ struct MeLayout {
 using MeLay31 = MeLayout<32, 30, 15, -15>;
 using MeLay15 = MeLayout<16, 14, 4, -7>;
 
-// the current block's sub-block averages and their range (cur_lb_map), when
-// the caller built them before the window arrived (k_motion)
+// A lane's candidates and their validity: the search's set-up, which needs
+// only the MB's position (k_motion computes it before its window arrives).
+struct MeSetup {
+  int dx, colb, dy0;
+  bool lane_ok, col_ok, interior;
+  uint32_t inv;
+  unsigned base;
+};
+template <class LY>
+__device__ __forceinline__ MeSetup me_setup(int w, int h, int x0, int y0, int sl, int lane) {
+  constexpr int ND = LY::ND;
+  MeSetup u;
+  const int q = lane / LY::DXL, dxi = lane % LY::DXL;
+  u.lane_ok = dxi < LY::NDX;
+  u.dx = (u.lane_ok ? dxi : LY::NDX - 1) + LY::D0;  // (idle lanes repeat the last column)
+  u.colb = u.dx + WIN_OX;                           // window byte column of dx
+  u.dy0 = LY::D0 + ND * q;                          // dy of the lane's d = 0
+  // Validity (me.c:206-212: range and `< W-16`) is folded into the sums: an
+  // invalid candidate starts at ME_INVALID, so it never survives and never wins.
+  const int hl = sl >> 1;
+  const int px = x0 + u.dx;
+  u.col_ok = u.lane_ok && u.dx >= -hl && u.dx < hl && px >= 0 && px < w - 16;
+  // valid dy: [max(-hl, -y0), min(hl, h-16-y0)), i.e. d in [dlo, dhi) for this group
+  const int dlo = max(-hl, -y0) - u.dy0, dhi = min(hl, h - 16 - y0) - u.dy0;
+  const bool all_rows = dlo <= 0 && dhi >= ND;
+  u.interior = uni(__all(!u.lane_ok || (u.col_ok && all_rows)));
+  // the sums start at 0; invalid candidates are marked afterwards (bit 19 of a
+  // sum < 2^17): interior macroblocks only mask the two idle lanes, the others
+  // OR in the lane's invalid rows, ~valid [dlo, dhi) (or every row)
+  u.inv = 0;
+  if (!u.interior) {
+    const int lo = min(max(dlo, 0), ND), hi = min(max(dhi, 0), ND);
+    u.inv = ~((u.col_ok && hi > lo) ? (1u << hi) - (1u << lo) : 0u);
+  }
+  u.base = ((unsigned)(u.dx + 15) << 5) + (unsigned)(u.dy0 + 15) + 1u;  // ord of d = 0
+  return u;
+}
+// the current block's sub-block averages and their range (cur_lb_map) and the
+// search's set-up, when the caller made them before the window arrived
+// (k_motion)
 struct CurMap {
   uint32_t cm[4];
   int range;
+  MeSetup su;
 };
 template <class G, class LY, bool PRE = false>
 __device__ __forceinline__ void me_full(const Sx &S, const uint8_t *cur_blk, int w, int h, int x0,
                                         int y0, int sl, int lane, int &sad0_out, int &mx, int &my,
                                         int &best, const CurMap &pre = CurMap{}) {
   constexpr int ND = LY::ND;
-  const int q = lane / LY::DXL, dxi = lane % LY::DXL;
-  const bool lane_ok = dxi < LY::NDX;
-  const int dx = (lane_ok ? dxi : LY::NDX - 1) + LY::D0;  // (idle lanes repeat the last column)
-  const int colb = dx + WIN_OX;                            // window byte column of dx
-  const int dy0 = LY::D0 + ND * q;                         // dy of the lane's d = 0
-
-  // Validity (me.c:206-212: range and `< W-16`) is folded into the sums: an
-  // invalid candidate starts at ME_INVALID, so it never survives and never wins.
-  const int hl = sl >> 1;
-  const int px = x0 + dx;
-  const bool col_ok = lane_ok && dx >= -hl && dx < hl && px >= 0 && px < w - 16;
-  // valid dy: [max(-hl, -y0), min(hl, h-16-y0)), i.e. d in [dlo, dhi) for this group
-  const int dlo = max(-hl, -y0) - dy0, dhi = min(hl, h - 16 - y0) - dy0;
-  const bool all_rows = dlo <= 0 && dhi >= ND;
-  const bool interior = uni(__all(!lane_ok || (col_ok && all_rows)));
-  // the sums start at 0; invalid candidates are marked afterwards (bit 19 of a
-  // sum < 2^17): interior macroblocks only mask the two idle lanes, the others
-  // OR in the lane's invalid rows, ~valid [dlo, dhi) (or every row)
-  uint32_t inv = 0;
-  if (!interior) {
-    const int lo = min(max(dlo, 0), ND), hi = min(max(dhi, 0), ND);
-    inv = ~((col_ok && hi > lo) ? (1u << hi) - (1u << lo) : 0u);
-  }
+  const MeSetup su = PRE ? pre.su : me_setup<LY>(w, h, x0, y0, sl, lane);
+  const int colb = su.colb, dy0 = su.dy0;
+  const bool lane_ok = su.lane_ok, interior = su.interior;
+  const uint32_t inv = su.inv;
   auto mark_invalid = [&](uint32_t *a) {
     if (!interior) {
 #pragma unroll
@@ -469,7 +489,7 @@ __device__ __forceinline__ void me_full(const Sx &S, const uint8_t *cur_blk, int
     }
   };
   static_assert(ME_INVALID == 1u << 19, "invalid mark");
-  const unsigned base = ((unsigned)(dx + 15) << 5) + (unsigned)(dy0 + 15) + 1u;  // ord of d = 0
+  const unsigned base = su.base;
 
   SECTION("cur_map");
   uint32_t cm[4];
@@ -1077,10 +1097,12 @@ __global__ __launch_bounds__(64, 1) void k_motion(int w, int h, int64_t stride, 
   if (MODE == 2 && sl <= 15) {  // (the SL <= 15 layout reads window rows 8..38 only)
     const LumaFetch f = fetch_luma<WIN15_R0, WIN15_NR>(ref_y + (size_t)fi * stride, cur_y + (size_t)fi * stride,
                                                        w, h, x0, y0, lane);
+    cmap.su = me_setup<MeLay15>(w, h, x0, y0, sl, lane);
     cur_first(f);
     put_win<WIN15_R0, WIN15_NR>(L, f, lane);
   } else {
     const LumaFetch f = fetch_luma(ref_y + (size_t)fi * stride, cur_y + (size_t)fi * stride, w, h, x0, y0, lane);
+    if (MODE == 2) cmap.su = me_setup<MeLay31>(w, h, x0, y0, sl, lane);
     cur_first(f);
     put_win(L, f, lane);
   }
