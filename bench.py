@@ -561,6 +561,9 @@ def timed_region(torch, dist, world, steps, t_first, launch, pre=None, post=None
                 f"(P64GPU_FLAG_ME_GIVEN); {first} = the difference")
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
           for _ in range(1 if graph else steps)]
+    if os.environ.get("P64_BENCH_PREPROBE"):  # (experiment) one short kernel + sync before the region
+        torch.cuda.synchronize()
+        p64_amd.clock_probe(5)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
