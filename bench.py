@@ -561,9 +561,13 @@ def timed_region(torch, dist, world, steps, t_first, launch, pre=None, post=None
                 f"(P64GPU_FLAG_ME_GIVEN); {first} = the difference")
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
           for _ in range(1 if graph else steps)]
-    if os.environ.get("P64_BENCH_PREPROBE"):  # (experiment) one short kernel + sync before the region
-        torch.cuda.synchronize()
-        p64_amd.clock_probe(5)
+    # torch creates an event's HIP event at its first record(): recorded once
+    # here, so that creation (~100 us of host time the first time in a process,
+    # measured as the intra line's 45.2 vs 38.0 us per step) is not inside the
+    # timed region
+    for a, b in ev:
+        a.record()
+        b.record()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
