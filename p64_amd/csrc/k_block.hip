@@ -326,15 +326,66 @@ __device__ __forceinline__ void iq_idct_cols(PairFn pair, uint32_t q2, uint32_t 
 // The final rounding's +8 rides in the accumulators of q0 and q1 (8 x 512:
 // ms9(x + 4,096) = ms9(x) + 8, and every output is e_i +- f with e_i built
 // from q0 or q1), then final_clamp_pack8_o8.
+// The intra column pass two columns at a time on packed int16 pairs: the
+// quantiser's bounds keep every intermediate of the pass (and its outputs,
+// above) within int16 (q and p sums <= 25,062, f2 -+ f1 <= 4 x 4,958), so
+// each product pair is one v_dot2 with halved constants and two columns'
+// ms9 results pack by pk_ms8, the butterflies run as v_pk_add/sub_i16, and
+// g = ms9(C1D4 x) = (181 x) >> 8 per half.  Columns (A, B) = (0, 4), (1, 7),
+// (5, 3), (2, 6): out[k] = (x_kA, x_kB) is the row pass's input pair as it
+// stands (a04, a17, a53, a26 of row k).
+__device__ __forceinline__ void idct_col_pair_pk(const uint32_t a[4], const uint32_t b[4], s16x2 out[8]) {
+  // a/b: column A's/B's dequantised natural pairs (x0,x4) (x1,x7) (x5,x3) (x2,x6)
+  auto d = [](uint32_t x) { return __builtin_bit_cast(s16x2, x); };
+  const s16x2 P0 = pk_ms8(dot2(d(a[1]), 2 * C7D16, -2 * C1D16), dot2(d(b[1]), 2 * C7D16, -2 * C1D16));
+  const s16x2 P3 = pk_ms8(dot2(d(a[1]), 2 * C1D16, 2 * C7D16), dot2(d(b[1]), 2 * C1D16, 2 * C7D16));
+  const s16x2 P1 = pk_ms8(dot2(d(a[2]), 2 * C3D16, -2 * C5D16), dot2(d(b[2]), 2 * C3D16, -2 * C5D16));
+  const s16x2 P2 = pk_ms8(dot2(d(a[2]), 2 * C5D16, 2 * C3D16), dot2(d(b[2]), 2 * C5D16, 2 * C3D16));
+  const s16x2 Q0 = pk_ms8(dot2(d(a[0]), 2 * C1D4, 2 * C1D4), dot2(d(b[0]), 2 * C1D4, 2 * C1D4));
+  const s16x2 Q1 = pk_ms8(dot2(d(a[0]), 2 * C1D4, -2 * C1D4), dot2(d(b[0]), 2 * C1D4, -2 * C1D4));
+  const s16x2 Q2 = pk_ms8(dot2(d(a[3]), 2 * C3D8, -2 * C1D8), dot2(d(b[3]), 2 * C3D8, -2 * C1D8));
+  const s16x2 Q3 = pk_ms8(dot2(d(a[3]), 2 * C1D8, 2 * C3D8), dot2(d(b[3]), 2 * C1D8, 2 * C3D8));
+  const s16x2 E0 = Q0 + Q3, E1 = Q1 + Q2, E2 = Q1 - Q2, E3 = Q0 - Q3;
+  const s16x2 F0 = P0 + P1, F1 = P0 - P1, F2 = P3 - P2, F3 = P3 + P2;
+  const s16x2 Dm = F2 - F1, Dp = F2 + F1;
+  const s16x2 G1 = pk_ms8(dot2(Dm, C1D4 / 2, 0), dot2(Dm, 0, C1D4 / 2));
+  const s16x2 G2 = pk_ms8(dot2(Dp, C1D4 / 2, 0), dot2(Dp, 0, C1D4 / 2));
+  out[0] = E0 + F3;
+  out[1] = E1 + G2;
+  out[2] = E2 + G1;
+  out[3] = E3 + F0;
+  out[4] = E3 - F0;
+  out[5] = E2 - G1;
+  out[6] = E1 - G2;
+  out[7] = E0 - F3;
+}
 __device__ __forceinline__ void iq_idct_intra_rec(int v[64], int q, uint2 rec[8]) {
   const uint32_t q2 = 0x20002u * (uint32_t)q, qq = 0x10001u * (uint32_t)(q - (int)!(q & 1));
-  iq_idct_cols([&](int e, int f) { return pk2(v[e], v[f]); }, q2, qq, true, v[0] * 8, v);
+  const int dc8 = v[0] * 8;
+  // the column's dequantised natural pairs (x0,x4) (x1,x7) (x5,x3) (x2,x6)
+  auto col = [&](int c, uint32_t o[4]) {
+    o[0] = dequantise_pk(pk2(v[c], v[32 + c]), q2, qq);
+    if (c == 0) o[0] = __builtin_amdgcn_perm(o[0], (uint32_t)dc8, 0x07060100u);  // (DC x 8, x4)
+    o[1] = dequantise_pk(pk2(v[8 + c], v[56 + c]), q2, qq);
+    o[2] = dequantise_pk(pk2(v[40 + c], v[24 + c]), q2, qq);
+    o[3] = dequantise_pk(pk2(v[16 + c], v[48 + c]), q2, qq);
+  };
+  s16x2 cp[4][8];  // [column pair (0,4) (1,7) (5,3) (2,6)][row]
+  {
+    constexpr int CA[4] = {0, 1, 5, 2}, CB[4] = {4, 7, 3, 6};
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      uint32_t a[4], b[4];
+      col(CA[i], a);
+      col(CB[i], b);
+      idct_col_pair_pk(a, b, cp[i]);
+      SCHED_FENCE();
+    }
+  }
   const int r8 = opaque(8 << 9);  // one VGPR for every row (not rematerialised per use)
 #pragma unroll
   for (int r = 0; r < 8; r++) {
-    const int *x = v + 8 * r;
-    const s16x2 a04 = __builtin_bit_cast(s16x2, pk2(x[0], x[4])), a17 = __builtin_bit_cast(s16x2, pk2(x[1], x[7]));
-    const s16x2 a53 = __builtin_bit_cast(s16x2, pk2(x[5], x[3])), a26 = __builtin_bit_cast(s16x2, pk2(x[2], x[6]));
+    const s16x2 a04 = cp[0][r], a17 = cp[1][r], a53 = cp[2][r], a26 = cp[3][r];
     const int p0 = ms9(dot2(a17, C7D16, -C1D16)), p3 = ms9(dot2(a17, C1D16, C7D16));
     const int p1 = ms9(dot2(a53, C3D16, -C5D16)), p2 = ms9(dot2(a53, C5D16, C3D16));
     const int q0 = ms9(dot2acc(a04, C1D4, C1D4, r8)), q1 = ms9(dot2acc(a04, C1D4, -C1D4, r8));
