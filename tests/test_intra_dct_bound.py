@@ -115,3 +115,55 @@ def test_clamp_is_inactive_from_q5():
     for q in range(1, 32):
         qbr = 256 * q - 1 - (0 if q & 1 else 1)
         assert (qbr >= 1023) == (q >= 5)
+
+
+def test_intra_idct_column_pass_fits_int16():
+    """k_intra_mbg's IDCT column pass runs two columns at a time on packed
+    int16 pairs (k_block.hip idct_col_pair_pk): with the dequantised intra
+    inputs bounded by the quantiser (|AC| <= 1,023 + q <= 1,054, the DC x 8 in
+    8..2,032, iq_idct_intra_rec) every value the pass packs -- the products'
+    ms9 results P/Q, the sums E/F, the g inputs F2 -+ F1, g itself and the
+    outputs -- must stay inside int16.  Interval arithmetic per input (each
+    input independent: a superset of what a block can produce)."""
+    ac, dc = 1054, 2032
+
+    class I:
+        def __init__(self, lo, hi):
+            self.lo, self.hi = lo, hi
+
+        def __add__(self, o):
+            return I(self.lo + o.lo, self.hi + o.hi)
+
+        def __sub__(self, o):
+            return I(self.lo - o.hi, self.hi - o.lo)
+
+        def mul(self, c):
+            return I(min(self.lo * c, self.hi * c), max(self.lo * c, self.hi * c))
+
+        def ms9(self):
+            return I(self.lo // 512, self.hi // 512)
+
+        def mag(self):
+            return max(-self.lo, self.hi)
+
+    for col0 in (True, False):  # column 0 carries the DC in row 0
+        x = [I(-ac, ac) for _ in range(8)]
+        if col0:
+            x[0] = I(8, dc)
+        d = lambda a, ca, b, cb: (a.mul(ca) + b.mul(cb)).ms9()  # noqa: E731
+        P0 = d(x[1], 4 * C7D16, x[7], -4 * C1D16)
+        P3 = d(x[1], 4 * C1D16, x[7], 4 * C7D16)
+        P1 = d(x[5], 4 * C3D16, x[3], -4 * C5D16)
+        P2 = d(x[5], 4 * C5D16, x[3], 4 * C3D16)
+        Q0 = d(x[0], 4 * C1D4, x[4], 4 * C1D4)
+        Q1 = d(x[0], 4 * C1D4, x[4], -4 * C1D4)
+        Q2 = d(x[2], 4 * C3D8, x[6], -4 * C1D8)
+        Q3 = d(x[2], 4 * C1D8, x[6], 4 * C3D8)
+        E = [Q0 + Q3, Q1 + Q2, Q1 - Q2, Q0 - Q3]
+        F = [P0 + P1, P0 - P1, P3 - P2, P3 + P2]
+        Dm, Dp = F[2] - F[1], F[2] + F[1]
+        G1, G2 = Dm.mul(C1D4).ms9(), Dp.mul(C1D4).ms9()
+        O = [E[0] + F[3], E[1] + G2, E[2] + G1, E[3] + F[0], E[3] - F[0], E[2] - G1, E[1] - G2, E[0] - F[3]]
+        vals = [P0, P1, P2, P3, Q0, Q1, Q2, Q3] + E + F + [Dm, Dp, G1, G2] + O
+        worst = max(v.mag() for v in vals)
+        assert worst < 2 ** 15, (col0, worst)
