@@ -13,6 +13,8 @@
 // per-wave LDS staging area as whole 1-KB stores; every load and store is a
 // buffer access whose out-of-range offset replaces a branch.
 
+#include <type_traits>
+
 #include "common.h"
 #include "launch.h"
 #include "quant_int.h"
@@ -1047,28 +1049,47 @@ __global__ __launch_bounds__(64) OCC4 void k_inter_mbg(p64gpu_encode_args a, Blk
   // ChenDct of the residual, each row quantised right after its row pass and
   // kept as natural int16 level pairs L[r][j] = (x_r,2j, x_r,2j+1): 32
   // registers instead of 64 ints for the levels
+  // BoundDct's clamp of the quantiser cannot act from q = 5 on (the level
+  // bound then lies beyond it) when every AC |v| <= 8,187: for a residual
+  // block |v| <= 1.9227 sum|r| + 8.56 (affine bound over this kernel's
+  // butterfly, tests/test_intra_dct_bound.py), so sum|r| <= 4,253 suffices
+  // (the DC's own bound, >= 10,235 from q = 5, is then far away too); an intra
+  // MB's block is 8-bit pixels, 8,163.5 at most.  sum|r| is 16 v_sad_u8 of the
+  // current rows against the prediction; where the whole wave qualifies (on
+  // natural content nearly always) the quantiser runs without its v_med3.
+  uint32_t sar = 0;
+#pragma unroll
+  for (int r = 0; r < 8; r++) sar = sad4(f.rows[r].y, prow[r].y, sad4(f.rows[r].x, prow[r].x, sar));
+  const bool no_clamp = uni(__all(q >= 5 && (intra || sar <= 4253u)));
   uint32_t L[8][4];
   {
     s16x2 p[8][4];
     fdct_cols_pk<true>(f.rows, p, prow);
+    auto rows = [&](auto clamp) {
+      constexpr bool CL = decltype(clamp)::value;
 #pragma unroll
-    for (int r = 0; r < 8; r++) {
-      int o[8];
-      fwd_row_pk(p[r], o);
+      for (int r = 0; r < 8; r++) {
+        int o[8];
+        fwd_row_pk(p[r], o);
 #pragma unroll
-      for (int k = 0; k < 8; k++) o[k] = opaque(o[k]);
-      int l[8];
+        for (int k = 0; k < 8; k++) o[k] = opaque(o[k]);
+        int l[8];
 #pragma unroll
-      for (int k = 0; k < 8; k++) {
-        if (r == 0 && k == 0)  // DC: intra (DC +- 4) / 8 in 1..254, inter as AC with DC bounds
-          l[k] = intra ? clampi(dct_final(min(dct_final(o[0]), 2047)), 1, 254) : qlevel_int(o[0], qd);
-        else
-          l[k] = qlevel_int(o[k], qt);
+        for (int k = 0; k < 8; k++) {
+          if (r == 0 && k == 0)  // DC: intra (DC +- 4) / 8 in 1..254, inter as AC with DC bounds
+            l[k] = intra ? clampi(dct_final(min(dct_final(o[0]), 2047)), 1, 254) : qlevel_int<CL>(o[0], qd);
+          else
+            l[k] = qlevel_int<CL>(o[k], qt);
+        }
+#pragma unroll
+        for (int j = 0; j < 4; j++) L[r][j] = pk2(l[2 * j], l[2 * j + 1]);
+        SCHED_FENCE();
       }
-#pragma unroll
-      for (int j = 0; j < 4; j++) L[r][j] = pk2(l[2 * j], l[2 * j + 1]);
-      SCHED_FENCE();
-    }
+    };
+    if (no_clamp)
+      rows(std::false_type{});
+    else
+      rows(std::true_type{});
   }
   // natural positions e (low half) and f (high half) as one pair
   auto lpair = [&](int e, int f) {
