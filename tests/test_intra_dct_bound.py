@@ -167,3 +167,25 @@ def test_intra_idct_column_pass_fits_int16():
         vals = [P0, P1, P2, P3, Q0, Q1, Q2, Q3] + E + F + [Dm, Dp, G1, G2] + O
         worst = max(v.mag() for v in vals)
         assert worst < 2 ** 15, (col0, worst)
+
+
+def test_inter_residual_sum_bound_keeps_the_clamp_inactive():
+    """k_inter_mbg drops the quantiser's BoundDct clamp for a wave whose
+    blocks all have sum|residual| <= 4,253 (q >= 5): |v| = |sum a_i r_i + err|
+    <= max|a_i| sum|r| + max|err| over every AC output of the kernel's
+    butterfly must stay <= 8 x 1023 + 3, and the DC within its own bound
+    (>= 10,235 from q = 5 on)."""
+    px = [[Aff(np.eye(64)[8 * r + c]) for c in range(8)] for r in range(8)]
+    cols = [col_pass([px[r][c] for r in range(8)])[0] for c in range(8)]
+    worst_ac = worst_dc = 0.0
+    for r in range(8):
+        o, _ = row_pass([cols[c][r] for c in range(8)])
+        for k in range(8):
+            a = o[k]
+            v = np.abs(a.a).max() * 4253 + max(-a.lo, a.hi)
+            if (r, k) == (0, 0):
+                worst_dc = max(worst_dc, v)
+            else:
+                worst_ac = max(worst_ac, v)
+    assert worst_ac <= 8 * 1023 + 3, worst_ac
+    assert worst_dc <= 8 * (256 * 5 - 1) + 3, worst_dc
