@@ -34,6 +34,7 @@ namespace {
 // lane writes its block's 128 bytes of levels as whole cache lines.
 
 constexpr ZigZag k_zz = make_zigzag();  // compile-time copy for register renaming
+typedef short s16x2 __attribute__((ext_vector_type(2)));  // an int16 pair in one VGPR
 
 // The forward quantiser from the raw row-pass output (quant_int.h: final /8,
 // BoundDct, CCITT(Flat)Quantize, bound, as one clamp, one 24-bit multiply-add
@@ -52,6 +53,26 @@ constexpr QIntTab make_qint_tab() {
   return t;
 }
 __constant__ QIntTab c_qint = make_qint_tab();
+// The quantiser on an int16 pair when D = 16q is a power of two (q = 1, 2, 4,
+// 8, 16: the table's multiplier is 1, level = (vc + C) >> s): clamp (two
+// v_pk min/max against per-half bounds), the sign-selected addend by v_bfi
+// under v_pk_ashrrev 15, v_pk_add, v_pk_ashrrev s -- four to six
+// instructions per two levels instead of four to five per level.
+template <bool CLAMP>
+__device__ __forceinline__ uint32_t qlevel_pk2(uint32_t x, uint32_t lo2, uint32_t hi2, uint32_t cp2, uint32_t cn2,
+                                               int s) {
+  if (CLAMP) {
+    asm("v_pk_min_i16 %0, %1, %2" : "=v"(x) : "v"(x), "v"(hi2));
+    asm("v_pk_max_i16 %0, %1, %2" : "=v"(x) : "v"(x), "v"(lo2));
+  }
+  const s16x2 v = __builtin_bit_cast(s16x2, x);
+  const uint32_t m = __builtin_bit_cast(uint32_t, (s16x2)(v >> (s16x2){15, 15}));
+  uint32_t c;
+  asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(c) : "v"(m), "v"(cn2), "v"(cp2));
+  const s16x2 r = (s16x2)(v + __builtin_bit_cast(s16x2, c)) >> (s16x2){(short)s, (short)s};
+  return __builtin_bit_cast(uint32_t, r);
+}
+__device__ __forceinline__ uint32_t pk16u(int lo, int hi) { return (uint32_t)(lo & 0xffff) | ((uint32_t)hi << 16); }
 // CLAMP false: the caller knows |v| <= t.vhi (tests/test_intra_dct_bound.py)
 template <bool CLAMP = true>
 __device__ __forceinline__ int qlevel_int(int v, const p64_qint &t) {
@@ -114,7 +135,6 @@ __device__ __forceinline__ BlkPos blk_pos_mb(unsigned gmb, int b, int w, int h, 
 // 32 bits, the same ms9 rounding after).  Row-pass intermediates stay below
 // 2^15: sums <= 11,600, u = d + r <= 14,000.  Half the registers of the
 // scalar form between the passes.
-typedef short s16x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ s16x2 pk16(int lo, int hi) {  // two values that fit int16
   return __builtin_bit_cast(s16x2, (uint32_t)(lo & 0xffff) | ((uint32_t)hi << 16));
 }
@@ -169,6 +189,27 @@ __device__ __forceinline__ void fwd_row_pk(const s16x2 p[4], int o[8]) {
 // for d0, d3, which are added to products and shift themselves.  Pixel or
 // residual input (|x| <= 255): sums <= 1,020, u = 4d + r <= 2,462, every
 // intermediate inside int16; the products and their sums exact in 32 bits.
+// The same row pass with its outputs as natural int16 pairs (o0,o1) (o2,o3)
+// (o4,o5) (o6,o7) (|o| <= 8,187 x ... < 2^15 for 8-bit input, BoundDct's
+// range): pk_ms8 for the pairs whose constants halve, one shift for o2 and o6
+// (C1D8 is odd) joined to the halved o3 / o7 by one v_perm.
+__device__ __forceinline__ void fwd_row_pk2(const s16x2 p[4], uint32_t P[4]) {
+  const s16x2 s01 = (p[0] + p[3].yx) >> 1, s23 = (p[1] + p[2].yx) >> 1;
+  const s16x2 d01 = (p[0] - p[3].yx) >> 1, d23 = (p[1] - p[2].yx) >> 1;
+  const s16x2 e01 = s01 + s23.yx, e32 = s01 - s23.yx;
+  const int A0 = dot2(e01, C1D4 / 2, C1D4 / 2), A4 = dot2(e01, C1D4 / 2, -C1D4 / 2);
+  const int o2 = ms9(dot2(e32, C1D8, C3D8)), o6 = ms9(dot2(e32, C3D8, -C1D8));
+  const s16x2 q = __builtin_shufflevector(d01, d23, 1, 2);
+  const s16x2 dd = __builtin_shufflevector(d23, d01, 1, 2);
+  const s16x2 rr = pk_ms8(dot2(q, C1D4 / 2, -C1D4 / 2), dot2(q, C1D4 / 2, C1D4 / 2));
+  const s16x2 u03 = dd + rr, u12 = dd - rr;
+  const int A1 = dot2(u03, C7D16 / 2, C1D16 / 2), A7 = dot2(u03, -C1D16 / 2, C7D16 / 2);
+  const int A3 = dot2(u12, -C5D16 / 2, C3D16 / 2), A5 = dot2(u12, C3D16 / 2, C5D16 / 2);
+  P[0] = __builtin_bit_cast(uint32_t, pk_ms8(A0, A1));
+  P[2] = __builtin_bit_cast(uint32_t, pk_ms8(A4, A5));
+  P[1] = __builtin_amdgcn_perm((uint32_t)A3, (uint32_t)o2, 0x06050100u);
+  P[3] = __builtin_amdgcn_perm((uint32_t)A7, (uint32_t)o6, 0x06050100u);
+}
 // The outputs are left as 2 x the pre-shift sums (halved constants, A above):
 // the caller packs two columns' outputs with pk_ms8.
 __device__ __forceinline__ void fwd_col_pk(const s16x2 p[4], int o[8]) {
@@ -985,7 +1026,8 @@ __device__ __forceinline__ void pred_rows(const PredSrc &P, bool filter, uint2 p
 // OVR: an -o MTYPE override array is given.  Without one every MTYPE the
 // decision can return (0, 2, 5, 8: decide_mtype) carries coefficients, so
 // the level mask for MC-only types (4, 7) is left out.
-template <bool QMB, bool OVR>
+// POW2: a uniform q whose D = 16q is a power of two (qlevel_pk2)
+template <bool QMB, bool OVR, bool POW2 = false>
 __global__ __launch_bounds__(64) OCC4 void k_inter_mbg(p64gpu_encode_args a, BlkDiv kd, unsigned nmbs,
                                                              const p64_me_rec *me) {
   __shared__ __align__(16) uint8_t lds[LVL_WAVE];
@@ -1067,6 +1109,28 @@ __global__ __launch_bounds__(64) OCC4 void k_inter_mbg(p64gpu_encode_args a, Blk
     fdct_cols_pk<true>(f.rows, p, prow);
     auto rows = [&](auto clamp) {
       constexpr bool CL = decltype(clamp)::value;
+      if (POW2) {  // level pairs straight from the packed row pass
+        const uint32_t lo_ac = pk16u(qt.vlo, qt.vlo), hi_ac = pk16u(qt.vhi, qt.vhi);
+        const uint32_t cp2 = pk16u(qt.cp, qt.cp), cn2 = pk16u(qt.cn, qt.cn);
+#pragma unroll
+        for (int r = 0; r < 8; r++) {
+          uint32_t P[4];
+          fwd_row_pk2(p[r], P);
+#pragma unroll
+          for (int j = 0; j < 4; j++) {
+            const bool dcp = r == 0 && j == 0;  // (DC, o1): the DC's own bounds in the low half
+            L[r][j] = qlevel_pk2<CL>(P[j], dcp ? pk16u(qd.vlo, qt.vlo) : lo_ac, dcp ? pk16u(qd.vhi, qt.vhi) : hi_ac,
+                                     cp2, cn2, qt.s);
+          }
+          if (r == 0) {  // intra DC: (DC +- 4) / 8 in 1..254 of the bounded DC (transform.c:321-325)
+            const int dc = (int)(int16_t)(P[0] & 0xffffu);
+            const int l0 = clampi(dct_final(min(dct_final(dc), 2047)), 1, 254);
+            L[0][0] = intra ? (L[0][0] & 0xffff0000u) | (uint32_t)l0 : L[0][0];
+          }
+          SCHED_FENCE();
+        }
+        return;
+      }
 #pragma unroll
       for (int r = 0; r < 8; r++) {
         int o[8];
@@ -1187,12 +1251,19 @@ hipError_t inter_mbg(const p64gpu_encode_args &a, const p64_me_rec *me, hipStrea
   const dim3 grid(mbg_workgroups(nm, 1)), block(64);
   const BlkDiv kd = blk_div(a.width, a.height);
   const bool ovr = a.mtype_override != nullptr;
+  // a uniform q with D = 16q a power of two: the packed quantiser (multiplier 1)
+  const bool pow2 = !a.quant_mb && (a.quant & (a.quant - 1)) == 0 && make_qint_tab().ac[a.quant].m == 1 &&
+                    make_qint_tab().dc[a.quant].m == 1;
   if (a.quant_mb && ovr)
     hipLaunchKernelGGL((k_inter_mbg<true, true>), grid, block, 0, st, a, kd, nm, me);
   else if (a.quant_mb)
     hipLaunchKernelGGL((k_inter_mbg<true, false>), grid, block, 0, st, a, kd, nm, me);
+  else if (ovr && pow2)
+    hipLaunchKernelGGL((k_inter_mbg<false, true, true>), grid, block, 0, st, a, kd, nm, me);
   else if (ovr)
     hipLaunchKernelGGL((k_inter_mbg<false, true>), grid, block, 0, st, a, kd, nm, me);
+  else if (pow2)
+    hipLaunchKernelGGL((k_inter_mbg<false, false, true>), grid, block, 0, st, a, kd, nm, me);
   else
     hipLaunchKernelGGL((k_inter_mbg<false, false>), grid, block, 0, st, a, kd, nm, me);
   return hipGetLastError();

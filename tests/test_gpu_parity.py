@@ -906,6 +906,34 @@ def _edge_pictures(w, h):
     return out
 
 
+@pytest.mark.parametrize("quant", [1, 2, 3, 4, 5, 8, 16, 31])
+def test_inter_uniform_quant_vs_oracle(p64, oracle_mod, torch_dev, quant):
+    """k_inter_mbg at one uniform q, the case its launch specialises: q with
+    D = 16q a power of two (1, 2, 4, 8, 16) quantises packed level pairs
+    (qlevel_pk2), q >= 5 drops the clamp where the residual-sum bound allows,
+    the others keep the scalar clamped quantiser.  Extreme +-255 residuals
+    (every clamp active), a synthetic picture pair (small residuals), and the
+    MTYPE overrides 0..9 (the override instance), against oracle.encode_frame."""
+    torch = torch_dev
+    w, h = 176, 144
+    nmb = 99
+    pairs = _edge_pictures(w, h)[:3] + [(p64.synth_frame(5, 3, w, h), p64.synth_frame(5, 2, w, h))]
+    for i, (cur, ref) in enumerate(pairs):
+        for ov in (None, (np.arange(nmb) % 10).astype(np.int8)):
+            li = np.zeros(nmb, np.uint8)
+            coef, mb, me, rec = oracle_mod.encode_frame(w, h, cur, ref, li, intra=False, quant=quant,
+                                                        me_mode=1, search_limit=31, mtype_override=ov)
+            lid = torch.zeros(nmb, dtype=torch.uint8, device="cuda")
+            rd = torch.zeros(cur.size, dtype=torch.uint8, device="cuda")
+            o = p64.encode_frames(dev(torch, cur), dev(torch, ref), rd, lid, width=w, height=h,
+                                  intra=False, quant=quant, me_mode=p64.ME_FULL, search_limit=31,
+                                  mtype_override=(dev(torch, ov) if ov is not None else None))
+            tag = f"q{quant} pair {i} override {ov is not None}"
+            np.testing.assert_array_equal(host(o.coef)[0], coef, err_msg=f"coef {tag}")
+            np.testing.assert_array_equal(host(o.mb)[0].view(p64.MB_DTYPE).reshape(nmb), mb, err_msg=f"mb {tag}")
+            np.testing.assert_array_equal(host(rd), rec, err_msg=f"recon {tag}")
+
+
 def test_block_encoders_extreme_residuals_vs_oracle(p64, oracle_mod, torch_dev):
     """k_intra_mbg / k_inter_mbg at the edges of their 16-bit range proofs
     (column outputs of a +-255 residual, row-pass intermediates < 2^15, the
