@@ -402,16 +402,19 @@ __device__ __forceinline__ void idct_col_pair_pk(const uint32_t a[4], const uint
   out[6] = E1 - G2;
   out[7] = E0 - F3;
 }
-__device__ __forceinline__ void iq_idct_intra_rec(int v[64], int q, uint2 rec[8]) {
+// pair(e, f): the levels of natural positions e (low half) and f (high half)
+// packed; dc: the DC level
+template <class PairFn>
+__device__ __forceinline__ void iq_idct_intra_rec_pairs(PairFn pair, int dc, int q, uint2 rec[8]) {
   const uint32_t q2 = 0x20002u * (uint32_t)q, qq = 0x10001u * (uint32_t)(q - (int)!(q & 1));
-  const int dc8 = v[0] * 8;
+  const int dc8 = dc * 8;
   // the column's dequantised natural pairs (x0,x4) (x1,x7) (x5,x3) (x2,x6)
   auto col = [&](int c, uint32_t o[4]) {
-    o[0] = dequantise_pk(pk2(v[c], v[32 + c]), q2, qq);
+    o[0] = dequantise_pk(pair(c, 32 + c), q2, qq);
     if (c == 0) o[0] = __builtin_amdgcn_perm(o[0], (uint32_t)dc8, 0x07060100u);  // (DC x 8, x4)
-    o[1] = dequantise_pk(pk2(v[8 + c], v[56 + c]), q2, qq);
-    o[2] = dequantise_pk(pk2(v[40 + c], v[24 + c]), q2, qq);
-    o[3] = dequantise_pk(pk2(v[16 + c], v[48 + c]), q2, qq);
+    o[1] = dequantise_pk(pair(8 + c, 56 + c), q2, qq);
+    o[2] = dequantise_pk(pair(40 + c, 24 + c), q2, qq);
+    o[3] = dequantise_pk(pair(16 + c, 48 + c), q2, qq);
   };
   s16x2 cp[4][8];  // [column pair (0,4) (1,7) (5,3) (2,6)][row]
   {
@@ -440,6 +443,16 @@ __device__ __forceinline__ void iq_idct_intra_rec(int v[64], int q, uint2 rec[8]
     rec[r] = final_clamp_pack8_o8(o8);
     SCHED_FENCE();
   }
+}
+__device__ __forceinline__ void iq_idct_intra_rec(int v[64], int q, uint2 rec[8]) {
+  iq_idct_intra_rec_pairs([&](int e, int f) { return pk2(v[e], v[f]); }, v[0], q, rec);
+}
+// the levels of natural positions e (low half) and f (high half) of the
+// natural int16 level pairs L[r][j] = (x_r,2j, x_r,2j+1) as one pair
+__device__ __forceinline__ uint32_t lvl_pair(const uint32_t L[8][4], int e, int f) {
+  const uint32_t sel = (uint32_t)(2 * (e & 1)) | ((uint32_t)(2 * (e & 1) + 1) << 8) |
+                       ((uint32_t)(4 + 2 * (f & 1)) << 16) | ((uint32_t)(5 + 2 * (f & 1)) << 24);
+  return __builtin_amdgcn_perm(L[f >> 3][(f & 7) >> 1], L[e >> 3][(e & 7) >> 1], sel);
 }
 
 // intra picture (p64.c:635, 770-771: every MB is MTYPE 0, CBP 0x3f), block
@@ -491,13 +504,48 @@ struct IntraOut {
 };
 // one block: ChenDct, quantise + zigzag into the LDS staging, dequantise,
 // ChenIDct, reconstruction into `out`
-template <bool CLAMP>
+template <bool CLAMP, bool POW2 = false>
 __device__ __forceinline__ void intra_block(const p64gpu_encode_args &a, const IntraFetch &f, uint8_t *lds,
                                             int lane, IntraOut &out) {
   const int w = a.width, h = a.height;
   const BlkPos &p = f.p;
   const int q = f.q;
   const p64_qint qt = c_qint.ac[q];
+  out.pw = p.plane ? w >> 1 : w;
+  out.rec_off = (uint32_t)((int64_t)p.fi * a.frame_stride) + (uint32_t)plane_offset(p.plane, w, h) +
+                (uint32_t)mul24(p.y, out.pw) + (uint32_t)p.x;
+  if (POW2) {  // a uniform q with 16q a power of two: level pairs from the packed row pass (qlevel_pk2)
+    uint32_t L[8][4];
+    int l0;
+    {
+      s16x2 pc[8][4];
+      fdct_cols_pk(f.rows, pc);
+      const uint32_t lo2 = pk16u(qt.vlo, qt.vlo), hi2 = pk16u(qt.vhi, qt.vhi);
+      const uint32_t cp2 = pk16u(qt.cp, qt.cp), cn2 = pk16u(qt.cn, qt.cn);
+#pragma unroll
+      for (int r = 0; r < 8; r++) {
+        uint32_t P[4];
+        fwd_row_pk2(pc[r], P);
+#pragma unroll
+        for (int j = 0; j < 4; j++) L[r][j] = qlevel_pk2<CLAMP>(P[j], lo2, hi2, cp2, cn2, qt.s);
+        if (r == 0) {  // intra DC: ((DC +- 4) / 8) in 1..254 of the bounded DC (transform.c:321-325)
+          l0 = clampi(dct_final(min(dct_final((int)(int16_t)(P[0] & 0xffffu)), 2047)), 1, 254);
+          L[0][0] = (L[0][0] & 0xffff0000u) | (uint32_t)l0;
+        }
+        SCHED_FENCE();
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      uint32_t pk[4];
+#pragma unroll
+      for (int j = 0; j < 4; j++) pk[j] = lvl_pair(L, k_zz.inv[8 * k + 2 * j], k_zz.inv[8 * k + 2 * j + 1]);
+      put_levels(lds, lane, k, make_uint4(pk[0], pk[1], pk[2], pk[3]));
+      SCHED_FENCE();
+    }
+    iq_idct_intra_rec_pairs([&](int e, int f) { return lvl_pair(L, e, f); }, l0, q, out.rec);
+    return;
+  }
   int v[64];
   fdct_block_pk(f.rows, v);
   // in scan order: quantise (BoundDct + CCITTFlatQuantize + FlatBound), pack
@@ -525,9 +573,6 @@ __device__ __forceinline__ void intra_block(const p64gpu_encode_args &a, const I
     SCHED_FENCE();
   }
   iq_idct_intra_rec(v, q, out.rec);  // ICCITTFlatQuantize + ChenIDct + BoundIDctMatrix
-  out.pw = p.plane ? w >> 1 : w;
-  out.rec_off = (uint32_t)((int64_t)p.fi * a.frame_stride) + (uint32_t)plane_offset(p.plane, w, h) +
-                (uint32_t)mul24(p.y, out.pw) + (uint32_t)p.x;
 }
 // the stores of an MB-grouped wave (k_intra_mbg, k_inter_mbg), all buffer
 // stores with out-of-range offsets instead of branches: the wave's levels run
@@ -601,7 +646,7 @@ __device__ __forceinline__ void mbg_store(const p64gpu_encode_args &a, const Blk
 // looks at its MB's other blocks; levels leave as one contiguous 8-KB run per
 // wave.  (Ten whole MBs per wave, as the inter kernel needs for its CBP
 // ballots, leave lanes 60..63 idle: 6.25% more waves.)
-template <bool QMB, bool CLAMP>
+template <bool QMB, bool CLAMP, bool POW2 = false>
 __global__ __launch_bounds__(64 * MBG_WAVES) void k_intra_mbg(p64gpu_encode_args a, BlkDiv kd, unsigned nmbs) {
   __shared__ __align__(16) uint8_t lvl[MBG_WAVES * LVL_WAVE];
   const int lane = threadIdx.x & 63;
@@ -616,7 +661,7 @@ __global__ __launch_bounds__(64 * MBG_WAVES) void k_intra_mbg(p64gpu_encode_args
   const IntraFetch f = intra_fetch_at<QMB>(a, blk_pos_mb(gmb, b, a.width, a.height, kd));
   PRIO_LOW();
   IntraOut o;
-  intra_block<CLAMP>(a, f, lds, lane, o);
+  intra_block<CLAMP, POW2>(a, f, lds, lane, o);
   // the MB's record and LastIntra (p64.c:909-910: MTYPE 0, CBP 0x3f, LastIntra
   // reset) from the lane of its block 0
   const bool rl = b == 0 && g0 + (unsigned)lane < nblk;
@@ -1237,10 +1282,15 @@ hipError_t intra_mbg(const p64gpu_encode_args &a, hipStream_t st) {
   const unsigned waves = (6u * nm + 63u) / 64u;  // 64 blocks a wave
   const dim3 grid((waves + MBG_WAVES - 1) / MBG_WAVES), block(64 * MBG_WAVES);
   const BlkDiv kd = blk_div(a.width, a.height);
+  const bool pow2 = !a.quant_mb && (a.quant & (a.quant - 1)) == 0 && make_qint_tab().ac[a.quant].m == 1;
   if (a.quant_mb)
     hipLaunchKernelGGL((k_intra_mbg<true, true>), grid, block, 0, st, a, kd, nm);
-  else if (a.quant >= 5)  // no BoundDct clamp can act (intra_block)
+  else if (a.quant >= 5 && pow2)  // no BoundDct clamp can act (intra_block), packed quantiser
+    hipLaunchKernelGGL((k_intra_mbg<false, false, true>), grid, block, 0, st, a, kd, nm);
+  else if (a.quant >= 5)
     hipLaunchKernelGGL((k_intra_mbg<false, false>), grid, block, 0, st, a, kd, nm);
+  else if (pow2)
+    hipLaunchKernelGGL((k_intra_mbg<false, true, true>), grid, block, 0, st, a, kd, nm);
   else
     hipLaunchKernelGGL((k_intra_mbg<false, true>), grid, block, 0, st, a, kd, nm);
   return hipGetLastError();

@@ -908,7 +908,7 @@ def _edge_pictures(w, h):
 
 @pytest.mark.parametrize("quant", [1, 2, 3, 4, 5, 8, 16, 31])
 def test_inter_uniform_quant_vs_oracle(p64, oracle_mod, torch_dev, quant):
-    """k_inter_mbg at one uniform q, the case its launch specialises: q with
+    """k_intra_mbg / k_inter_mbg at one uniform q, the case their launches specialise: q with
     D = 16q a power of two (1, 2, 4, 8, 16) quantises packed level pairs
     (qlevel_pk2), q >= 5 drops the clamp where the residual-sum bound allows,
     the others keep the scalar clamped quantiser.  Extreme +-255 residuals
@@ -919,6 +919,15 @@ def test_inter_uniform_quant_vs_oracle(p64, oracle_mod, torch_dev, quant):
     nmb = 99
     pairs = _edge_pictures(w, h)[:3] + [(p64.synth_frame(5, 3, w, h), p64.synth_frame(5, 2, w, h))]
     for i, (cur, ref) in enumerate(pairs):
+        # the intra picture at the same uniform q (k_intra_mbg's packed
+        # quantiser for powers of two, the clamp below q = 5)
+        li = np.zeros(nmb, np.uint8)
+        coef, mb, _, rec = oracle_mod.encode_frame(w, h, cur, None, li, intra=True, quant=quant)
+        lid = torch.zeros(nmb, dtype=torch.uint8, device="cuda")
+        rd = torch.zeros(cur.size, dtype=torch.uint8, device="cuda")
+        o = p64.encode_frames(dev(torch, cur), None, rd, lid, width=w, height=h, intra=True, quant=quant)
+        np.testing.assert_array_equal(host(o.coef)[0], coef, err_msg=f"intra coef q{quant} picture {i}")
+        np.testing.assert_array_equal(host(rd), rec, err_msg=f"intra recon q{quant} picture {i}")
         for ov in (None, (np.arange(nmb) % 10).astype(np.int8)):
             li = np.zeros(nmb, np.uint8)
             coef, mb, me, rec = oracle_mod.encode_frame(w, h, cur, ref, li, intra=False, quant=quant,
