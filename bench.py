@@ -441,6 +441,25 @@ def make_inputs(torch, p64_amd, content, w, h, seed0, S, nslots):
     return out
 
 
+def _pow2_quant(q):
+    """the library's packed-quantiser instances: a uniform q with 16q a power
+    of two (k_block.hip qlevel_pk2)"""
+    return q in (1, 2, 4, 8, 16)
+
+
+def intra_kernel_name(q):
+    """k_intra_mbg's instance for a uniform q (p64k::intra_mbg): <QMB, CLAMP,
+    POW2> as rocprof prints it"""
+    clamp = "false" if q >= 5 else "true"
+    return f"k_intra_mbg<false, {clamp}, true>" if _pow2_quant(q) else f"k_intra_mbg<false, {clamp}, false>"
+
+
+def inter_kernel_name(q):
+    """k_inter_mbg's instance for a uniform q without overrides
+    (p64k::inter_mbg): <QMB, OVR, POW2>"""
+    return "k_inter_mbg<false, false, %s>" % ("true" if _pow2_quant(q) else "false")
+
+
 def load_pmc(path, workload_key):
     try:
         with open(path) as f:
@@ -704,7 +723,7 @@ def main(argv=None):
                 post(t)
 
         # steady-state spin-up (timed_region): the same launches into scratch
-        kme, kin = "k_motion<%d>" % (2 if args.mode == "full" else 1), "k_inter_mbg<false, false>"
+        kme, kin = "k_motion<%d>" % (2 if args.mode == "full" else 1), inter_kernel_name(args.quant)
         sp = {}
 
         def spin_init():
@@ -1053,7 +1072,7 @@ def run_intra(args, torch, dist, np, p64_amd, world, frames, S, nmb, pic, nslots
                                    f"{S} pictures/step/GPU", "macroblocks_per_step_per_gpu": mbs,
                        "distinct_input_pictures": nslots},
             "roofline": roofline(mbs * INTRA_BYTES_PER_MB, kavg,
-                                 "k_intra_mbg<false, %s>" % ("false" if args.quant >= 5 else "true"),
+                                 intra_kernel_name(args.quant),
                                  load_pmc(args.pmc_json, key),
                                  algorithmic_bytes_per_mb=INTRA_BYTES_PER_MB, timing=timing_note(args)),
             "valu_busy": (load_pmc(args.pmc_json, key) or {}).get("valu_busy"),
