@@ -73,12 +73,15 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
 SAD_PEAK = 256 * 4 * 16 * 4 * 2.4e9
 # algorithmic HBM bytes per macroblock:
 #   inter: read cur 384 + previous recon 384 + last_intra 1;
-#          write levels 768 + recon 384 + p64_mb_rec 4 + p64_me_rec 28 + last_intra 1
+#          write recon 384 + p64_mb_rec 4 + p64_me_rec 28 + last_intra 1, and
+#          128 per transmitted block (MTYPE with coefficients, CBP bit set:
+#          counted from the last step's records, coded_level_bytes; the kernel
+#          writes every block with a nonzero level, include/p64gpu.h)
 #   intra: read cur 384; write levels 768 + recon 384 + p64_mb_rec 4 + last_intra 1
 #   decode: per MB record 4 + UseQuant 1 + coded flag 1, 128 per coded block,
 #          384 prediction source if not intra, 384 recon write (counted exactly
 #          from the records of each launch, see decode_bytes)
-BYTES_PER_MB = 384 + 384 + 1 + 768 + 384 + 4 + 28 + 1
+BYTES_PER_MB_FIXED = 384 + 384 + 1 + 384 + 4 + 28 + 1
 READ_BYTES_PER_MB = 384 + 384 + 1
 INTRA_BYTES_PER_MB = 384 + 768 + 384 + 4 + 1
 # per-kernel means over the timed region of the driver's command (rocprofv3
@@ -616,18 +619,24 @@ def timed_region(torch, dist, world, steps, t_first, launch, pre=None, post=None
     return elapsed, kern, st
 
 
-def decode_bytes(torch, mb, nmb_all):
-    """Algorithmic HBM bytes of one k_recon_mbg launch over records mb
-    [nmb_all, 4] (all MBs coded): record + UseQuant + coded flag, the levels of
-    coded blocks, the prediction source of non-intra MBs, the recon write."""
+def coded_level_bytes(torch, mb):
+    """128 bytes per transmitted block of the records mb [..., 4]: MTYPE with
+    coefficients and (for MTYPEs with a CBP) its CBP bit set."""
     mt = mb[..., 0].reshape(-1).long()
     cbp = mb[..., 1].reshape(-1).long() & 63
     tc = torch.tensor([1, 1, 1, 1, 0, 1, 1, 0, 1, 1], device=mb.device)[mt]
     has_cbp = torch.tensor([0, 0, 1, 1, 0, 1, 1, 0, 1, 1], device=mb.device)[mt]
     cbp = torch.where(has_cbp == 1, cbp, torch.full_like(cbp, 63))
     nblk = sum(((cbp >> b) & 1) for b in range(6)) * tc
-    inter = (mt >= 2).long()
-    return int((6 * nmb_all + 128 * nblk.sum() + 384 * inter.sum() + 384 * nmb_all).item())
+    return int(128 * nblk.sum().item())
+
+
+def decode_bytes(torch, mb, nmb_all):
+    """Algorithmic HBM bytes of one k_recon_mbg launch over records mb
+    [nmb_all, 4] (all MBs coded): record + UseQuant + coded flag, the levels of
+    coded blocks, the prediction source of non-intra MBs, the recon write."""
+    inter = (mb[..., 0].reshape(-1).long() >= 2).long()
+    return int(6 * nmb_all + coded_level_bytes(torch, mb) + 384 * inter.sum().item() + 384 * nmb_all)
 
 
 def main(argv=None):
@@ -758,10 +767,12 @@ def main(argv=None):
                                   me_mode=mode, search_limit=args.search_limit, out=spin_out(k),
                                   me_given=True)
 
+        vt = args.warmup
         for t in range(1 + args.warmup):  # intra picture + warmup, untimed
+            if t == vt:  # the checked picture's level array whole (only blocks with
+                out_of(t).coef.zero_()  # a nonzero level are written, include/p64gpu.h)
             step(t)
         # snapshot of sequence 0 after the warmup: checked against the oracle
-        vt = args.warmup
         snap = None
         if rank == 0 and not args.no_verify:
             o = out_of(vt)
@@ -777,6 +788,7 @@ def main(argv=None):
         sp.clear()
         tmax = max_over_ranks(elapsed, world, device="cuda")
         last = t_first + args.steps - 1
+        lvl_bytes = coded_level_bytes(torch, out_of(last).mb)  # (the last step's records)
 
         verified, ok = None, True
         if rank == 0 and not args.no_verify:
@@ -795,6 +807,9 @@ def main(argv=None):
                                           search_limit=args.search_limit)
             for t, (gc, gm, ge, gr) in checks:
                 coef, mb, mev, recon = outs[t]
+                if t != vt:  # a reused level buffer: the blocks with a nonzero level
+                    nzb = coef.reshape(-1, 64).any(axis=1)
+                    gc, coef = gc.reshape(-1, 64)[nzb], coef.reshape(-1, 64)[nzb]
                 ok = ok and bool(np.array_equal(gc, coef)
                                  and np.array_equal(gm.view(p64_amd.MB_DTYPE).reshape(nmb), mb)
                                  and np.array_equal(ge.view(p64_amd.ME_DTYPE).reshape(nmb), mev)
@@ -866,8 +881,9 @@ def main(argv=None):
                                        f"collective)" if not root else
                                        f"dp{world} (rank 0 RCCL-scatters pictures, gathers levels "
                                        f"+ records; roofline times the encode launch alone)")},
-            "roofline": roofline(mbs_launch * BYTES_PER_MB, kavg, kernel, pmc,
-                                 algorithmic_bytes_per_mb=BYTES_PER_MB, timing=timing_note(args, root),
+            "roofline": roofline(mbs_launch * BYTES_PER_MB_FIXED + lvl_bytes, kavg, kernel, pmc,
+                                 algorithmic_bytes_per_mb=round(BYTES_PER_MB_FIXED + lvl_bytes / mbs_launch, 1),
+                                 timing=timing_note(args, root),
                                  **split),
             "roofline_hbm_read": {
                 "bound": "hbm", "achieved": round(mbs_launch * READ_BYTES_PER_MB / kavg / 1e9, 1),

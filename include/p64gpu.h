@@ -160,7 +160,13 @@ typedef struct {
   const uint8_t *quant_mb;      /* NULL or [nframes][nmb] UseQuant per MB    */
   const int8_t *mtype_override; /* NULL or [nframes][nmb]; < 0 = no override
                                    (-o interpreter program 0, p64.c:761-768) */
-  int16_t *coef;          /* [nframes][nmb][6][64] zigzag levels, written    */
+  int16_t *coef;          /* [nframes][nmb][6][64] zigzag levels, written:
+                             every block of an intra picture; of an inter
+                             picture every block with a nonzero level, a
+                             block whose 64 levels are all zero is left as
+                             it was (zero the buffer for the whole array;
+                             every block the MB record's CBP and MTYPE
+                             transmit has a nonzero level)                  */
   p64_mb_rec *mb;         /* [nframes][nmb], written                         */
   p64_me_rec *me;         /* NULL or [nframes][nmb], written (inter only)    */
 } p64gpu_encode_args;

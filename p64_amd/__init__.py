@@ -385,7 +385,9 @@ def encode_frames(cur, ref, recon, last_intra, *, width: int, height: int, intra
         raise P64GpuError("buffer sizes do not match nframes x picture geometry")
     if out is None:
         out = FrameBatchOut(
-            coef=torch.empty((nframes, nmb, 6, 64), dtype=torch.int16, device=dev),
+            # zeroed: an inter picture's levels are written for the blocks with a
+            # nonzero level only (P64GPU coef contract, include/p64gpu.h)
+            coef=torch.zeros((nframes, nmb, 6, 64), dtype=torch.int16, device=dev),
             mb=torch.empty((nframes, nmb, 4), dtype=torch.int8, device=dev),
             me=torch.empty((nframes, nmb, 7), dtype=torch.int32, device=dev) if want_me else None)
     else:  # caller-supplied outputs: the kernels write nmb_all records into them

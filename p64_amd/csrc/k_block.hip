@@ -580,9 +580,10 @@ __device__ __forceinline__ void intra_block(const p64gpu_encode_args &a, const I
 // lane's 8 reconstructed rows (rec_off, plane width pw), and from the record
 // lanes (rl) the MB record dword and the LastIntra byte of MB gmb
 // (block form: the wave's blocks g0 .. g0 + nblk - 1 of the launch, 128 bytes
-// of levels each, from lane b's staging)
+// of levels each, from lane b's staging; block b only if bit b of keep is set)
 __device__ __forceinline__ void blk_store_levels(const p64gpu_encode_args &a, const uint8_t *lds, int lane,
-                                                 unsigned nmbs, unsigned g0, uint32_t nblk) {
+                                                 unsigned nmbs, unsigned g0, uint32_t nblk,
+                                                 uint64_t keep = ~0ull) {
   const __amdgpu_buffer_rsrc_t coef =
       __builtin_amdgcn_make_buffer_rsrc((void *)a.coef, (short)0, (int)(nmbs * 768u), BUF_RSRC_W3);
   const uint32_t nbytes = nblk * 128u;
@@ -598,14 +599,16 @@ __device__ __forceinline__ void blk_store_levels(const p64gpu_encode_args &a, co
     d[1] = v.y;
     d[2] = v.z;
     d[3] = v.w;
-    __builtin_amdgcn_raw_buffer_store_b128(d, coef, ob < nbytes ? g0 * 128u + ob : BUF_OOB, 0, 0);
+    const bool st = ob < nbytes && ((keep >> (ob >> 7)) & 1u);
+    __builtin_amdgcn_raw_buffer_store_b128(d, coef, st ? g0 * 128u + ob : BUF_OOB, 0, 0);
   }
   __builtin_amdgcn_wave_barrier();
   WAVE_FENCE();  // these reads before the staging is reused (idct_coded_blocks' slots)
 }
 __device__ __forceinline__ void mbg_store_levels(const p64gpu_encode_args &a, const uint8_t *lds, int lane,
-                                                 unsigned nmbs, unsigned gmb0, uint32_t nvalid) {
-  blk_store_levels(a, lds, lane, nmbs, 6u * gmb0, 6u * nvalid);
+                                                 unsigned nmbs, unsigned gmb0, uint32_t nvalid,
+                                                 uint64_t keep = ~0ull) {
+  blk_store_levels(a, lds, lane, nmbs, 6u * gmb0, 6u * nvalid, keep);
 }
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t recon_rsrc(const p64gpu_encode_args &a, const BlkDiv &kd,
                                                              unsigned nmbs) {
@@ -1226,7 +1229,8 @@ __global__ __launch_bounds__(64) OCC4 void k_inter_mbg(p64gpu_encode_args a, Blk
   // block with a nonzero level; no nonzero level at all -> MC without
   // coefficients (MTYPE 4 / 7), vector kept, CBP 0x3f
   const int sh = 6 * (l / 6);
-  const uint32_t big = (uint32_t)(__ballot(ss > 1) >> sh) & 63u, any = (uint32_t)(__ballot(ss > 0) >> sh) & 63u;
+  const uint64_t nz = __ballot(ss > 0);  // blocks with a nonzero level
+  const uint32_t big = (uint32_t)(__ballot(ss > 1) >> sh) & 63u, any = (uint32_t)(nz >> sh) & 63u;
   int cbp = 0x3f;
   bool repred = false;  // 2/3 -> 4 switches from the zero vector to the ME vector
   if (mt_cbp(mt)) {
@@ -1251,7 +1255,9 @@ __global__ __launch_bounds__(64) OCC4 void k_inter_mbg(p64gpu_encode_args a, Blk
   }
   // the levels leave first: the staging then holds idct_coded_blocks' slots
   const uint32_t nvalid = min((unsigned)MBS_PER_WAVE, nmbs - gmb0);
-  mbg_store_levels(a, lds, lane, nmbs, gmb0, nvalid);
+  // only blocks with a nonzero level are written (include/p64gpu.h): three
+  // quarters of the inter blocks have none (k_inter_mbg 49.1 -> 42.9 us, A/B x3)
+  mbg_store_levels(a, lds, lane, nmbs, gmb0, nvalid, nz);
   const int pw = pos.plane ? w >> 1 : w;
   const uint32_t ro = (uint32_t)((int64_t)pos.fi * stride) + (uint32_t)plane_offset(pos.plane, w, h) +
                       (uint32_t)mul24(pos.y, pw) + (uint32_t)pos.x;

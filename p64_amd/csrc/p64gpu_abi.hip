@@ -480,6 +480,9 @@ int p64gpu_encoder_frame(p64gpu_encoder *e, const uint8_t *picture, int intra, i
   HIP_TRY(hipSetDevice(e->device));
   HIP_TRY(hipMemcpyAsync(e->d_cur, picture, e->pic, hipMemcpyHostToDevice, e->stream));
   if (intra) HIP_TRY(hipMemsetAsync(e->d_li, 0, e->nmb, e->stream));
+  // the caller gets every block's levels: an inter picture writes only the
+  // blocks with a nonzero level (include/p64gpu.h), the rest are zero
+  if (!intra) HIP_TRY(hipMemsetAsync(e->d_coef, 0, (size_t)e->nmb * 384 * sizeof(int16_t), e->stream));
   if (mtype_override)
     HIP_TRY(hipMemcpyAsync(e->d_ov, mtype_override, e->nmb, hipMemcpyHostToDevice, e->stream));
   p64gpu_encode_args a;

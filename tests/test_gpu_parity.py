@@ -310,7 +310,7 @@ def test_split_encoder_without_me_output_and_in_graph(p64, torch_dev):
         li = torch.zeros(S * nmb, dtype=torch.uint8, device="cuda")
         bufs = [torch.zeros(S * pic, dtype=torch.uint8, device="cuda") for _ in range(2)]
         cur = [dev(torch, frames[t]) for t in range(T)]
-        outs = [p64.FrameBatchOut(coef=torch.empty((S, nmb, 6, 64), dtype=torch.int16, device="cuda"),
+        outs = [p64.FrameBatchOut(coef=torch.zeros((S, nmb, 6, 64), dtype=torch.int16, device="cuda"),
                                   mb=torch.empty((S, nmb, 4), dtype=torch.int8, device="cuda"),
                                   me=torch.empty((S, nmb, 7), dtype=torch.int32, device="cuda")
                                   if want_me else None) for _ in range(T)]
@@ -363,7 +363,7 @@ def test_encode_with_given_me_records(p64, torch_dev, mode, sl):
         got = []
         for t in range(T):
             ref, rec = bufs[t % 2], bufs[(t + 1) % 2]
-            o = p64.FrameBatchOut(coef=torch.empty((S, nmb, 6, 64), dtype=torch.int16, device="cuda"),
+            o = p64.FrameBatchOut(coef=torch.zeros((S, nmb, 6, 64), dtype=torch.int16, device="cuda"),
                                   mb=torch.empty((S, nmb, 4), dtype=torch.int8, device="cuda"),
                                   me=torch.empty((S, nmb, 7), dtype=torch.int32, device="cuda"))
             if given and t > 0:
@@ -417,7 +417,7 @@ def test_library_me_scratch_per_stream_and_graph_safe(p64, torch_dev):
     def outputs(S):
         return (torch.empty(S * pic, dtype=torch.uint8, device="cuda"),
                 torch.zeros(S * nmb, dtype=torch.uint8, device="cuda"),
-                torch.empty((S, nmb, 6, 64), dtype=torch.int16, device="cuda"),
+                torch.zeros((S, nmb, 6, 64), dtype=torch.int16, device="cuda"),
                 torch.empty((S, nmb, 4), dtype=torch.int8, device="cuda"))
 
     def expected(cur, ref, li, S):
@@ -508,7 +508,7 @@ def test_library_me_scratch_per_thread_stream(p64, torch_dev):
     def outputs():
         return (torch.empty(S * pic, dtype=torch.uint8, device="cuda"),
                 torch.zeros(S * nmb, dtype=torch.uint8, device="cuda"),
-                torch.empty((S, nmb, 6, 64), dtype=torch.int16, device="cuda"),
+                torch.zeros((S, nmb, 6, 64), dtype=torch.int16, device="cuda"),
                 torch.empty((S, nmb, 4), dtype=torch.int8, device="cuda"))
 
     want = []
@@ -642,6 +642,42 @@ def test_env_switches_same_bytes(torch_dev):
     ref = digest({})
     for sw in ({"P64GPU_FUSED": "1"},):
         assert digest(sw) == ref, sw
+
+
+def test_inter_levels_sparse_store(p64, oracle_mod, torch_dev):
+    """coef contract (include/p64gpu.h): an inter picture writes exactly the
+    blocks with a nonzero level; all-zero blocks keep what the buffer held.
+    Sentinel-filled output vs the oracle, with and without -o overrides (MC
+    types without coefficients write nothing)."""
+    torch = torch_dev
+    w, h, nmb = 176, 144, 99
+    rng = np.random.default_rng(11)
+    f0, f1 = p64.synth_frame(33, 0, w, h), p64.synth_frame(33, 1, w, h)
+    _, _, _, rec0 = oracle_mod.encode_frame(w, h, f0, None, np.zeros(nmb, np.uint8), intra=True, quant=8)
+    SENT = 0x5A5A
+    for ov in (None, rng.integers(-1, 10, nmb).astype(np.int8)):
+        for quant in (3, 8, 16):
+            li_o = np.zeros(nmb, np.uint8)
+            coef, mb, _, recon = oracle_mod.encode_frame(w, h, f1, rec0, li_o, intra=False, quant=quant,
+                                                          me_mode=p64.ME_FULL, search_limit=31,
+                                                          mtype_override=ov)
+            out = p64.FrameBatchOut(coef=torch.full((1, nmb, 6, 64), SENT, dtype=torch.int16, device="cuda"),
+                                    mb=torch.empty((1, nmb, 4), dtype=torch.int8, device="cuda"),
+                                    me=torch.empty((1, nmb, 7), dtype=torch.int32, device="cuda"))
+            rec_d = torch.zeros(w * h * 3 // 2, dtype=torch.uint8, device="cuda")
+            p64.encode_frames(dev(torch, f1), dev(torch, rec0), rec_d, dev(torch, np.zeros(nmb, np.uint8)),
+                              width=w, height=h, intra=False, quant=quant, me_mode=p64.ME_FULL,
+                              search_limit=31, mtype_override=dev(torch, ov) if ov is not None else None,
+                              out=out)
+            got = host(out.coef)[0].reshape(-1, 64)
+            want = coef.reshape(-1, 64)
+            nz = want.any(axis=1)
+            tag = f"q{quant} ov={ov is not None}"
+            assert 0 < nz.sum() < nz.size, tag  # both kinds present
+            np.testing.assert_array_equal(got[nz], want[nz], err_msg=tag)
+            assert (got[~nz] == SENT).all(), tag
+            np.testing.assert_array_equal(host(out.mb)[0].view(p64.MB_DTYPE).reshape(nmb), mb, err_msg=tag)
+            np.testing.assert_array_equal(host(rec_d), recon, err_msg=tag)
 
 
 def test_intra_refresh_and_override(p64, oracle_mod, torch_dev):
