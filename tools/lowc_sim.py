@@ -12,6 +12,8 @@ min(SAD(c*), SAD(0,0)) with c* the least-bound candidate, and the survivors
   rowcol   max(rows, cols)
   s44      sum over the 16 4x4 sub-blocks of |sum cur - sum candidate|
   s22      the same over the 64 2x2 sub-blocks
+  p8       the partial SAD of rows 0..7
+  p8s44    p8 + the s44 terms of sub-block rows 2..3
 usage: python tools/lowc_sim.py [pictures]"""
 import os
 import sys
@@ -42,7 +44,7 @@ def blocksum(B, k):
     return B.reshape(16 // k, k, 16 // k, k).sum((1, 3))
 
 
-stats = {k: [] for k in ("rows", "cols", "rowcol", "s44", "s22")}
+stats = {k: [] for k in ("rows", "cols", "rowcol", "s44", "s22", "p8", "p8s44")}
 for seed in (7, 15):
     frames = [p64_amd.synth_frame(seed, t, W, H) for t in range(NP)]
     outs = oracle.encode_sequence(frames, W, H, quant=8, me_mode=oracle.ME_FULL, search_limit=31)
@@ -67,6 +69,9 @@ for seed in (7, 15):
                 b["rowcol"][(dx, dy)] = max(rr, cc)
                 b["s44"][(dx, dy)] = int(np.abs(blocksum(C, 4) - blocksum(Rb, 4)).sum())
                 b["s22"][(dx, dy)] = int(np.abs(blocksum(C, 2) - blocksum(Rb, 2)).sum())
+                p8 = int(np.abs(C[:8] - Rb[:8]).sum())
+                b["p8"][(dx, dy)] = p8
+                b["p8s44"][(dx, dy)] = p8 + int(np.abs(blocksum(C, 4)[2:] - blocksum(Rb, 4)[2:]).sum())
             s00 = sad.get((0, 0), 1 << 30)
             for k in stats:
                 bb = b[k]
