@@ -349,7 +349,8 @@ def MotionEstimation(ref, cur, width: int, height: int, mode: int = ME_TSS,
 
 @dataclass
 class FrameBatchOut:
-    coef: object        # int16 [nframes, nmb, 6, 64]
+    coef: object        # int16 [nframes, nmb, 6, 64]; inter pictures write only the
+                        # blocks with a nonzero level (include/p64gpu.h)
     mb: object          # int8  [nframes, nmb, 4]  (mtype, cbp, mvx, mvy)
     me: object          # int32 [nframes, nmb, 7] or None
 
