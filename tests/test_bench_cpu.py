@@ -33,3 +33,18 @@ def test_cpu_baseline_4cif_is_the_port():
     r = out["inter"]
     assert r["kind"] == "port" and r["cores"] == 1
     assert "cannot encode 4CIF" in r["sample"]
+
+
+def test_level_byte_accounting():
+    """coded_level_bytes: 128 bytes per transmitted block (MTYPE with
+    coefficients; CBP bit for the MTYPEs that carry one, all six otherwise);
+    decode_bytes adds records, prediction source and recon on top."""
+    import torch
+    # (mtype, cbp): intra 0 (six blocks), inter 2 with cbp 0b100001 (two),
+    # MC-only 4 (none), MC+coef 5 with cbp 0x3f (six), MQUANT intra 1 (six)
+    mb = torch.tensor([[0, 0x3f, 0, 0], [2, 0x21, 0, 0], [4, 0x3f, 1, 1], [5, 0x3f, 2, 0],
+                       [1, 0, 0, 0]], dtype=torch.int8)
+    assert bench.coded_level_bytes(torch, mb) == 128 * (6 + 2 + 0 + 6 + 6)
+    n = mb.shape[0]
+    inter = 3  # mtypes >= 2
+    assert bench.decode_bytes(torch, mb, n) == 6 * n + 128 * 20 + 384 * inter + 384 * n
