@@ -26,10 +26,14 @@ scratch outputs, replayed for --spinup-ms (timed_region).  The default `inter` r
 configs on the same pictures and reports them under "configs" (each with its own
 roofline), so one driver run carries all three kernels.
 
-`--content` picks the input: synth (the seeded texture generator, default),
-pan15 (texture panned +-15 px per picture: the search range edge), noise
-(uniform random bytes: nothing prunes) or flat (constant planes: SAD ties
-everywhere) -- the stress sets of SURVEY.md 8(d).
+`--content` picks the input: survey (default: SURVEY.md 8(d)'s content --
+128 + 50 sin(x/7) cos(y/11) + 30 sin((x+y)/23) + N(0,12) texture translated by
+(+3,-2) px per picture + N(0,4) temporal noise, seeds 1..S), synth (the
+builder's value-noise generator: per-seed motion, weaker temporal noise,
+scene-cut / noise-free / low-contrast seed classes), pan15 (texture panned
++-15 px per picture: the search range edge), noise (uniform random bytes:
+nothing prunes) or flat (constant planes: SAD ties everywhere) -- the stress
+sets of SURVEY.md 8(d).
 
 Multi-GPU: `--gpus N` without a launcher starts N ranks itself (torch
 distributed run as a child process, before any GPU call); under a launcher
@@ -73,7 +77,8 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
 SAD_PEAK = 256 * 4 * 16 * 4 * 2.4e9
 # algorithmic HBM bytes per macroblock:
 #   inter: read cur 384 + previous recon 384 + last_intra 1;
-#          write recon 384 + p64_mb_rec 4 + p64_me_rec 28 + last_intra 1, and
+#          write recon 384 + p64_mb_rec 4 + p64_me_rec 28 + last_intra 1 +
+#          nonzero-block mask 1, and
 #          128 per transmitted block (MTYPE with coefficients, CBP bit set:
 #          counted from the last step's records, coded_level_bytes; the kernel
 #          writes every block with a nonzero level, include/p64gpu.h)
@@ -81,13 +86,13 @@ SAD_PEAK = 256 * 4 * 16 * 4 * 2.4e9
 #   decode: per MB record 4 + UseQuant 1 + coded flag 1, 128 per coded block,
 #          384 prediction source if not intra, 384 recon write (counted exactly
 #          from the records of each launch, see decode_bytes)
-BYTES_PER_MB_FIXED = 384 + 384 + 1 + 384 + 4 + 28 + 1
+BYTES_PER_MB_FIXED = 384 + 384 + 1 + 384 + 4 + 28 + 1 + 1
 READ_BYTES_PER_MB = 384 + 384 + 1
 INTRA_BYTES_PER_MB = 384 + 768 + 384 + 4 + 1
 # per-kernel means over the timed region of the driver's command (rocprofv3
 # --kernel-trace of `bench.py --steps 20 --warmup 5 --no-cpu`, reduced by
 # tools/timed_region.py --json; the spin-up's replays are outside the region)
-PROFILE_TIMED = "profiles/r04_timed_region.json"
+PROFILE_TIMED = "profiles/r05_timed_region.json"  # {workload key: {kernel: mean us}}
 # executed v_sad_u8 work of k_motion per launch (tools/sad_count.py side build)
 PROFILE_SAD = "profiles/sad_executed.json"
 MAX_SLOTS = 256  # distinct input pictures per sequence kept resident (~10 GB at S=256 CIF)
@@ -100,7 +105,7 @@ def parse(argv=None):
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--config", choices=("inter", "intra", "decode", "4cif"), default="inter")
     p.add_argument("--mode", choices=("full", "tss"), default="full")
-    p.add_argument("--content", choices=("synth", "pan15", "noise", "flat"), default="synth")
+    p.add_argument("--content", choices=("survey", "synth", "pan15", "noise", "flat"), default="survey")
     p.add_argument("--search-limit", type=int, default=31)
     p.add_argument("--quant", type=int, default=8)
     p.add_argument("--width", type=int, default=None)
@@ -331,7 +336,8 @@ def cpu_baselines(args, legs):
                      "-i", str(args.search_limit), *extra, os.path.join(td, f"s{k}"), "-z", ".y4m",
                      "-s", os.path.join(td, f"s{k}.p64")] for k in range(n)]
         desc = (f"{nfr}-picture {w}x{h} y4m sequence per process (content {args.content}, host "
-                f"generator{'' if args.content == 'synth' else ' of the same kind'}), q={args.quant}")
+                f"generator{'' if args.content in ('survey', 'synth') else ' of the same kind'}), "
+                f"q={args.quant}")
         if "inter" in legs or "decode" in legs:
             me = "FastBME SL=%d" % args.search_limit if args.mode == "full" else "StepBME (TSS)"
             env_i = dict(env, P64REF_ME="full") if args.mode == "full" else env
@@ -360,13 +366,13 @@ def cpu_baselines(args, legs):
 
 
 def host_frames(p64_amd, content, seed, n, w, h):
-    """Host pictures for the CPU legs: the synth generator (the same bytes as the
-    device one), or the stress contents of make_inputs in kind -- uniform noise,
+    """Host pictures for the CPU legs: the survey or synth generator (the same
+    bytes as the device one), or the stress contents of make_inputs in kind -- uniform noise,
     one constant per sequence, picture 0 panned by +-15 px per picture with
     +-3 noise (numpy, seeded; the device versions draw from torch's generator)."""
     import numpy as np
-    if content == "synth":
-        return [p64_amd.synth_frame(seed, t, w, h) for t in range(n)]
+    if content in p64_amd.CONTENTS:
+        return [p64_amd.synth_frame(seed, t, w, h, content=p64_amd.CONTENTS[content]) for t in range(n)]
     pic = w * h * 3 // 2
     rng = np.random.default_rng(1000 + seed)
     if content == "noise":
@@ -412,14 +418,14 @@ def cpu_port(args, p64_amd, w, h, nmb):
 # inputs
 
 def make_inputs(torch, p64_amd, content, w, h, seed0, S, nslots):
-    """[nslots][S][picture] uint8 on the device.  synth: the seeded integer
-    generator (same bytes as the host one the CPU legs use); the stress sets are
+    """[nslots][S][picture] uint8 on the device.  survey / synth: the seeded
+    integer generators (same bytes as the host ones the CPU legs use); the stress sets are
     generated on the device with torch (seeded): pan15 = picture 0 of the synth
     sequence translated by (+-15, +-15) px per picture (wrapping), plus
     uniform +-3 noise; noise = uniform bytes; flat = one constant per sequence."""
     pic = w * h * 3 // 2
-    if content == "synth":
-        return p64_amd.synth_frames_device(w, h, seed0, S, 0, nslots)
+    if content in p64_amd.CONTENTS:
+        return p64_amd.synth_frames_device(w, h, seed0, S, 0, nslots, content=p64_amd.CONTENTS[content])
     g = torch.Generator(device="cuda")
     g.manual_seed(1000 + seed0)
     if content == "noise":
@@ -461,6 +467,13 @@ def inter_kernel_name(q):
     """k_inter_mbg's instance for a uniform q without overrides
     (p64k::inter_mbg): <QMB, OVR, POW2>"""
     return "k_inter_mbg<false, false, %s>" % ("true" if _pow2_quant(q) else "false")
+
+
+def content_key(args, base):
+    """Key of a workload in the tracked profiles (PMC passes, rocprof timed
+    regions, executed SAD counts): the builder's synth content has none, the
+    others their name."""
+    return base if args.content == "synth" else f"{base}_{args.content}"
 
 
 def load_pmc(path, workload_key):
@@ -702,14 +715,22 @@ def main(argv=None):
         rec = [torch.zeros(S * pic, dtype=torch.uint8, device="cuda") for _ in range(2)]
         li = torch.zeros(S * nmb, dtype=torch.uint8, device="cuda")
         # levels and records of every step stay resident when the decode config
-        # is measured from them afterwards (nslots x 78 MB at S=256 CIF)
-        ncoef = nslots if keep else 1
-        coef_all = torch.empty((ncoef, S, nmb, 6, 64), dtype=torch.int16, device="cuda")
+        # is measured from them afterwards (nslots x 78 MB at S=256 CIF);
+        # otherwise the checked pictures (vt, last) get level buffers of their
+        # own.  The level buffers start as LEVEL_SENTINEL: an inter picture
+        # stores exactly the blocks its nonzero-block mask names
+        # (include/p64gpu.h), so every other block must still hold it.
+        vt, last = args.warmup, args.warmup + args.steps
+        ncoef = nslots if keep else 3
+        coef_all = torch.full((ncoef, S, nmb, 6, 64), LEVEL_SENTINEL, dtype=torch.int16, device="cuda")
+        nz_all = torch.empty((ncoef, S, nmb), dtype=torch.uint8, device="cuda")
         mb_all = torch.empty((ncoef, S, nmb, 4), dtype=torch.int8, device="cuda")
         me = torch.empty((S, nmb, 7), dtype=torch.int32, device="cuda")
         def out_of(t):
-            i = slot(t) if keep else 0
-            return p64_amd.FrameBatchOut(coef=coef_all[i], mb=mb_all[i], me=me)
+            i = slot(t) if keep else (1 if t == vt else (2 if t == last else 0))
+            return p64_amd.FrameBatchOut(coef=coef_all[i], mb=mb_all[i], me=me, nz=nz_all[i])
+        # the checked pictures' buffers were written by no earlier step
+        fresh = {t: (not keep) or (1 + args.warmup + args.steps <= nslots) for t in (vt, last)}
 
         def pre(t):  # --feed root: this step's pictures from rank 0
             scatter_pictures(world, rank, all_frames[slot(t)] if rank == 0 else None, frames[slot(t)])
@@ -739,7 +760,8 @@ def main(argv=None):
             sp["rec"] = [torch.empty_like(r) for r in rec]
             sp["li"] = torch.empty_like(li)
             sp["out"] = p64_amd.FrameBatchOut(coef=torch.empty_like(coef_all[0]),
-                                              mb=torch.empty_like(mb_all[0]), me=torch.empty_like(me))
+                                              mb=torch.empty_like(mb_all[0]), me=torch.empty_like(me),
+                                              nz=torch.empty_like(nz_all[0]))
 
         def spin_reset():
             for a, b in zip(sp["rec"], rec):
@@ -754,7 +776,8 @@ def main(argv=None):
         def spin_out(k):  # scratch outputs with step k's own ME records
             if "mes" not in sp:
                 sp["mes"] = [torch.empty_like(me) for _ in range(args.steps)]
-            return p64_amd.FrameBatchOut(coef=sp["out"].coef, mb=sp["out"].mb, me=sp["mes"][k])
+            return p64_amd.FrameBatchOut(coef=sp["out"].coef, mb=sp["out"].mb, me=sp["mes"][k],
+                                         nz=sp["out"].nz)
 
         def spin_full(t, k):  # the whole step, its ME records kept
             p64_amd.encode_frames(frames[slot(t)].reshape(-1), sp["rec"][(t + 1) % 2], sp["rec"][t % 2],
@@ -767,17 +790,14 @@ def main(argv=None):
                                   me_mode=mode, search_limit=args.search_limit, out=spin_out(k),
                                   me_given=True)
 
-        vt = args.warmup
         for t in range(1 + args.warmup):  # intra picture + warmup, untimed
-            if t == vt:  # the checked picture's level array whole (only blocks with
-                out_of(t).coef.zero_()  # a nonzero level are written, include/p64gpu.h)
             step(t)
-        # snapshot of sequence 0 after the warmup: checked against the oracle
-        snap = None
+        # the checked sequences (VERIFY_SEQS: one of each synth seed class) after
+        # the warmup, checked against the oracle after the timed region
+        seqs = [i for i in VERIFY_SEQS if i < S]
+        snap = {}
         if rank == 0 and not args.no_verify:
-            o = out_of(vt)
-            snap = (o.coef[0].cpu().numpy(), o.mb[0].cpu().numpy(), me[0].cpu().numpy(),
-                    rec[vt % 2][:pic].cpu().numpy())
+            snap[vt] = snapshot(out_of(vt), me, rec[vt % 2], seqs, pic)
         t_first = 1 + args.warmup
         elapsed, kavg, clk = timed_region(torch, dist, world, args.steps, t_first, launch,
                                           pre if root else None, post if root else None,
@@ -787,35 +807,18 @@ def main(argv=None):
                                                 "split": (kme, kin, spin_full, spin_rest)})
         sp.clear()
         tmax = max_over_ranks(elapsed, world, device="cuda")
-        last = t_first + args.steps - 1
+        assert last == t_first + args.steps - 1
         lvl_bytes = coded_level_bytes(torch, out_of(last).mb)  # (the last step's records)
 
         verified, ok = None, True
         if rank == 0 and not args.no_verify:
-            import oracle
             # closed loop: every picture feeds the next, so matching one picture's
             # outputs and reconstruction pins the whole chain before it
-            checks = [(vt, snap)]
-            if nmb * (last + 1) <= 100_000:  # whole run (~20 s of oracle on CIF FULL)
-                o = out_of(last)
-                checks.append((last, (o.coef[0].cpu().numpy(), o.mb[0].cpu().numpy(),
-                                      me[0].cpu().numpy(), rec[last % 2][:pic].cpu().numpy())))
-            upto = max(t for t, _ in checks)
+            if nmb * (last + 1) <= VERIFY_MAX_MBS:
+                snap[last] = snapshot(out_of(last), me, rec[last % 2], seqs, pic)
             src = all_frames if root else frames
-            fr0 = [src[slot(t), 0].cpu().numpy() for t in range(upto + 1)]
-            outs = oracle.encode_sequence(fr0, w, h, quant=args.quant, me_mode=mode,
-                                          search_limit=args.search_limit)
-            for t, (gc, gm, ge, gr) in checks:
-                coef, mb, mev, recon = outs[t]
-                if t != vt:  # a reused level buffer: the blocks with a nonzero level
-                    nzb = coef.reshape(-1, 64).any(axis=1)
-                    gc, coef = gc.reshape(-1, 64)[nzb], coef.reshape(-1, 64)[nzb]
-                ok = ok and bool(np.array_equal(gc, coef)
-                                 and np.array_equal(gm.view(p64_amd.MB_DTYPE).reshape(nmb), mb)
-                                 and np.array_equal(ge.view(p64_amd.ME_DTYPE).reshape(nmb), mev)
-                                 and np.array_equal(gr, recon))
-            verified = {"ok": ok, "pictures_checked": [t for t, _ in checks],
-                        "note": "sequence 0 vs the CPU oracle (closed loop from picture 0)"}
+            verified = verify_sequences(args, p64_amd, src, slot, seqs, snap, fresh, w, h, mode)
+            ok = verified["ok"]
         if not all_ranks_ok(ok, world, device="cuda"):
             raise SystemExit("bench: GPU output differs from the oracle -- refusing to report")
 
@@ -845,19 +848,18 @@ def main(argv=None):
         me_name = "FULL FastBME SL=%d" % args.search_limit if args.mode == "full" else "TSS StepBME"
         workload = (f"{w}x{h} inter, {me_name}, q={args.quant}, content {args.content}, "
                     f"closed loop, {S} sequences/GPU")
-        key = f"{w}x{h}_{args.mode}{args.search_limit}_q{args.quant}_S{S}" + \
-            ("" if args.content == "synth" else f"_{args.content}")
+        key = content_key(args, f"{w}x{h}_{args.mode}{args.search_limit}_q{args.quant}_S{S}")
         pmc = load_pmc(args.pmc_json, key)
         pmc_me, pmc_in = load_pmc(args.pmc_json, key + "_me"), load_pmc(args.pmc_json, key + "_inter")
         if os.environ.get("P64GPU_FUSED", "0") in ("", "0"):  # split: k_motion, k_inter_mbg
             kernel = f"{kme} + {kin} (one step)"
-            prof = load_json(os.path.join(REPO, PROFILE_TIMED)) or {}
+            prof = (load_json(os.path.join(REPO, PROFILE_TIMED)) or {}).get(key) or {}
             split = {"dominant": kme,
                      "dominant_note": "k_motion is VALU-bound (roofline_sad_executed, valu_busy); the "
                                       "HBM roofline is taken over the whole step, both kernels",
                      "kernels_us_live": clk.get("kernels_us_live"),
-                     "kernels_us_rocprof": ({k: prof[k] for k in (kme, kin)} if key.endswith("S256") and
-                                            all(k in prof for k in (kme, kin)) else None),
+                     "kernels_us_rocprof": ({k: prof[k] for k in (kme, kin)}
+                                            if all(k in prof for k in (kme, kin)) else None),
                      "kernels_us_rocprof_source": f"{PROFILE_TIMED} (rocprofv3 --kernel-trace of "
                                                   "`bench.py --steps 20 --warmup 5 --no-cpu`, timed "
                                                   "region only: tools/timed_region.py)"}
@@ -925,7 +927,8 @@ def main(argv=None):
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "u8",
-        "data": f"synthetic ({args.content}: seeded, generated on device)",
+        "data": (f"synthetic ({args.content}: seeded, generated on device"
+                 + ("; SURVEY.md 8(d)'s texture, motion and noise" if args.content == "survey" else "") + ")"),
     }
     line.update(result)
     line["ranks"] = ranks
@@ -935,6 +938,67 @@ def main(argv=None):
                                   "with entropy coding (value stops at the levels)")
     line["cpu_baseline"] = cpu
     print(json.dumps(line), flush=True)
+
+
+LEVEL_SENTINEL = 0x5A5A  # never a level: H.261 levels are |l| <= 127 (DC 1..254)
+# the sequences bench.py checks against the oracle: seeds 1, 5, 6, 7 -- with
+# --content synth one of each generator class (plain, scene cut at picture 12,
+# noise-free, low contrast: the dense-search class, synth_impl.h)
+VERIFY_SEQS = (0, 4, 5, 6)
+VERIFY_MAX_MBS = 120_000  # per sequence: the last picture is checked up to this run length
+
+
+def snapshot(o, me, recon, seqs, pic):
+    """Host copies of the checked sequences' outputs of one picture."""
+    return {s: (o.coef[s].cpu().numpy(), o.nz[s].cpu().numpy(), o.mb[s].cpu().numpy(),
+                me[s].cpu().numpy(), recon[s * pic:(s + 1) * pic].cpu().numpy()) for s in seqs}
+
+
+def verify_sequences(args, p64_amd, src, slot, seqs, snap, fresh, w, h, mode):
+    """The checked sequences against the CPU oracle (closed loop from picture
+    0), one host thread per sequence (the oracle's C code runs without the
+    GIL).  Per checked picture: MB records, ME records and reconstruction
+    equal; the levels rebuilt through the nonzero-block mask (a set bit: the
+    stored block, else 64 zeros) equal the oracle's whole inputbuf array
+    (p64.c:823-913); the mask names exactly the oracle's blocks with a nonzero
+    level; and blocks outside the mask still hold LEVEL_SENTINEL (the buffer
+    was written by no other step), so nothing else was stored."""
+    import oracle
+    from concurrent.futures import ThreadPoolExecutor
+    nmb = (w // 16) * (h // 16)
+    upto = max(snap)
+    oracle.lib()  # loaded (and its tables built) before the threads start
+
+    def one(s):
+        fr = [src[slot(t), s].cpu().numpy() for t in range(upto + 1)]
+        outs = oracle.encode_sequence(fr, w, h, quant=args.quant, me_mode=mode,
+                                      search_limit=args.search_limit)
+        res = {}
+        for t, per in snap.items():
+            gc, gnz, gm, ge, gr = per[s]
+            coef, mb, mev, recon = outs[t]
+            bits = (gnz[:, None] >> (5 - np.arange(6))[None, :]) & 1  # [nmb, 6]
+            want_nz = coef.reshape(nmb, 6, 64).any(axis=2)
+            rebuilt = np.where(bits[:, :, None] == 1, gc, 0)
+            checks = {"levels_via_mask": bool(np.array_equal(rebuilt, coef)),
+                      "mask": bool(np.array_equal(bits == 1, want_nz)),
+                      "mb": bool(np.array_equal(gm.view(p64_amd.MB_DTYPE).reshape(nmb), mb)),
+                      "me": mev is None or bool(np.array_equal(ge.view(p64_amd.ME_DTYPE).reshape(nmb), mev)),
+                      "recon": bool(np.array_equal(gr, recon))}
+            if fresh.get(t):
+                checks["untouched_blocks_sentinel"] = bool((gc[bits == 0] == LEVEL_SENTINEL).all())
+            res[t] = checks
+        return s, res
+
+    with ThreadPoolExecutor(len(seqs)) as ex:
+        got = dict(ex.map(one, seqs))
+    ok = all(all(c.values()) for r in got.values() for c in r.values())
+    return {"ok": ok, "pictures_checked": sorted(snap), "sequences_checked": [1 + s for s in seqs],
+            "failed": {f"seed{1 + s}_t{t}": [k for k, v in c.items() if not v]
+                       for s, r in got.items() for t, c in r.items() if not all(c.values())},
+            "note": "per sequence (seed) vs the CPU oracle, closed loop from picture 0: records, "
+                    "reconstruction, the whole level array rebuilt through the nonzero-block mask, "
+                    "the mask itself, and the sentinel in every block the mask leaves out"}
 
 
 def load_json(path):
@@ -955,7 +1019,7 @@ def sad_executed(args, key, kme, clk, mbs):
     us = (clk.get("kernels_us_live") or {}).get(kme)
     src = "live"
     if us is None:
-        us = (load_json(os.path.join(REPO, PROFILE_TIMED)) or {}).get(kme)
+        us = ((load_json(os.path.join(REPO, PROFILE_TIMED)) or {}).get(key) or {}).get(kme)
         src = PROFILE_TIMED
     if not cnt or not us or args.mode != "full":
         return None
@@ -1081,7 +1145,7 @@ def run_intra(args, torch, dist, np, p64_amd, world, frames, S, nmb, pic, nslots
     if not all_ranks_ok(verified is not False, world, device="cuda"):
         raise SystemExit("bench: intra output differs from the oracle -- refusing to report")
     mbs = S * nmb
-    key = f"{w}x{h}_intra_q{args.quant}_S{S}"
+    key = content_key(args, f"{w}x{h}_intra_q{args.quant}_S{S}")
     return {"metric": METRICS["intra"], "value": round(aggregate_rate(world, mbs, args.steps, tmax), 1),
             "ms_per_step": round(tmax / args.steps * 1e3, 4),
             "config": {"workload": f"{w}x{h} intra pictures, q={args.quant}, content {args.content}, "
@@ -1162,7 +1226,7 @@ def run_decode(args, torch, dist, np, p64_amd, world, enc, S, nmb, pic):
         raise SystemExit("bench: decoded pictures differ from the encoder's reconstruction")
     mbs = S * nmb
     bpl = sum(nbytes) / len(nbytes)
-    key = f"{w}x{h}_decode_q{args.quant}_S{S}"
+    key = content_key(args, f"{w}x{h}_decode_q{args.quant}_S{S}")
     return {"metric": METRICS["decode"], "value": round(aggregate_rate(world, mbs, args.steps, tmax), 1),
             "ms_per_step": round(tmax / args.steps * 1e3, 4),
             "config": {"workload": f"{w}x{h} decoder reconstruction of a GPU-encoded stream "

@@ -41,8 +41,17 @@
  * index Bpos() yields in the MDU loop, io.c:757-783); GOB order is the host
  * writer's business.  Per macroblock, blocks c = 0..3 are luma
  * (h,v) = (0,0),(1,0),(0,1),(1,1), c = 4 is U, c = 5 is V (p64.c:77-79).
- * Coefficients are int16 levels in zigzag order, [mb][6][64], exactly as
- * ReadCompressMDU leaves inputbuf (p64.c:885) -- i.e. before CBP zeroing.
+ * Coefficients are int16 levels in zigzag order, [mb][6][64]: the values
+ * ReadCompressMDU leaves in inputbuf (p64.c:823-913), i.e. before CBP zeroing.
+ * An inter picture stores only the blocks holding a nonzero level; the
+ * optional nzmask output names them (bit 5-b for block b, the CBP bit order),
+ * so inputbuf is exactly: block b's stored levels if its bit is set, else 64
+ * zeros (p64gpu_encode_args.coef / .nzmask).
+ *
+ * ABI version 2 (round 5): p64gpu_encode_args.nzmask (appended); the sparse
+ * inter level store of version 1's last revision, now with that mask;
+ * p64gpu_vlc_args.flags (was `reserved`, must be 0 or P64GPU_VLC_*) and its
+ * scratch of 6*nframes*nmb uint32, 8-byte aligned; synthetic contents.
  */
 #ifndef P64GPU_H
 #define P64GPU_H
@@ -54,7 +63,7 @@
 extern "C" {
 #endif
 
-#define P64GPU_ABI_VERSION 1
+#define P64GPU_ABI_VERSION 2
 
 enum p64gpu_status {
   P64GPU_OK = 0,
@@ -164,11 +173,17 @@ typedef struct {
                              every block of an intra picture; of an inter
                              picture every block with a nonzero level, a
                              block whose 64 levels are all zero is left as
-                             it was (zero the buffer for the whole array;
-                             every block the MB record's CBP and MTYPE
-                             transmit has a nonzero level)                  */
+                             it was (zero the buffer for the whole array, or
+                             read it through nzmask; every block the MB
+                             record's CBP and MTYPE transmit has a nonzero
+                             level)                                         */
   p64_mb_rec *mb;         /* [nframes][nmb], written                         */
   p64_me_rec *me;         /* NULL or [nframes][nmb], written (inter only)    */
+  uint8_t *nzmask;        /* NULL or [nframes][nmb], written: bit 5-b set iff
+                             block b has a nonzero level (then its levels
+                             were stored; clear: the block's levels are all
+                             zero).  Intra pictures: 0x3f (the intra DC is
+                             1..254)                                         */
 } p64gpu_encode_args;
 
 /* Alignment: cur, ref, recon and coef 16 bytes; mb and me 4 bytes (the
@@ -216,9 +231,12 @@ int p64gpu_decode_recon(int width, int height, int nframes, int64_t frame_stride
  * byte -- the bit position the sequence's stream has reached -- so the host
  * appends it by OR-ing the first byte into its pending byte.  bits[i] receives
  * the bit count including the phase, or 0xFFFFFFFF if a record was invalid.
- * All pointers are device pointers; scratch holds 6*nframes*nmb uint32. */
+ * All pointers are device pointers; scratch holds 6*nframes*nmb uint32 and is
+ * 8-byte aligned, coef 16-byte, mb 4-byte (else P64GPU_E_INVALID).  Batches
+ * whose levels exceed 2 GiB are coded in several launches. */
 typedef struct {
-  int width, height, nframes, reserved;
+  int width, height, nframes;
+  int flags;                /* 0 (was `reserved` before ABI version 2)        */
   const p64_mb_rec *mb;     /* [nframes][nmb] raster order (encoder output)   */
   const int16_t *coef;      /* [nframes][nmb][6][64] zigzag levels            */
   const uint8_t *gquant;    /* [nframes][ngob] GQUANT of each GOB header      */
@@ -228,7 +246,7 @@ typedef struct {
   uint8_t *out;             /* [nframes][out_stride], zeroed by the call      */
   int64_t out_stride;       /* >= p64gpu_vlc_max_bytes, multiple of 4         */
   uint32_t *bits;           /* [nframes]                                      */
-  uint32_t *scratch;        /* [6][nframes][nmb]                              */
+  uint32_t *scratch;        /* [6][nframes][nmb], 8-byte aligned              */
 } p64gpu_vlc_args;
 int64_t p64gpu_vlc_max_bytes(int width, int height);
 int p64gpu_vlc_pictures(const p64gpu_vlc_args *args, void *stream);
@@ -247,16 +265,30 @@ int p64gpu_encoder_frame(p64gpu_encoder *enc, const uint8_t *picture, int intra,
 void p64gpu_encoder_close(p64gpu_encoder *enc);
 
 /* ---- deterministic synthetic input (integer only) ----------------------- */
+/* Two contents:
+ *   P64_SYNTH_VNOISE  value-noise texture, per-seed motion in [-3,3]x[-2,2],
+ *                     small temporal noise; seed classes mod 8: 5 scene cut at
+ *                     picture 12, 6 noise-free, 7 low contrast (synth.c)
+ *   P64_SYNTH_SURVEY  SURVEY.md 8(d): 128 + 50 sin(x/7) cos(y/11)
+ *                     + 30 sin((x+y)/23) + N(0,12) texture translated by
+ *                     (+3,-2) px per picture + N(0,4) temporal noise; chroma
+ *                     from the 2x2-averaged luma (synth_impl.h)            */
+enum p64_synth_content { P64_SYNTH_VNOISE = 0, P64_SYNTH_SURVEY = 1 };
 /* Host: picture `frame` of stream `seed` (Y|U|V, w*h*3/2 bytes). */
-void p64_synth_motion(uint32_t seed, int *mvx, int *mvy);
+void p64_synth_motion(uint32_t seed, int *mvx, int *mvy); /* VNOISE only */
 void p64_synth_frame(uint32_t seed, int frame, int width, int height,
-                     uint8_t *out);
+                     uint8_t *out); /* = p64_synth_frame_content(VNOISE, ...) */
+int p64_synth_frame_content(int content, uint32_t seed, int frame, int width,
+                            int height, uint8_t *out);
 /* Device: the same bytes for nslots x nseeds pictures, slot-major: picture
- * (t, s) = p64_synth_frame(seed0 + s, frame0 + t) at out + (t*nseeds + s)*stride.
- * nseeds*nslots <= 65535. */
+ * (t, s) = p64_synth_frame_content(content, seed0 + s, frame0 + t) at
+ * out + (t*nseeds + s)*stride.  nseeds*nslots <= 65535. */
 int p64gpu_synth_frames(int width, int height, uint32_t seed0, int nseeds,
                         int frame0, int nslots, int64_t frame_stride,
-                        uint8_t *out, void *stream);
+                        uint8_t *out, void *stream); /* VNOISE */
+int p64gpu_synth_content(int content, int width, int height, uint32_t seed0,
+                         int nseeds, int frame0, int nslots,
+                         int64_t frame_stride, uint8_t *out, void *stream);
 
 /* Clock probe (measurement aid; no reference counterpart): runs
  * v_sad_u8 chains on every SIMD for `microseconds`, then reports the median

@@ -35,6 +35,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # P64GPU_LIB lets development A/B runs point at an alternative build.
 LIB_PATH = os.environ.get("P64GPU_LIB", os.path.join(_HERE, "libp64gpu.so"))
 
+ABI_VERSION = 2  # include/p64gpu.h P64GPU_ABI_VERSION
 ME_TSS = 0
 ME_FULL = 1
 
@@ -73,7 +74,7 @@ class EncodeArgs(ctypes.Structure):
         ("cur", ctypes.c_void_p), ("ref", ctypes.c_void_p), ("recon", ctypes.c_void_p),
         ("last_intra", ctypes.c_void_p), ("quant_mb", ctypes.c_void_p),
         ("mtype_override", ctypes.c_void_p), ("coef", ctypes.c_void_p),
-        ("mb", ctypes.c_void_p), ("me", ctypes.c_void_p),
+        ("mb", ctypes.c_void_p), ("me", ctypes.c_void_p), ("nzmask", ctypes.c_void_p),
     ]
 
 
@@ -119,6 +120,8 @@ def lib() -> ctypes.CDLL:
     L.p64gpu_encoder_close.argtypes = [vp]
     L.p64gpu_encoder_close.restype = None
     L.p64gpu_synth_frames.argtypes = [i32, i32, ctypes.c_uint32, i32, i32, i32, i64, vp, vp]
+    L.p64gpu_synth_content.argtypes = [i32, i32, i32, ctypes.c_uint32, i32, i32, i32, i64, vp, vp]
+    L.p64_synth_frame_content.argtypes = [i32, ctypes.c_uint32, i32, i32, i32, vp]
     L.p64gpu_clock_probe.argtypes = [i32, ctypes.POINTER(i32), vp]
     L.p64_synth_frame.argtypes = [ctypes.c_uint32, i32, i32, i32, vp]
     L.p64_synth_frame.restype = None
@@ -167,7 +170,7 @@ def lib() -> ctypes.CDLL:
     L.p64prog_execute.argtypes = [vp, i32]
     L.p64prog_memory.argtypes = [vp]
     L.p64prog_memory.restype = ctypes.POINTER(ctypes.c_double)
-    if L.p64gpu_abi_version() != 1:
+    if L.p64gpu_abi_version() != ABI_VERSION:
         raise P64GpuError("libp64gpu.so ABI version mismatch")
     _lib = L
     return L
@@ -197,9 +200,18 @@ def picture_bytes(width: int, height: int) -> int:
     return width * height * 3 // 2
 
 
-def synth_frame(seed: int, frame: int, width: int, height: int) -> np.ndarray:
+# synthetic contents (include/p64gpu.h p64_synth_content)
+SYNTH_VNOISE, SYNTH_SURVEY = 0, 1
+CONTENTS = {"synth": SYNTH_VNOISE, "survey": SYNTH_SURVEY}
+
+
+def synth_frame(seed: int, frame: int, width: int, height: int, content: int = SYNTH_VNOISE) -> np.ndarray:
+    """Picture `frame` of synthetic stream `seed` (host, integer only).
+    content SYNTH_VNOISE: the value-noise texture (seed classes mod 8);
+    SYNTH_SURVEY: SURVEY.md 8(d)'s sinusoid texture + N(0,12), (+3,-2) px
+    per picture, N(0,4) temporal noise."""
     out = np.empty(picture_bytes(width, height), np.uint8)
-    lib().p64_synth_frame(seed, frame, width, height, out.ctypes.data)
+    _check(lib().p64_synth_frame_content(content, seed, frame, width, height, out.ctypes.data))
     return out
 
 
@@ -213,9 +225,9 @@ def synth_motion(seed: int) -> tuple[int, int]:
 # device-tensor API (torch tensors on a HIP device)
 
 def synth_frames_device(width: int, height: int, seed0: int, nseeds: int, frame0: int,
-                        nslots: int, out=None):
+                        nslots: int, out=None, content: int = SYNTH_VNOISE):
     """Device copy of synth_frame for nslots x nseeds pictures, slot-major:
-    out[t, s] = synth_frame(seed0 + s, frame0 + t)."""
+    out[t, s] = synth_frame(seed0 + s, frame0 + t, content=content)."""
     torch = _torch()
     pic = picture_bytes(width, height)
     if out is None:
@@ -227,8 +239,8 @@ def synth_frames_device(width: int, height: int, seed0: int, nseeds: int, frame0
     step = max(1, 65535 // nseeds)
     for t0 in range(0, nslots, step):
         n = min(step, nslots - t0)
-        _check(lib().p64gpu_synth_frames(width, height, seed0, nseeds, frame0 + t0, n, pic,
-                                         out.data_ptr() + t0 * nseeds * pic, _stream(torch)))
+        _check(lib().p64gpu_synth_content(content, width, height, seed0, nseeds, frame0 + t0, n, pic,
+                                          out.data_ptr() + t0 * nseeds * pic, _stream(torch)))
     return out
 
 def _torch():
@@ -353,6 +365,8 @@ class FrameBatchOut:
                         # blocks with a nonzero level (include/p64gpu.h)
     mb: object          # int8  [nframes, nmb, 4]  (mtype, cbp, mvx, mvy)
     me: object          # int32 [nframes, nmb, 7] or None
+    nz: object = None   # uint8 [nframes, nmb] or None: bit 5-b set iff block b
+                        # has a nonzero level (its levels were stored)
 
 
 def encode_frames(cur, ref, recon, last_intra, *, width: int, height: int, intra: bool,
@@ -396,6 +410,10 @@ def encode_frames(cur, ref, recon, last_intra, *, width: int, height: int, intra
         _dev_check(out.mb, torch.int8, "out.mb")
         if out.coef.numel() < nmb_all * 384 or out.mb.numel() < nmb_all * 4:
             raise P64GpuError("out.coef / out.mb smaller than nframes x nmb records")
+        if out.nz is not None:
+            _dev_check(out.nz, torch.uint8, "out.nz")
+            if out.nz.numel() < nmb_all:
+                raise P64GpuError("out.nz smaller than nframes x nmb")
         if out.me is not None:
             _dev_check(out.me, torch.int32, "out.me")
             if out.me.numel() < nmb_all * 7:
@@ -417,7 +435,8 @@ def encode_frames(cur, ref, recon, last_intra, *, width: int, height: int, intra
                    quant_mb=(quant_mb.data_ptr() if quant_mb is not None else None),
                    mtype_override=(mtype_override.data_ptr() if mtype_override is not None else None),
                    coef=out.coef.data_ptr(), mb=out.mb.data_ptr(),
-                   me=(me.data_ptr() if me is not None else None))
+                   me=(me.data_ptr() if me is not None else None),
+                   nzmask=(out.nz.data_ptr() if out.nz is not None else None))
     _check(lib().p64gpu_encode_frames(ctypes.byref(a), _stream(torch)))
     return out
 

@@ -114,6 +114,30 @@ __global__ __launch_bounds__(256) void k_synth(int w, int h, uint32_t seed0, int
   }
 }
 
+// the SURVEY.md 8(d) content (synth_impl.h p64v_*), same layout as k_synth;
+// a chroma sample recomputes its four luma samples (same bytes as synth.c,
+// which averages the stored luma plane)
+__global__ __launch_bounds__(256) void k_synth_survey(int w, int h, uint32_t seed0, int nseeds, int frame0,
+                                                      int64_t stride, uint8_t *out) {
+  const int pic = blockIdx.y;
+  const int t = pic / nseeds, sidx = pic - t * nseeds;
+  const uint32_t seed = seed0 + (uint32_t)sidx;
+  const int frame = frame0 + t;
+  uint8_t *y = out + (size_t)pic * stride;
+  uint8_t *u = y + (size_t)w * h, *v = u + (size_t)(w / 2) * (h / 2);
+  const int nl = w * h, nc = (w / 2) * (h / 2);
+  for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < nl + nc; k += gridDim.x * blockDim.x) {
+    if (k < nl) {
+      y[k] = p64v_luma(seed, frame, k % w, k / w);
+    } else {
+      const int c = k - nl, i = c % (w / 2), j = c / (w / 2);
+      const int a4 = p64v_luma(seed, frame, 2 * i, 2 * j) + p64v_luma(seed, frame, 2 * i + 1, 2 * j) +
+                     p64v_luma(seed, frame, 2 * i, 2 * j + 1) + p64v_luma(seed, frame, 2 * i + 1, 2 * j + 1);
+      p64v_chroma_of(a4, &u[c], &v[c]);
+    }
+  }
+}
+
 // Clock probe and spin-up (measurement aid, bench.py): every wave issues
 // chains of v_sad_u8 -- k_motion's dominant instruction -- until `ticks` of
 // the 100 MHz real-time counter have passed, then records how many shader
@@ -169,10 +193,14 @@ hipError_t block_op(int op, const int32_t *in, int32_t *out, int64_t nblocks, in
   return hipGetLastError();
 }
 
-hipError_t synth(int w, int h, uint32_t seed0, int nseeds, int frame0, int nslots, int64_t stride,
+hipError_t synth(int content, int w, int h, uint32_t seed0, int nseeds, int frame0, int nslots, int64_t stride,
                  uint8_t *out, hipStream_t st) {
-  hipLaunchKernelGGL(k_synth, dim3(64, (unsigned)(nseeds * nslots)), dim3(256), 0, st, w, h, seed0, nseeds,
-                     frame0, stride, out);
+  if (content == P64_SYNTH_SURVEY)
+    hipLaunchKernelGGL(k_synth_survey, dim3(64, (unsigned)(nseeds * nslots)), dim3(256), 0, st, w, h, seed0,
+                       nseeds, frame0, stride, out);
+  else
+    hipLaunchKernelGGL(k_synth, dim3(64, (unsigned)(nseeds * nslots)), dim3(256), 0, st, w, h, seed0, nseeds,
+                       frame0, stride, out);
   return hipGetLastError();
 }
 

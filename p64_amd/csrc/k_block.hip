@@ -615,10 +615,12 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t recon_rsrc(const p64gpu_encode
   const int nfr = (int)mdiv(nmbs, kd.mn, kd.sn);
   return __builtin_amdgcn_make_buffer_rsrc((void *)a.recon, (short)0, (int)(nfr * a.frame_stride), BUF_RSRC_W3);
 }
-// the rows (rec_off out of range: none) and the record of an MB-grouped wave
+// the rows (rec_off out of range: none) and the record of an MB-grouped wave,
+// with the MB's nonzero-block mask nzm (bit 5-b: block b has a nonzero level)
+// when the caller asked for it (a.nzmask)
 __device__ __forceinline__ void mbg_store_rows(const p64gpu_encode_args &a, const BlkDiv &kd, unsigned nmbs,
                                                uint32_t rec_off, int pw, const uint2 rows[8], bool rl,
-                                               unsigned gmb, uint32_t mbw, uint8_t li) {
+                                               unsigned gmb, uint32_t mbw, uint8_t li, uint32_t nzm) {
   const __amdgpu_buffer_rsrc_t rec = recon_rsrc(a, kd, nmbs);
 #pragma unroll
   for (int k = 0; k < 8; k++) {
@@ -632,17 +634,12 @@ __device__ __forceinline__ void mbg_store_rows(const p64gpu_encode_args &a, cons
       __builtin_amdgcn_make_buffer_rsrc((void *)a.mb, (short)0, (int)(nmbs * 4u), BUF_RSRC_W3);
   const __amdgpu_buffer_rsrc_t lir =
       __builtin_amdgcn_make_buffer_rsrc((void *)a.last_intra, (short)0, (int)nmbs, BUF_RSRC_W3);
+  const __amdgpu_buffer_rsrc_t nzr =
+      __builtin_amdgcn_make_buffer_rsrc((void *)a.nzmask, (short)0, a.nzmask ? (int)nmbs : 0, BUF_RSRC_W3);
   __builtin_amdgcn_raw_buffer_store_b32(mbw, mbr, rl ? 4u * gmb : BUF_OOB, 0, 0);
   __builtin_amdgcn_raw_buffer_store_b8(li, lir, rl ? gmb : BUF_OOB, 0, 0);
+  __builtin_amdgcn_raw_buffer_store_b8((uint8_t)nzm, nzr, rl ? gmb : BUF_OOB, 0, 0);
 }
-__device__ __forceinline__ void mbg_store(const p64gpu_encode_args &a, const BlkDiv &kd, const uint8_t *lds, int lane,
-                                          unsigned nmbs, unsigned gmb0, uint32_t nvalid, uint32_t rec_off,
-                                          int pw, const uint2 rows[8], bool rl, unsigned gmb, uint32_t mbw,
-                                          uint8_t li) {
-  mbg_store_levels(a, lds, lane, nmbs, gmb0, nvalid);
-  mbg_store_rows(a, kd, nmbs, rec_off, pw, rows, rl, gmb, mbw, li);
-}
-
 // intra picture, block layout over all 64 lanes: wave w takes the launch's
 // blocks 64 w .. 64 w + 63 in MB-major order (blk_pos_mb of block g: MB g / 6,
 // block g % 6), so an MB may straddle two waves -- nothing in an intra block
@@ -666,10 +663,11 @@ __global__ __launch_bounds__(64 * MBG_WAVES) void k_intra_mbg(p64gpu_encode_args
   IntraOut o;
   intra_block<CLAMP, POW2>(a, f, lds, lane, o);
   // the MB's record and LastIntra (p64.c:909-910: MTYPE 0, CBP 0x3f, LastIntra
-  // reset) from the lane of its block 0
+  // reset) from the lane of its block 0; every intra block has a nonzero level
+  // (the DC, 1..254)
   const bool rl = b == 0 && g0 + (unsigned)lane < nblk;
   blk_store_levels(a, lds, lane, nmbs, g0, min(64u, nblk - g0));
-  mbg_store_rows(a, kd, nmbs, o.rec_off, o.pw, o.rec, rl, gmb, 0x3f00u, 0);
+  mbg_store_rows(a, kd, nmbs, o.rec_off, o.pw, o.rec, rl, gmb, 0x3f00u, 0, 0x3fu);
 }
 // The source of an 8x8 prediction at (x, y) of a plane (any byte alignment):
 // three aligned dwords per row (the third only matters when the row is
@@ -1269,9 +1267,10 @@ __global__ __launch_bounds__(64) OCC4 void k_inter_mbg(p64gpu_encode_args a, Blk
   const bool rl = b == 0 && lane < 6 * MBS_PER_WAVE && gmb0 + (unsigned)(l / 6) < nmbs;
   const uint32_t mbw = (uint32_t)(mt & 0xff) | ((uint32_t)(cbp & 0xff) << 8) |
                        (mt_mf(mt) ? ((uint32_t)(mvx & 0xff) << 16) | ((uint32_t)(mvy & 0xff) << 24) : 0u);
-  // every block: the reconstruction (coded) or the prediction (uncoded)
+  // every block: the reconstruction (coded) or the prediction (uncoded); the
+  // MB's nonzero-block mask (block b -> bit 5 - b, as the CBP)
   mbg_store_rows(a, kd, nmbs, ro, pw, prow, rl, gmb, mbw,
-                 mt_intra(mt) ? (uint8_t)0 : (uint8_t)(li + 1));
+                 mt_intra(mt) ? (uint8_t)0 : (uint8_t)(li + 1), __builtin_bitreverse32(any) >> 26);
 }
 
 }  // namespace

@@ -1052,6 +1052,12 @@ __device__ __forceinline__ void encode_mb(const p64gpu_encode_args &a, const uin
     a.mb[gmb] = o;
     a.last_intra[gmb] = mt_intra(mt) ? 0 : (uint8_t)(li + 1);
   }
+  if (a.nzmask) {  // block k has a nonzero level -> bit 5 - k
+    uint32_t nzm = 0;
+#pragma unroll
+    for (int k = 0; k < 6; k++) nzm |= __ballot(lev[k] != 0) ? 1u << (5 - k) : 0u;
+    if (lane == 0) a.nzmask[gmb] = (uint8_t)nzm;
+  }
 }
 
 template <int MODE>

@@ -32,7 +32,7 @@ hipError_t recon_mbg(int w, int h, int nframes, int64_t stride, const uint8_t *r
 // the clock probe
 hipError_t block_op(int op, const int32_t *in, int32_t *out, int64_t nblocks, int dcq, int acq,
                     hipStream_t st);
-hipError_t synth(int w, int h, uint32_t seed0, int nseeds, int frame0, int nslots, int64_t stride,
+hipError_t synth(int content, int w, int h, uint32_t seed0, int nseeds, int frame0, int nslots, int64_t stride,
                  uint8_t *out, hipStream_t st);
 // clock probe: clock_waves() waves (8 per SIMD), each spinning `ticks` of the
 // 100 MHz counter; out [clock_waves()][2] = (shader ticks, real-time ticks)

@@ -130,20 +130,30 @@ p64_me_rec *me_scratch(size_t n, hipStream_t st, std::unique_lock<std::mutex> &l
   return e->buf;
 }
 
-// pictures per launch of the block-layout kernels: every buffer of a launch
-// within the 2 GiB of a 32-bit buffer offset (per = the larger of a picture's
-// bytes and its levels' bytes).  P64GPU_CHUNK_BYTES lowers the limit (tests
-// exercise the split launches with it); read on every call.
-int pictures_per_launch(int w, int h, int64_t stride) {
-  const int64_t levels = (int64_t)(w / 16) * (h / 16) * 768;
-  const int64_t per = levels > stride ? levels : stride;
+}  // namespace
+
+// the byte limit of one launch's buffers: the 2 GiB of a 32-bit buffer
+// offset, or lower by P64GPU_CHUNK_BYTES (tests exercise the split launches
+// with it); read on every call.  Also used by p64vlc.hip.
+extern "C" int64_t p64gpu_chunk_bytes_(void) {
   int64_t lim = ((int64_t)1 << 31) - 1;
   const char *e = getenv("P64GPU_CHUNK_BYTES");
   if (e && *e) {
     const long long v = atoll(e);
     if (v > 0 && v < lim) lim = v;
   }
-  const int64_t n = lim / per;
+  return lim;
+}
+
+namespace {
+
+// pictures per launch of the block-layout kernels: every buffer of a launch
+// within p64gpu_chunk_bytes_() (per = the larger of a picture's bytes and its
+// levels' bytes)
+int pictures_per_launch(int w, int h, int64_t stride) {
+  const int64_t levels = (int64_t)(w / 16) * (h / 16) * 768;
+  const int64_t per = levels > stride ? levels : stride;
+  const int64_t n = p64gpu_chunk_bytes_() / per;
   return n < 1 ? 1 : (int)n;
 }
 
@@ -161,6 +171,7 @@ p64gpu_encode_args sub_batch(const p64gpu_encode_args &a, int f0, int n) {
   c.coef = a.coef + m0 * 384;
   c.mb = a.mb + m0;
   c.me = a.me ? a.me + m0 : nullptr;
+  c.nzmask = a.nzmask ? a.nzmask + m0 : nullptr;
   return c;
 }
 
@@ -372,15 +383,22 @@ int p64gpu_decode_recon(int w, int h, int nframes, int64_t stride, const uint8_t
   return P64GPU_OK;
 }
 
-int p64gpu_synth_frames(int w, int h, uint32_t seed0, int nseeds, int frame0, int nslots,
-                        int64_t stride, uint8_t *out, void *stream) {
+int p64gpu_synth_content(int content, int w, int h, uint32_t seed0, int nseeds, int frame0, int nslots,
+                         int64_t stride, uint8_t *out, void *stream) {
   int s = check_geometry(w, h, 1, stride);
   if (s) return s;
+  if (content != P64_SYNTH_VNOISE && content != P64_SYNTH_SURVEY)
+    return fail(P64GPU_E_INVALID, "synth: content %d", content);
   if (!out || nseeds < 1 || nslots < 1 || frame0 < 0 || (int64_t)nseeds * nslots > 65535)
     return fail(P64GPU_E_INVALID, "synth: out=%p nseeds=%d nslots=%d frame0=%d", (void *)out,
                 nseeds, nslots, frame0);
-  HIP_TRY(p64k::synth(w, h, seed0, nseeds, frame0, nslots, stride, out, (hipStream_t)stream));
+  HIP_TRY(p64k::synth(content, w, h, seed0, nseeds, frame0, nslots, stride, out, (hipStream_t)stream));
   return P64GPU_OK;
+}
+
+int p64gpu_synth_frames(int w, int h, uint32_t seed0, int nseeds, int frame0, int nslots,
+                        int64_t stride, uint8_t *out, void *stream) {
+  return p64gpu_synth_content(P64_SYNTH_VNOISE, w, h, seed0, nseeds, frame0, nslots, stride, out, stream);
 }
 
 int p64gpu_clock_probe(int microseconds, int *mhz, void *stream) {

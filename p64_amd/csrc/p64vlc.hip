@@ -19,6 +19,7 @@
 // sequence's bitstream exactly (pictures are not byte aligned in H.261).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdint>
 
 #include "../../include/p64gpu.h"
@@ -26,6 +27,7 @@
 
 extern "C" int p64s_vlc_tables_(uint32_t *t);
 extern "C" int p64gpu_fail_(int status, const char *msg);
+extern "C" int64_t p64gpu_chunk_bytes_(void);
 
 namespace {
 
@@ -258,7 +260,7 @@ __global__ __launch_bounds__(64 * VLC_WAVES) void k_vlc_blk(VlcArgs a, VlcTables
   uint32_t lv[32];
   {
     const __amdgpu_buffer_rsrc_t cr = __builtin_amdgcn_make_buffer_rsrc(
-        (void *)a.coef, (short)0, (int)min((size_t)a.nframes * a.nmb * 768, (size_t)0x7fffffff), 0x00020000);
+        (void *)a.coef, (short)0, (int)((size_t)a.nframes * a.nmb * 768), 0x00020000);  // < 2 GiB (host split)
     const uint32_t co = coded ? (uint32_t)(((base + k) * 6 + b) * 128) : 0x80000000u;
 #pragma unroll
     for (int i = 0; i < 8; i++) {
@@ -377,39 +379,55 @@ int p64gpu_vlc_pictures(const p64gpu_vlc_args *x, void *stream) {
   if (fmt < 0) return fmt;
   if (x->nframes < 1 || x->nframes > 65535)
     return p64gpu_fail_(P64GPU_E_INVALID, "vlc: nframes out of range");
+  if (x->flags != 0) return p64gpu_fail_(P64GPU_E_INVALID, "vlc: unknown flags");
   if (x->out_stride < p64gpu_vlc_max_bytes(x->width, x->height) || (x->out_stride & 3) ||
       ((uintptr_t)x->out & 3))
     return p64gpu_fail_(P64GPU_E_INVALID, "vlc: out_stride below p64gpu_vlc_max_bytes or not 4-aligned");
+  if (((uintptr_t)x->scratch & 7) || ((uintptr_t)x->coef & 15) || ((uintptr_t)x->mb & 3))
+    return p64gpu_fail_(P64GPU_E_INVALID, "vlc: scratch must be 8-byte, coef 16-byte, mb 4-byte aligned");
   if (!g_tab_ok) {
     const int s = p64s_vlc_tables_(g_tab.t);
     if (s) return s;
     g_tab_ok = true;
   }
-  VlcArgs a;
-  a.width = x->width;
-  a.height = x->height;
-  a.nframes = x->nframes;
-  a.format = fmt;
-  p64s_geometry(fmt, nullptr, nullptr, &a.ngob);
-  a.nmb = a.ngob * 33;
-  a.mb = x->mb;
-  a.coef = x->coef;
-  a.gquant = x->gquant;
-  a.mquant = x->mquant;
-  a.tr = x->tr;
-  a.phase = x->phase;
-  a.out = reinterpret_cast<uint32_t *>(x->out);
-  a.out_words = x->out_stride / 4;
-  a.bits = x->bits;
-  a.mb_bits = x->scratch;
-  a.mb_off = x->scratch + (size_t)x->nframes * a.nmb;
+  int ngob = 0;
+  p64s_geometry(fmt, nullptr, nullptr, &ngob);
+  const int nmb = ngob * 33;
+  // pictures per launch: the levels of one launch within the 2 GiB range of
+  // the kernels' 32-bit buffer offsets (the encoder's split, p64gpu_abi.hip)
+  const int64_t per = (int64_t)nmb * 768;
+  const int chunk = (int)std::max<int64_t>(1, std::min<int64_t>(x->nframes, p64gpu_chunk_bytes_() / per));
   hipStream_t st = (hipStream_t)stream;
-  const dim3 grid((unsigned)((a.nmb + VLC_WAVES * VLC_MBS - 1) / (VLC_WAVES * VLC_MBS)),
-                  (unsigned)a.nframes);
-  a.blk_bits = reinterpret_cast<uint16_t *>(x->scratch + 2 * (size_t)x->nframes * a.nmb);
-  hipLaunchKernelGGL(k_vlc_blk<false>, grid, dim3(64 * VLC_WAVES), 0, st, a, g_tab);
-  hipLaunchKernelGGL(k_vlc_scan, dim3((unsigned)a.nframes), dim3(64), 0, st, a);
-  hipLaunchKernelGGL(k_vlc_blk<true>, grid, dim3(64 * VLC_WAVES), 0, st, a, g_tab);
+  const int64_t out_words = x->out_stride / 4;
+  for (int f0 = 0; f0 < x->nframes; f0 += chunk) {
+    const int nc = std::min(chunk, x->nframes - f0);
+    const size_t m0 = (size_t)f0 * nmb;
+    VlcArgs a;
+    a.width = x->width;
+    a.height = x->height;
+    a.nframes = nc;
+    a.format = fmt;
+    a.ngob = ngob;
+    a.nmb = nmb;
+    a.mb = x->mb + m0;
+    a.coef = x->coef + m0 * 384;
+    a.gquant = x->gquant + (size_t)f0 * ngob;
+    a.mquant = x->mquant ? x->mquant + m0 : nullptr;
+    a.tr = x->tr + f0;
+    a.phase = x->phase ? x->phase + f0 : nullptr;
+    a.out = reinterpret_cast<uint32_t *>(x->out) + (size_t)f0 * out_words;
+    a.out_words = out_words;
+    a.bits = x->bits + f0;
+    // this chunk's [6][nc][nmb] words of the scratch
+    uint32_t *scr = x->scratch + 6 * m0;
+    a.mb_bits = scr;
+    a.mb_off = scr + (size_t)nc * nmb;
+    a.blk_bits = reinterpret_cast<uint16_t *>(scr + 2 * (size_t)nc * nmb);
+    const dim3 grid((unsigned)((nmb + VLC_WAVES * VLC_MBS - 1) / (VLC_WAVES * VLC_MBS)), (unsigned)nc);
+    hipLaunchKernelGGL(k_vlc_blk<false>, grid, dim3(64 * VLC_WAVES), 0, st, a, g_tab);
+    hipLaunchKernelGGL(k_vlc_scan, dim3((unsigned)nc), dim3(64), 0, st, a);
+    hipLaunchKernelGGL(k_vlc_blk<true>, grid, dim3(64 * VLC_WAVES), 0, st, a, g_tab);
+  }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return p64gpu_fail_(P64GPU_E_HIP, hipGetErrorString(e));
   return P64GPU_OK;

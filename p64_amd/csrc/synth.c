@@ -23,6 +23,31 @@
 
 void p64_synth_motion(uint32_t seed, int *mvx, int *mvy) { p64s_motion(seed, mvx, mvy); }
 
+/* SURVEY.md 8(d) content (synth_impl.h p64v_*): luma, then chroma from it */
+static void survey_frame(uint32_t seed, int frame, int width, int height, uint8_t *out) {
+  uint8_t *y = out, *u = out + (size_t)width * height;
+  uint8_t *v = u + (size_t)(width / 2) * (height / 2);
+  for (int j = 0; j < height; j++)
+    for (int i = 0; i < width; i++) y[(size_t)j * width + i] = p64v_luma(seed, frame, i, j);
+  for (int j = 0; j < height / 2; j++)
+    for (int i = 0; i < width / 2; i++) {
+      const uint8_t *p = y + (size_t)(2 * j) * width + 2 * i;
+      size_t k = (size_t)j * (width / 2) + i;
+      p64v_chroma_of(p[0] + p[1] + p[width] + p[width + 1], &u[k], &v[k]);
+    }
+}
+
+int p64_synth_frame_content(int content, uint32_t seed, int frame, int width, int height, uint8_t *out) {
+  if (!out || width < 16 || height < 16 || (width & 15) || (height & 15) || frame < 0) return P64GPU_E_INVALID;
+  if (content == P64_SYNTH_VNOISE)
+    p64_synth_frame(seed, frame, width, height, out);
+  else if (content == P64_SYNTH_SURVEY)
+    survey_frame(seed, frame, width, height, out);
+  else
+    return P64GPU_E_INVALID;
+  return P64GPU_OK;
+}
+
 void p64_synth_frame(uint32_t seed, int frame, int width, int height, uint8_t *out) {
   uint8_t *y = out, *u = out + (size_t)width * height;
   uint8_t *v = u + (size_t)(width / 2) * (height / 2);

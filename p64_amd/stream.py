@@ -371,7 +371,7 @@ def decode_sequence(data: bytes, start_frame: int = 0, force_cif: bool = False) 
 
 class VlcArgs(ctypes.Structure):
     _fields_ = [("width", ctypes.c_int), ("height", ctypes.c_int), ("nframes", ctypes.c_int),
-                ("reserved", ctypes.c_int), ("mb", ctypes.c_void_p), ("coef", ctypes.c_void_p),
+                ("flags", ctypes.c_int), ("mb", ctypes.c_void_p), ("coef", ctypes.c_void_p),
                 ("gquant", ctypes.c_void_p), ("mquant", ctypes.c_void_p), ("tr", ctypes.c_void_p),
                 ("phase", ctypes.c_void_p), ("out", ctypes.c_void_p), ("out_stride", ctypes.c_int64),
                 ("bits", ctypes.c_void_p), ("scratch", ctypes.c_void_p)]
@@ -412,7 +412,7 @@ def vlc_pictures(mb, coef, gquant, tr, *, width: int, height: int, phase=None, m
     if out.shape[0] < n or bits.numel() < n or scratch.numel() < 6 * n * nmb or \
             stride < int(L.p64gpu_vlc_max_bytes(width, height)):
         raise P64GpuError("vlc_pictures: buffers smaller than the batch")
-    a = VlcArgs(width=width, height=height, nframes=n, reserved=0, mb=mb.data_ptr(),
+    a = VlcArgs(width=width, height=height, nframes=n, flags=0, mb=mb.data_ptr(),
                 coef=coef.data_ptr(), gquant=gquant.data_ptr(),
                 mquant=mquant.data_ptr() if mquant is not None else None, tr=tr.data_ptr(),
                 phase=phase.data_ptr() if phase is not None else None, out=out.data_ptr(),

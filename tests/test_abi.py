@@ -43,7 +43,7 @@ def test_library_exports_every_declared_symbol(p64):
 
 def test_abi_version_and_strings(p64):
     L = p64.lib()
-    assert L.p64gpu_abi_version() == 1
+    assert L.p64gpu_abi_version() == 2 == p64.ABI_VERSION
     assert L.p64gpu_strerror(0) == b"ok"
     assert L.p64gpu_strerror(-1) == b"invalid argument"
 
@@ -60,7 +60,7 @@ int main(void) {
          sizeof(p64_me_rec), sizeof(p64_mb_rec));
   O(width); O(height); O(nframes); O(intra); O(quant); O(me_mode); O(search_limit);
   O(flags); O(frame_stride); O(cur); O(ref); O(recon); O(last_intra); O(quant_mb);
-  O(mtype_override); O(coef); O(mb); O(me);
+  O(mtype_override); O(coef); O(mb); O(me); O(nzmask);
   return 0;
 }''')
     exe = tmp_path / "layout"
@@ -102,6 +102,43 @@ def test_invalid_arguments_rejected_without_device(p64):
     assert L.p64gpu_motion_estimation(176, 144, 1, 176 * 144, 16, 16, 7, 15, 16, None) == -1
     assert L.p64gpu_motion_estimation(176, 144, 1, 176 * 144, 16, 16, 1, 32, 16, None) == -1
     assert L.p64gpu_synth_frames(176, 144, 1, 0, 0, 1, 38016, 16, None) == -1
+    assert L.p64gpu_synth_content(7, 176, 144, 1, 1, 0, 1, 38016, 16, None) == -1
+    assert b"content" in L.p64gpu_last_error()
+    out = np.empty(176 * 144 * 3 // 2, np.uint8)
+    assert L.p64_synth_frame_content(2, 1, 0, 176, 144, out.ctypes.data) == -1
+    # entropy coder: flags must be 0, scratch 8-byte aligned (ABI version 2)
+    from p64_amd import stream as p64s
+    stride = (int(L.p64gpu_vlc_max_bytes(176, 144)) + 3) // 4 * 4
+    v = p64s.VlcArgs(width=176, height=144, nframes=1, flags=1, mb=16, coef=16, gquant=16, tr=16,
+                     out=16, out_stride=stride, bits=16, scratch=16)
+    assert L.p64gpu_vlc_pictures(ctypes.byref(v), None) == -1
+    assert b"flags" in L.p64gpu_last_error()
+    v.flags, v.scratch = 0, 20
+    assert L.p64gpu_vlc_pictures(ctypes.byref(v), None) == -1
+    assert b"aligned" in L.p64gpu_last_error()
+
+
+def test_vlc_args_layout_matches_ctypes(p64, tmp_path):
+    from p64_amd import stream as p64s
+    src = tmp_path / "vlayout.c"
+    src.write_text(r'''
+#include <stdio.h>
+#include <stddef.h>
+#include "p64gpu.h"
+#define O(f) printf("%s %zu\n", #f, offsetof(p64gpu_vlc_args, f))
+int main(void) {
+  printf("sizeof_args %zu\n", sizeof(p64gpu_vlc_args));
+  O(width); O(height); O(nframes); O(flags); O(mb); O(coef); O(gquant); O(mquant); O(tr);
+  O(phase); O(out); O(out_stride); O(bits); O(scratch);
+  return 0;
+}''')
+    exe = tmp_path / "vlayout"
+    subprocess.run(["gcc", "-I", os.path.join(REPO, "include"), str(src), "-o", str(exe)], check=True)
+    got = dict(l.split() for l in subprocess.run([str(exe)], capture_output=True, text=True,
+                                                 check=True).stdout.splitlines())
+    assert int(got["sizeof_args"]) == ctypes.sizeof(p64s.VlcArgs)
+    for name, _ in p64s.VlcArgs._fields_:
+        assert int(got[name]) == getattr(p64s.VlcArgs, name).offset, name
 
 
 def test_device_count_without_gpu_is_not_an_error(p64):
@@ -121,6 +158,36 @@ def test_synth_is_deterministic_and_moves(p64):
     # frame 1 at (x, y) == frame 0 at (x + mx, y + my) for the noise-free class
     assert np.array_equal(f1[20:100, 20:100], f0[20 + my:100 + my, 20 + mx:100 + mx])
     assert (mvx, mvy) == (9 % 7 - 3, (9 // 7) % 5 - 2)
+
+
+def test_survey_content_follows_survey_8d(p64):
+    """--content survey: deterministic; picture t is picture
+    t-1 translated by (+3, -2) px up to the N(0,4) temporal noise (the
+    residual at the true shift has sigma 4 sqrt 2); the texture's spread is
+    that of 50 sin cos + 30 sin + N(0,12) (sigma ~35); chroma is derived from
+    the 2x2-averaged luma; seeds differ."""
+    w, h = 352, 288
+    S = p64.SYNTH_SURVEY
+    a = p64.synth_frame(3, 5, w, h, content=S)
+    assert np.array_equal(a, p64.synth_frame(3, 5, w, h, content=S))
+    assert not np.array_equal(a, p64.synth_frame(4, 5, w, h, content=S))
+    f = [p64.synth_frame(3, t, w, h, content=S) for t in range(3)]
+    Y = [x[:w * h].reshape(h, w).astype(np.int32) for x in f]
+    for t in (1, 2):
+        d = Y[t][0:h - 2, 3:w] - Y[t - 1][2:h, 0:w - 3]  # (x, y) <- (x - 3, y + 2)
+        assert abs(d.mean()) < 0.2 and 5.3 < d.std() < 6.1, (d.mean(), d.std())
+        assert (Y[t] - Y[t - 1]).std() > 15  # the zero vector is far worse
+    assert 127 < Y[0].mean() < 129.5 and 32 < Y[0].std() < 38
+    U = f[0][w * h:w * h + w * h // 4].reshape(h // 2, w // 2).astype(np.int32)
+    a4 = Y[0][0::2, 0::2] + Y[0][1::2, 0::2] + Y[0][0::2, 1::2] + Y[0][1::2, 1::2]
+    a = (a4 + 2) >> 2
+    np.testing.assert_array_equal(U, np.clip(128 + np.trunc((a - 128) / 2).astype(np.int32), 0, 255))
+    # the sinusoid part: the 1/7 rad/px carrier is among the strongest
+    # components of the luma's power spectrum
+    P = np.abs(np.fft.rfft2(Y[0] - Y[0].mean())) ** 2
+    fy, fx = np.unravel_index(np.argsort(P, axis=None)[-8:], P.shape)
+    fxs = {round(2 * np.pi * x / w, 2) for x in fx}
+    assert any(abs(v - 1 / 7) < 0.03 for v in fxs), fxs
 
 
 def test_host_driver_built():

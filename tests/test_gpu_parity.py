@@ -663,7 +663,8 @@ def test_inter_levels_sparse_store(p64, oracle_mod, torch_dev):
                                                           mtype_override=ov)
             out = p64.FrameBatchOut(coef=torch.full((1, nmb, 6, 64), SENT, dtype=torch.int16, device="cuda"),
                                     mb=torch.empty((1, nmb, 4), dtype=torch.int8, device="cuda"),
-                                    me=torch.empty((1, nmb, 7), dtype=torch.int32, device="cuda"))
+                                    me=torch.empty((1, nmb, 7), dtype=torch.int32, device="cuda"),
+                                    nz=torch.full((1, nmb), 0xC0, dtype=torch.uint8, device="cuda"))
             rec_d = torch.zeros(w * h * 3 // 2, dtype=torch.uint8, device="cuda")
             p64.encode_frames(dev(torch, f1), dev(torch, rec0), rec_d, dev(torch, np.zeros(nmb, np.uint8)),
                               width=w, height=h, intra=False, quant=quant, me_mode=p64.ME_FULL,
@@ -676,6 +677,10 @@ def test_inter_levels_sparse_store(p64, oracle_mod, torch_dev):
             assert 0 < nz.sum() < nz.size, tag  # both kinds present
             np.testing.assert_array_equal(got[nz], want[nz], err_msg=tag)
             assert (got[~nz] == SENT).all(), tag
+            # the nonzero-block mask names exactly those blocks (bit 5 - b), ABI v2
+            m = host(out.nz)[0]
+            np.testing.assert_array_equal(((m[:, None] >> (5 - np.arange(6))[None, :]) & 1).reshape(-1) == 1,
+                                          nz, err_msg=tag)
             np.testing.assert_array_equal(host(out.mb)[0].view(p64.MB_DTYPE).reshape(nmb), mb, err_msg=tag)
             np.testing.assert_array_equal(host(rec_d), recon, err_msg=tag)
 
@@ -778,12 +783,18 @@ def test_reference_cli_with_gpu_shim(p64, torch_dev, tmp_path, name):
 
 
 def test_device_synth_matches_host(p64, torch_dev):
-    """The bench's on-device inputs are the same bytes the CPU legs use."""
-    for (w, h) in ((352, 288), (176, 144)):
-        d = host(p64.synth_frames_device(w, h, 5, 3, 10, 2))
-        for t in range(2):
-            for s in range(3):
-                np.testing.assert_array_equal(d[t, s], p64.synth_frame(5 + s, 10 + t, w, h))
+    """The bench's on-device inputs are the same bytes the CPU legs use (both
+    contents: the survey sines are a fixed-point polynomial of integer phases,
+    identical on host and device)."""
+    for c in (p64.SYNTH_VNOISE, p64.SYNTH_SURVEY):
+        for (w, h) in ((352, 288), (176, 144), (704, 576)):
+            d = host(p64.synth_frames_device(w, h, 5, 3, 10, 2, content=c))
+            for t in range(2):
+                for s in range(3):
+                    np.testing.assert_array_equal(d[t, s], p64.synth_frame(5 + s, 10 + t, w, h, content=c))
+    # far along a sequence (texture coordinates well away from the origin)
+    d = host(p64.synth_frames_device(352, 288, 200, 2, 250, 1, content=p64.SYNTH_SURVEY))
+    np.testing.assert_array_equal(d[0, 1], p64.synth_frame(201, 250, 352, 288, content=p64.SYNTH_SURVEY))
     # more than 65535 pictures: the wrapper splits the slots over launches
     w, h = 176, 144
     big = p64.synth_frames_device(w, h, 3, 4096, 7, 17)
@@ -795,57 +806,83 @@ def test_device_synth_matches_host(p64, torch_dev):
 # ---------------------------------------------------------------------------
 # the bench's full size: 256 CIF sequences per launch, FULL SL=31, q=8
 
-def test_bench_scale_properties(p64, oracle_mod, torch_dev):
+@pytest.mark.parametrize("content", ["survey", "synth"])
+def test_bench_scale_properties(p64, oracle_mod, torch_dev, content):
     """At BASELINE's full size (one launch over 256 CIF pictures = 101,376 MBs,
-    device-generated as in bench.py): the decoder reconstruction of the coded
-    output equals the encoder's closed-loop reconstruction for every sequence,
-    a relaunch is bit-identical, the levels obey the H.261 bounds, and two
-    sampled sequences equal the oracle exactly."""
+    device-generated as in bench.py; SURVEY.md 8(d)'s content and the
+    builder's synth): the decoder reconstruction of the coded output equals
+    the encoder's closed-loop reconstruction for every sequence, a relaunch is
+    bit-identical, the levels obey the H.261 bounds, and sampled sequences
+    equal the oracle exactly -- for synth one of every seed class (1 plain,
+    5 scene cut, 6 noise-free, 7 low contrast: the dense-search class) and
+    the last one -- levels rebuilt through the nonzero-block mask."""
     torch = torch_dev
     w, h, S, nfr, q = 352, 288, 256, 3, 8
+    if content == "synth":
+        nfr = 14  # past the scene cut of seeds = 5 (mod 8) at picture 12
     nmb, pic = (w // 16) * (h // 16), w * h * 3 // 2
-    fr = p64.synth_frames_device(w, h, 1, S, 0, nfr)  # [t][s] = synth_frame(1 + s, t)
+    # [t][s] = synth_frame(1 + s, t, content)
+    fr = p64.synth_frames_device(w, h, 1, S, 0, nfr, content=p64.CONTENTS[content])
     li = torch.zeros(S * nmb, dtype=torch.uint8, device="cuda")
     recs = [torch.zeros(S * pic, dtype=torch.uint8, device="cuda") for _ in range(nfr)]
     outs = []
     for t in range(nfr):
-        o = p64.encode_frames(fr[t].reshape(-1), recs[t - 1] if t else None, recs[t], li, width=w,
-                              height=h, intra=(t == 0), quant=q, me_mode=p64.ME_FULL,
-                              search_limit=31)
-        outs.append((o.coef.clone(), o.mb.clone(), o.me.clone()))
+        o = p64.FrameBatchOut(coef=torch.full((S, nmb, 6, 64), 0x5A5A, dtype=torch.int16, device="cuda"),
+                              mb=torch.empty((S, nmb, 4), dtype=torch.int8, device="cuda"),
+                              me=torch.empty((S, nmb, 7), dtype=torch.int32, device="cuda"),
+                              nz=torch.empty((S, nmb), dtype=torch.uint8, device="cuda"))
+        p64.encode_frames(fr[t].reshape(-1), recs[t - 1] if t else None, recs[t], li, width=w,
+                          height=h, intra=(t == 0), quant=q, me_mode=p64.ME_FULL,
+                          search_limit=31, out=o)
+        outs.append((o.coef, o.mb, o.me, o.nz))
     qmb = torch.full((S * nmb,), q, dtype=torch.uint8, device="cuda")
     mask = torch.ones_like(qmb)
     prev = torch.zeros(S * pic, dtype=torch.uint8, device="cuda")
+    sel = torch.tensor([32 >> b for b in range(6)], dtype=torch.uint8, device="cuda")
     for t in range(nfr):
         d = torch.zeros_like(prev)
         p64.decode_recon(prev, d, outs[t][0], outs[t][1], qmb, mask, width=w, height=h)
         assert torch.equal(d, recs[t]), f"decoder recon != encoder recon at picture {t}"
         prev = d
         coef = outs[t][0].view(S, nmb, 6, 64)
-        assert int(coef.abs().max()) <= 254 and int(coef[:, :, :, 1:].abs().max()) <= 127
+        stored = (outs[t][3][..., None] & sel) != 0  # [S, nmb, 6]: the nonzero-block mask
+        lv = torch.where(stored[..., None], coef, torch.zeros_like(coef))
+        assert int(lv.abs().max()) <= 254 and int(lv[:, :, :, 1:].abs().max()) <= 127
+        # every block outside the mask was left alone (sentinel), every block in it is nonzero
+        assert bool((coef[~stored] == 0x5A5A).all())
+        assert bool((lv != 0).any(dim=3).eq(stored).all())
     # relaunch of the last picture: identical levels, records and reconstruction
     li2 = li.clone()
     li2.zero_()
     rec_again = torch.zeros_like(recs[-1])
     o = p64.encode_frames(fr[nfr - 1].reshape(-1), recs[nfr - 2], rec_again, li2, width=w, height=h,
                           intra=False, quant=q, me_mode=p64.ME_FULL, search_limit=31)
-    # (LastIntra differs only through the counters, which are all < 131 here)
-    assert torch.equal(o.coef, outs[-1][0]) and torch.equal(o.mb, outs[-1][1])
+    # (o.coef starts zeroed; LastIntra differs only through the counters, all < 131 here)
+    stored = ((outs[-1][3][..., None] & sel) != 0)[..., None]
+    assert torch.equal(o.coef, torch.where(stored, outs[-1][0], torch.zeros_like(outs[-1][0])))
+    assert torch.equal(o.mb, outs[-1][1])
     assert torch.equal(rec_again, recs[-1])
-    # two sampled sequences against the oracle
-    frames_h = fr.cpu().numpy()
-    for s in (0, S - 1):
+    # sampled sequences against the oracle: the whole inputbuf array rebuilt
+    # through the mask, the mask, the records and the reconstruction
+    checked = (0, 4, 5, 6, S - 1) if content == "synth" else (0, S - 1)
+    for s in checked:
+        frames_h = host(fr[:, s])
         li_o = np.zeros(nmb, np.uint8)
         ref = None
         for t in range(nfr):
-            coef, mb, me, recon = oracle_mod.encode_frame(w, h, frames_h[t][s], ref, li_o,
+            coef, mb, me, recon = oracle_mod.encode_frame(w, h, frames_h[t], ref, li_o,
                                                           intra=(t == 0), quant=q, me_mode=1,
                                                           search_limit=31)
             ref = recon
-            np.testing.assert_array_equal(host(outs[t][0]).reshape(S, nmb, 6, 64)[s], coef,
-                                          err_msg=f"coef s{s} t{t}")
-            np.testing.assert_array_equal(host(recs[t]).reshape(S, pic)[s], recon,
-                                          err_msg=f"recon s{s} t{t}")
+            nz = host(outs[t][3][s])
+            bits = ((nz[:, None] >> (5 - np.arange(6))[None, :]) & 1) == 1
+            np.testing.assert_array_equal(bits, coef.any(axis=2), err_msg=f"mask seed{s + 1} t{t}")
+            got = np.where(bits[:, :, None], host(outs[t][0][s]), 0)
+            np.testing.assert_array_equal(got, coef, err_msg=f"coef seed{s + 1} t{t}")
+            np.testing.assert_array_equal(host(outs[t][1][s]).view(p64.MB_DTYPE).reshape(nmb), mb,
+                                          err_msg=f"mb seed{s + 1} t{t}")
+            np.testing.assert_array_equal(host(recs[t].view(S, pic)[s]), recon,
+                                          err_msg=f"recon seed{s + 1} t{t}")
 
 
 # ---------------------------------------------------------------------------

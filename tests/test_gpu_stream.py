@@ -202,9 +202,14 @@ def test_gpu_vlc_byte_identical(p64, torch_dev, name):
     assert hashlib.sha256(data).hexdigest() == str(z["stream_sha256"])
 
 
-def test_gpu_vlc_batch_matches_host_writer(p64, torch_dev):
+@pytest.mark.parametrize("chunk", [None, 3 * 99 * 768])
+def test_gpu_vlc_batch_matches_host_writer(p64, torch_dev, monkeypatch, chunk):
     """One launch over pictures of several sequences, each at its own phase,
-    equals the host writer's bits for every picture."""
+    equals the host writer's bits for every picture -- also when the batch is
+    split into launches of three pictures (P64GPU_CHUNK_BYTES lowers the 2 GiB
+    level limit of one launch)."""
+    if chunk:
+        monkeypatch.setenv("P64GPU_CHUNK_BYTES", str(chunk))
     from p64_amd import stream
     torch = torch_dev
     names = ["qcif_tss", "qcif_q31", "qcif_full31", "qcif_prog_words"]

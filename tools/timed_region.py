@@ -4,6 +4,7 @@ k_clock dispatch after the spin-up (timed_region's clock probe).  Prints per
 kernel the mean, min and max duration over the region and the region's span
 per step, and the spin-up's per-replay means of the dominant kernel.
 usage: python tools/timed_region.py <kernel_trace.csv> <K> [kernel-prefix ...]
+       [--json profiles/r05_timed_region.json --key <bench.py workload key>]
 (the default prefixes are the inter step's two kernels; pass k_intra_mbg or
 k_recon_mbg for the nested configs)."""
 import csv
@@ -13,10 +14,16 @@ import sys
 
 args = sys.argv[1:]
 jpath = None
-if "--json" in args:  # also write {kernel: mean us} of every region found to this file
+if "--json" in args:  # also write {key: {kernel: mean us}} of every region found to this file
     i = args.index("--json")
     jpath = args[i + 1]
     del args[i:i + 2]
+jkey = None
+if "--key" in args:  # the workload key (bench.py content_key), required with --json
+    i = args.index("--key")
+    jkey = args[i + 1]
+    del args[i:i + 2]
+assert not jpath or jkey, "--json needs --key <bench.py workload key>"
 path, K = args[0], int(args[1])
 prefixes = args[2:] or ["k_motion", "k_inter_mbg"]
 found = {}
@@ -50,5 +57,5 @@ if jpath:
         old = json.load(open(jpath))
     except (OSError, ValueError):
         pass
-    old.update(found)
+    old.setdefault(jkey, {}).update(found)
     json.dump(old, open(jpath, "w"), indent=1, sort_keys=True)
