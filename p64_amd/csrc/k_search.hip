@@ -162,6 +162,9 @@ __device__ __forceinline__ int sad_zero(const Sx &S, int lane) {
 // SUM << 10 | ord, ord = 1 + (dx+15)*32 + (dy+15): FastBME's dx-major scan order
 // (ord 0 is reserved for the zero vector).
 constexpr int ME_LIST_MAX = 256;
+#ifndef ME_GROUPS_MAX
+#define ME_GROUPS_MAX 16  // survivors finished by 4-lane groups; more: finish_halves
+#endif
 static_assert(ME_LIST_MAX <= SURV_LIST_MAX, "survivor list size");
 constexpr uint32_t ME_INVALID = 1u << 19;
 constexpr int ME_LOW_CONTRAST = 12;
@@ -261,20 +264,26 @@ __device__ __forceinline__ void build_lb_map(const Sx &S, int lane) {
     const int ya = min(y0 + t, WIN_ROWS - 1), yb = min(y0 + t + 1, WIN_ROWS - 1);
     v1[t] = lerp4(S.win[ya * WIN_WORDS + n], S.win[yb * WIN_WORDS + n]);
   }
-  uint8_t *mp = reinterpret_cast<uint8_t *>(S.map) + n;
+  // the byte scatter to the planes in 16-bit pieces: lanes n and n ^ 1 swap
+  // their dwords (one DPP move), the even lane then holds planes 0 and 1 of
+  // map bytes n, n + 1, the odd lane planes 2 and 3 (one v_perm with a
+  // per-lane selector), written by two ds_write_b16 (lo / d16_hi) instead of
+  // four ds_write_b8: the map build is the largest LDS user of the search
+  const bool odd = n & 1;
+  const uint32_t psel = odd ? 0x03070206u : 0x05010400u;  // [x.b2 h.b2 x.b3 h.b3] : [h.b0 x.b0 h.b1 x.b1]
+  uint8_t *mp = reinterpret_cast<uint8_t *>(S.map) + (n & ~1) + (odd ? 2 * MAP_PLANE_BYTES : 0);
 #pragma unroll
   for (int t = 0; t < RPC; t++) {
     const uint32_t v = lerp4(v1[t], v1[t + 2]);  // rows y..y+3
     const uint32_t h1 = lerp4(v, align4(from_next_lane_wave(v), v, 1));
     const uint32_t h2 = lerp4(h1, align4(from_next_lane_wave(h1), h1, 2));
+    const uint32_t x = dpp<0xB1>(h2);  // the neighbour's (quad_perm [1,0,3,2])
+    const uint32_t pr = __builtin_amdgcn_perm(x, h2, psel);
     const int y = y0 + t;
-    if (act && y < MAP_ROWS) {  // bytes 0/2 and, after one shift, 1/3 (ds_write_b8[_d16_hi])
-      uint8_t *q = mp + y * MAP_ROW_BYTES;
-      const uint32_t h2s = h2 >> 8;
-      q[0] = (uint8_t)h2;
-      q[2 * MAP_PLANE_BYTES] = (uint8_t)(h2 >> 16);
-      q[MAP_PLANE_BYTES] = (uint8_t)h2s;
-      q[3 * MAP_PLANE_BYTES] = (uint8_t)(h2s >> 16);
+    if (act && y < MAP_ROWS) {
+      uint16_t *q = reinterpret_cast<uint16_t *>(mp + y * MAP_ROW_BYTES);
+      q[0] = (uint16_t)pr;
+      q[MAP_PLANE_BYTES / 2] = (uint16_t)(pr >> 16);
     }
   }
 }
@@ -364,7 +373,7 @@ __device__ __forceinline__ unsigned finish_groups(const Sx &S, int n, int lane) 
   unsigned bk = 0xFFFFFFFFu;
   for (int c0 = 0; c0 < n; c0 += PER) {
     const int j = c0 + slot;
-    const unsigned ord = j < n ? S.list[j] : 1u;
+    const unsigned ord = j < n ? S.list[j] & KEY_ORD : 1u;
     int cdx, cdy;
     ord_pos(ord, cdx, cdy);
     const int cb = WIN_OX + cdx, csh = cb & 3;
@@ -415,6 +424,93 @@ __device__ __forceinline__ unsigned finish_list(const Sx &S, int n, int lane) {
   return wave_min(bk);
 }
 
+
+// Two-stage finishing of many survivors (more than 8; SURVEY.md 8(d)'s
+// content leaves ~46 at the median, smooth texture under N(0,4) noise): the
+// first stage computes, one candidate per lane, the exact SAD of rows 0..7
+// only (the current rows 0..7 wave-uniform in SGPRs, no LDS broadcast) and
+// adds the lower bound of rows 8..15 from the sub-block averages, 16 Sbot -
+// 256 (Sbot: the candidate's terms of sub-block rows 2 and 3, carried in its
+// list entry above the ord); a candidate whose
+//     LB2 = SAD(rows 0..7) + 16 Sbot - 256 > T
+// can neither win nor tie (LB2 <= SAD, per sub-block as in me_full's bound).
+// The few left (c* excluded: its key is known) are compacted in place with
+// their half SAD and finished over rows 8..15 by lane groups.  Half the
+// window reads and SADs of one-per-lane finishing; the result is unchanged.
+// tools/me_sim.py-style model on the survey content: 46 -> 1 at the median.
+template <class G, int RG>
+__device__ __forceinline__ unsigned finish_bottom(const Sx &S, int n, int lane) {
+  constexpr int GL = 4 * RG, PER = 64 / GL, NR = 8 / RG;  // lanes per candidate, rows per lane
+  const int d = lane & 3, rg = (lane >> 2) & (RG - 1), slot = lane / GL;
+  uint32_t cw[NR];
+#pragma unroll
+  for (int t = 0; t < NR; t++) cw[t] = S.cur[4 * (8 + rg + RG * t) + d];
+  unsigned bk = 0xFFFFFFFFu;
+  for (int c0 = 0; c0 < n; c0 += PER) {
+    const int j = c0 + slot;
+    const unsigned e = j < n ? S.list[j] : 1u;
+    const unsigned ord = e & KEY_ORD;
+    int cdx, cdy;
+    ord_pos(ord, cdx, cdy);
+    const int cb = WIN_OX + cdx, csh = cb & 3;
+    const lds_u32 *p0 = lds_base(S.win + (WIN_OY + cdy + 8 + rg) * G::WS + (cb >> 2) + d);
+    uint32_t a = 0;
+#pragma unroll
+    for (int t = 0; t < NR; t++) {
+      const lds_u32 *p = p0 + RG * t * G::WS;
+      a = sad4(align4(p[1], p[0], csh), cw[t], a);
+    }
+    a += dpp<0xB1>(a);
+    a += dpp<0x4E>(a);
+    if (RG >= 2) a += dpp<0x141>(a);
+    if (RG >= 4) a += dpp<0x140>(a);
+    a += e >> KEY_SHIFT;  // + the SAD of rows 0..7
+    if (j < n) bk = min(bk, (a << KEY_SHIFT) | ord);
+  }
+  return wave_min(bk);
+}
+template <class G>
+__device__ __forceinline__ unsigned finish_halves(const Sx &S, const uint8_t *cur_blk, int w, int n, unsigned T,
+                                                  unsigned cstar_ord, int lane) {
+  lds_u32 *list = as_lds(S.list);
+  uint32_t cs[64];
+  load_cur_rows8<0>(cur_blk, w, cs);  // rows 0..7 as wave-uniform dwords (SGPRs)
+  int n2 = 0;
+  for (int c0 = 0; c0 < n; c0 += 64) {  // uniform
+    const bool act = c0 + lane < n;
+    const unsigned e = act ? (unsigned)list[c0 + lane] : 1u;
+    const unsigned ord = e & KEY_ORD;
+    int cdx, cdy;
+    ord_pos(ord, cdx, cdy);
+    const int cb = WIN_OX + cdx, csh = cb & 3;
+    const lds_u32 *p0 = lds_base(S.win + (WIN_OY + cdy) * G::WS + (cb >> 2));
+    uint32_t a = 0;
+#pragma unroll
+    for (int r = 0; r < 8; r++) {
+      const lds_u32 *p = p0 + r * G::WS;
+      const uint32_t a0 = p[0], a1 = p[1], a2 = p[2], a3 = p[3], a4 = p[4];
+      a = sad4(align4(a1, a0, csh), cs[4 * r + 0], a);
+      a = sad4(align4(a2, a1, csh), cs[4 * r + 1], a);
+      a = sad4(align4(a3, a2, csh), cs[4 * r + 2], a);
+      a = sad4(align4(a4, a3, csh), cs[4 * r + 3], a);
+    }
+    const int lb2 = (int)a + 16 * (int)(e >> KEY_SHIFT) - 256;
+    const bool sv = act && ord != cstar_ord && lb2 <= (int)T;
+    const uint64_t bl = __ballot(sv);
+    // compacted in place: every entry of this chunk was read above, and the
+    // write index never reaches the next chunk
+    const int idx = n2 + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bl >> 32),
+                                                        __builtin_amdgcn_mbcnt_lo((uint32_t)bl, 0u));
+    if (sv) list[idx] = ord | (a << KEY_SHIFT);
+    n2 += __popcll(bl);
+  }
+  n2 = uni(n2);
+  if (n2 == 0) return 0xFFFFFFFFu;
+  wsync();
+  if (n2 <= 4) return finish_bottom<G, 4>(S, n2, lane);
+  if (n2 <= 8) return finish_bottom<G, 2>(S, n2, lane);
+  return finish_bottom<G, 1>(S, n2, lane);
+}
 
 // Candidate layouts of the FULL search: lane = (dy group q, dx lane dxi),
 // ND vertically consecutive candidates per lane.  Search limits up to 15
@@ -505,8 +601,8 @@ __device__ __forceinline__ void me_full(const Sx &S, const uint8_t *cur_blk, int
   sad_zero_hf<G>(S, lane, sad0, ehf);
   sad0 = uni(sad0);
   sad0_out = sad0;
-  unsigned bk = 0xFFFFFFFFu, ckey = 0xFFFFFFFFu, Ts = 0, pk = 0;
-  uint32_t acc[ND];
+  unsigned bk = 0xFFFFFFFFu, ckey = 0xFFFFFFFFu, Ts = 0, pk = 0, T = 0;
+  uint32_t acc[ND], sb[ND];  // bound sums packed (low: sub-block rows 0-1, high: 2-3), and S
   lds_u32 *list = as_lds(S.list);  // (one-MB image: aliases the map once the map is dead)
   int nsurv = 1000;
   // Low-contrast blocks (sub-block averages within a few levels) prune almost
@@ -541,18 +637,25 @@ __device__ __forceinline__ void me_full(const Sx &S, const uint8_t *cur_blk, int
 #pragma unroll
         for (int j = 0; j < 4; j++) {
           const int d = i - 4 * j;
-          if (d >= 0 && d < ND) acc[d] = sad4(m4, cm[j], acc[d]);
+          // sub-block rows 0, 1 in the low half, rows 2, 3 (Sbot, finish_halves) in the high half
+          if (d >= 0 && d < ND)
+            acc[d] = j < 2 ? sad4(m4, cm[j], acc[d]) : __builtin_amdgcn_sad_hi_u8(m4, cm[j], acc[d]);
         }
       }
     }
-    mark_invalid(acc);
+#pragma unroll
+    for (int d = 0; d < ND; d++) {  // S = low + high half, one v_dot2_u32_u16
+      typedef unsigned short u16x2_t __attribute__((ext_vector_type(2)));
+      sb[d] = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2_t, acc[d]), (u16x2_t){1, 1}, 0u, false);
+    }
+    mark_invalid(sb);
 
     // 2. c* and its full SAD
     SECTION("cstar");
     {  // least (S, d) of the lane as S << 4 | d, then its key S << 10 | ord
       unsigned m = 0xFFFFFFFFu;
 #pragma unroll
-      for (int d = 0; d < ND; d++) m = min(m, (acc[d] << 4) | (unsigned)d);
+      for (int d = 0; d < ND; d++) m = min(m, (sb[d] << 4) | (unsigned)d);
       if (!lane_ok) m = ME_INVALID << 4;
       pk = m == 0xFFFFFFFFu ? m : ((m >> 4) << KEY_SHIFT) + base + (m & 15u);
     }
@@ -565,7 +668,7 @@ __device__ __forceinline__ void me_full(const Sx &S, const uint8_t *cur_blk, int
       const uint32_t s = sad4(align4(p[1], p[0], cb & 3), S.cur[lane], 0u);
       ckey = (pk & KEY_ORD) | ((unsigned)uni(wave_sum((int)s)) << KEY_SHIFT);
     }
-    const unsigned T = min(ckey >> KEY_SHIFT, (unsigned)sad0);
+    T = min(ckey >> KEY_SHIFT, (unsigned)sad0);
     Ts = (T + 512u) >> 4;  // survivors: S <= Ts
 
     SECTION("survivors");
@@ -575,12 +678,13 @@ __device__ __forceinline__ void me_full(const Sx &S, const uint8_t *cur_blk, int
     if (lane_ok) {  // (the idle lanes sit out: their sums are not masked)
 #pragma unroll
     for (int d = 0; d < ND; d++) {
-      const bool sv = acc[d] <= Ts;
+      const bool sv = sb[d] <= Ts;
       const uint64_t bl = __ballot(sv);
       if (bl) {
         const int idx = nsurv + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bl >> 32),
                                                                __builtin_amdgcn_mbcnt_lo((uint32_t)bl, 0u));
-        if (sv && idx < ME_LIST_MAX) list[idx] = base + d;
+        // the entry: ord | Sbot << KEY_SHIFT (finish_halves)
+        if (sv && idx < ME_LIST_MAX) list[idx] = (base + d) | ((acc[d] >> 16) << KEY_SHIFT);
         nsurv += __popcll(bl);
       }
     }
@@ -592,16 +696,16 @@ __device__ __forceinline__ void me_full(const Sx &S, const uint8_t *cur_blk, int
   if (nsurv <= ME_LIST_MAX) {
     wsync();
     // nothing to finish when c* (whose key is known) is the only survivor
-    if (nsurv == 0 || (nsurv == 1 && (unsigned)uni((int)list[0]) == (pk & KEY_ORD)))
+    if (nsurv == 0 || (nsurv == 1 && ((unsigned)uni((int)list[0]) & KEY_ORD) == (pk & KEY_ORD)))
       ;
     else if (nsurv <= 4)
       bk = finish_groups<G, 4>(S, nsurv, lane);
     else if (nsurv <= 8)
       bk = finish_groups<G, 2>(S, nsurv, lane);
-    else if (nsurv <= 32)
+    else if (nsurv <= ME_GROUPS_MAX)
       bk = finish_groups<G, 1>(S, nsurv, lane);
     else
-      bk = finish_list<G>(S, nsurv, lane);
+      bk = finish_halves<G>(S, cur_blk, w, nsurv, T, pk & KEY_ORD, lane);
   } else if (range < 4 && uni(ND < 15 ? window_constant<G, WIN15_R0, WIN15_NR>(S, lane)
                                        : window_constant<G>(S, lane))) {
     bk = 0xFFFFFFFFu;  // constant window (checked for nearly flat blocks): (0,0), below

@@ -177,46 +177,68 @@ struct BitWriter {
   }
 };
 
-// the codes of one block's levels (EncodeAC codec.c:96 / CBPEncodeAC
-// codec.c:141), scan positions from `s0` (1 for intra blocks: the DC is
-// coded alone); EMIT: into the writer, else only counted.  Returns the
-// bits, EOB included (0 for a CBP-type block without a level: nothing is
-// written, codec.c:151).
-template <bool EMIT>
-__device__ __forceinline__ int block_codes(const VlcTables &T, const uint32_t lv[32], bool cbpt, BitWriter &bw) {
-  int bits = 0, run = 0;
-  bool first = cbpt, any = false;
+// the scan positions of a block holding a nonzero level, as two 32-bit masks
+// (bit p of m0: position p; of m1: position 32 + p) from its 32 packed level
+// pairs: v_pk_min_u16 against 1 (a nonzero int16 is >= 1 as u16), v_dot2
+// (low + 2 high) and v_lshl_or -- three VALU per pair
+typedef unsigned short u16x2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void nz_masks(const uint32_t lv[32], uint32_t &m0, uint32_t &m1) {
+  m0 = m1 = 0;
 #pragma unroll
-  for (int sp = 0; sp < 64; sp++) {
-    if (!cbpt && sp == 0) continue;
-    const int l = (int)(int16_t)((lv[sp >> 1] >> (16 * (sp & 1))) & 0xffffu);
-    if (l != 0) {
-      const int al = l < 0 ? -l : l;
-      uint32_t v;
-      int n;
-      if (first && run == 0 && al == 1) {
-        const Code f = tab(T, T_FIRST01);
-        v = (f.v << 1) | (uint32_t)(l < 0);
-        n = f.len + 1;
-      } else {
-        const Code e = (run < 27 && al < 16) ? tab(T, T_TC + run * 16 + al) : Code{0u, 0};
-        if (e.len) {
-          v = (e.v << 1) | (uint32_t)(l < 0);
-          n = e.len + 1;
-        } else {  // ESCAPE, 6-bit run, 8-bit level
-          const Code esc = tab(T, T_ESC);
-          v = (esc.v << 14) | ((uint32_t)run << 8) | ((uint32_t)l & 0xffu);
-          n = esc.len + 14;
-        }
-      }
-      if (EMIT) bw.put(v, n);
-      bits += n;
-      first = false;
-      any = true;
-      run = 0;
+  for (int i = 0; i < 32; i++) {
+    const u16x2_t v = __builtin_bit_cast(u16x2_t, lv[i]);
+    const u16x2_t r = __builtin_elementwise_min(v, (u16x2_t){1, 1});
+    const uint32_t b = __builtin_amdgcn_udot2(r, (u16x2_t){1, 2}, 0u, false);
+    if (i < 16)
+      m0 |= b << (2 * i);
+    else
+      m1 |= b << (2 * (i - 16));
+  }
+}
+
+// the codes of one block's levels (EncodeAC codec.c:96 / CBPEncodeAC
+// codec.c:141), scan positions from 1 for intra blocks (the DC is coded
+// alone: the caller leaves bit 0 out of m0); EMIT: into the writer, else only
+// counted.  Returns the bits, EOB included (0 for a CBP-type block without a
+// level: nothing is written, codec.c:151).  Visits the nonzero positions only
+// (m0/m1, lowest first), each level read from the lane's scan-order copy in
+// LDS (lvs): as many steps as the block has levels, not 64.
+template <bool EMIT>
+__device__ __forceinline__ int block_codes(const VlcTables &T, const uint16_t *lvs, uint32_t m0, uint32_t m1,
+                                           bool cbpt, BitWriter &bw) {
+  const bool any = (m0 | m1) != 0;
+  int bits = 0, last = cbpt ? -1 : 0;
+  bool first = cbpt;
+  while (m0 | m1) {
+    const int p = m0 ? __builtin_ctz(m0) : 32 + __builtin_ctz(m1);
+    if (m0)
+      m0 &= m0 - 1u;
+    else
+      m1 &= m1 - 1u;
+    const int l = (int)(int16_t)lvs[p];
+    const int run = p - last - 1;
+    last = p;
+    const int al = l < 0 ? -l : l;
+    uint32_t v;
+    int n;
+    if (first && run == 0 && al == 1) {
+      const Code f = tab(T, T_FIRST01);
+      v = (f.v << 1) | (uint32_t)(l < 0);
+      n = f.len + 1;
     } else {
-      run++;
+      const Code e = (run < 27 && al < 16) ? tab(T, T_TC + run * 16 + al) : Code{0u, 0};
+      if (e.len) {
+        v = (e.v << 1) | (uint32_t)(l < 0);
+        n = e.len + 1;
+      } else {  // ESCAPE, 6-bit run, 8-bit level
+        const Code esc = tab(T, T_ESC);
+        v = (esc.v << 14) | ((uint32_t)run << 8) | ((uint32_t)l & 0xffu);
+        n = esc.len + 14;
+      }
     }
+    if (EMIT) bw.put(v, n);
+    bits += n;
+    first = false;
   }
   if (cbpt && !any) return 0;
   const Code eob = tab(T, T_EOB);
@@ -234,9 +256,11 @@ __device__ __forceinline__ int block_codes(const VlcTables &T, const uint32_t lv
 //     into mb_bits[stream position]
 //   emit  (EMIT true):  each block's codes from its bit offset: the MB's
 //     offset (k_vlc_scan) + its header + the blocks before it
+constexpr int VLC_STAGE = 144;  // bytes per lane of the level copy: 128 + 16 pad (ds_write_b128 without conflicts)
 template <bool EMIT>
 __global__ __launch_bounds__(64 * VLC_WAVES) void k_vlc_blk(VlcArgs a, VlcTables Tg) {
   __shared__ VlcTables T;  // per-lane table lookups from LDS, loaded once per workgroup
+  __shared__ __align__(16) uint8_t stage[VLC_WAVES * 64 * VLC_STAGE];  // each lane's levels, scan order
   for (int i = threadIdx.x; i < T_N; i += 64 * VLC_WAVES) T.t[i] = Tg.t[i];
   __syncthreads();
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -271,11 +295,22 @@ __global__ __launch_bounds__(64 * VLC_WAVES) void k_vlc_blk(VlcArgs a, VlcTables
       lv[4 * i + 3] = v[3];
     }
   }
+  // the block's nonzero positions (the DC of an intra block is coded apart)
+  // and its levels in LDS for the indexed reads of block_codes
+  uint32_t m0, m1;
+  nz_masks(lv, m0, m1);
+  if (!cbpt) m0 &= ~1u;
+  if (!coded) m0 = m1 = 0;
+  uint8_t *stl = stage + (wv * 64 + lane) * VLC_STAGE;
+#pragma unroll
+  for (int i = 0; i < 8; i++)
+    *reinterpret_cast<uint4 *>(stl + 16 * i) = make_uint4(lv[4 * i], lv[4 * i + 1], lv[4 * i + 2], lv[4 * i + 3]);
+  const uint16_t *lvs = reinterpret_cast<const uint16_t *>(stl);
   BitWriter bw;
   uint32_t *out = a.out + (size_t)fi * a.out_words;
   if (!EMIT) {
     const Header hd = header_codes(T, r, rp, mq, m);
-    int bb = coded ? block_codes<false>(T, lv, cbpt, bw) + (cbpt ? 0 : 8) : 0;  // (intra: + DC)
+    int bb = coded ? block_codes<false>(T, lvs, m0, m1, cbpt, bw) + (cbpt ? 0 : 8) : 0;  // (intra: + DC)
     // the MB's six lanes: header and block bits into blk_bits, the total
     uint16_t *bk = a.blk_bits + (base + k) * 8;
     if (act) bk[1 + b] = (uint16_t)bb;
@@ -322,7 +357,7 @@ __global__ __launch_bounds__(64 * VLC_WAVES) void k_vlc_blk(VlcArgs a, VlcTables
         const int dc = dc0 < 1 ? 1 : (dc0 > 254 ? 254 : dc0);
         bw.put((uint32_t)(dc == 128 ? 255 : dc), 8);
       }
-      block_codes<true>(T, lv, cbpt, bw);
+      block_codes<true>(T, lvs, m0, m1, cbpt, bw);
       bw.finish();
     }
   }

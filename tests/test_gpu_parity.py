@@ -480,6 +480,45 @@ def test_library_me_scratch_per_stream_and_graph_safe(p64, torch_dev):
     assert p64.lib().p64gpu_release_scratch() == 0
 
 
+def test_capture_fork_join_side_stream_without_me(p64, torch_dev):
+    """An inter encode with args.me == NULL launched on a side stream that a
+    capture forked from its stream and joined back (the two-stream pattern
+    of DESIGN.md 9b): the captured call takes the fused kernel (no library
+    scratch under capture), its replay equals the eager split-kernel call."""
+    torch = torch_dev
+    w, h, S = 176, 144, 4
+    nmb, pic = 99, w * h * 3 // 2
+    fr = p64.synth_frames_device(w, h, 1, S, 0, 2, content=p64.SYNTH_SURVEY)
+    li0 = torch.zeros(S * nmb, dtype=torch.uint8, device="cuda")
+    r0 = torch.zeros(S * pic, dtype=torch.uint8, device="cuda")
+    p64.encode_frames(fr[0].reshape(-1), None, r0, li0, width=w, height=h, intra=True)
+    cap, side = torch.cuda.Stream(), torch.cuda.Stream()
+    res = []
+    for graph in (False, True):
+        rec = torch.zeros_like(r0)
+        li = li0.clone()
+        coef = torch.zeros((S, nmb, 6, 64), dtype=torch.int16, device="cuda")
+        mb = torch.empty((S, nmb, 4), dtype=torch.int8, device="cuda")
+        torch.cuda.synchronize()
+        if graph:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=cap):
+                side.wait_stream(cap)
+                with torch.cuda.stream(side):
+                    _raw_encode(p64, torch, fr[1].reshape(-1), r0, rec, li, coef, mb, w=w, h=h, stream=side)
+                cap.wait_stream(side)
+            torch.cuda.synchronize()
+            li.copy_(li0)
+            g.replay()
+        else:
+            _raw_encode(p64, torch, fr[1].reshape(-1), r0, rec, li, coef, mb, w=w, h=h,
+                        stream=torch.cuda.current_stream())
+        torch.cuda.synchronize()
+        res.append((host(coef), host(mb), host(rec), host(li)))
+    for a, b in zip(*res):
+        np.testing.assert_array_equal(a, b)
+
+
 def test_library_me_scratch_per_thread_stream(p64, torch_dev):
     """hipStreamPerThread stands for each calling thread's own stream: two
     threads encoding without an ME-record output on it, at the same time,

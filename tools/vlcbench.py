@@ -1,4 +1,6 @@
-"""Times the GPU entropy coder on the bench workload's records (GPU box)."""
+"""Times the GPU entropy coder on the bench workload's records (GPU box).
+usage: python tools/vlcbench.py [survey|synth]  (rocprofv3 --kernel-trace
+gives the per-kernel split: tools/vlc_prof.sh)"""
 import os
 import sys
 import time
@@ -12,7 +14,8 @@ from p64_amd import stream  # noqa: E402
 w, h, S = 352, 288, 256
 nmb = 396
 pic = w * h * 3 // 2
-fr = p64_amd.synth_frames_device(w, h, 1, S, 0, 2)
+content = sys.argv[1] if len(sys.argv) > 1 else "survey"
+fr = p64_amd.synth_frames_device(w, h, 1, S, 0, 2, content=p64_amd.CONTENTS[content])
 li = torch.zeros(S * nmb, dtype=torch.uint8, device="cuda")
 r0 = torch.zeros(S * pic, dtype=torch.uint8, device="cuda")
 r1 = torch.zeros_like(r0)
