@@ -49,6 +49,7 @@ encoder from oracle/_ref, 1 process and one per core of the box's share).
 from __future__ import annotations
 
 import argparse
+import dataclasses
 import json
 import os
 import socket
@@ -95,6 +96,9 @@ INTRA_BYTES_PER_MB = 384 + 768 + 384 + 4 + 1
 PROFILE_TIMED = "profiles/r05_timed_region.json"  # {workload key: {kernel: mean us}}
 # executed v_sad_u8 work of k_motion per launch (tools/sad_count.py side build)
 PROFILE_SAD = "profiles/sad_executed.json"
+VALU_BUSY_NOTE = ("derived, not a busy counter: SQ_INSTS_VALU (PMC) x the kernel's mean VALU issue cost "
+                  "(static ISA mix priced by tools/ubench_valu's measured clocks, tools/pmc_merge.py) / "
+                  "(1024 SIMDs x kernel cycles)")
 MAX_SLOTS = 256  # distinct input pictures per sequence kept resident (~10 GB at S=256 CIF)
 
 
@@ -124,6 +128,10 @@ def parse(argv=None):
                    help="local: every rank generates its own sequences (default, no data-path "
                         "collective); root: rank 0 holds all inputs, RCCL-scatters each step's "
                         "pictures and gathers the levels/records back (the timed step includes both)")
+    p.add_argument("--gather", choices=("coded", "levels"), default="coded",
+                   help="--feed root: what rank 0 collects each step -- coded (default: every "
+                        "picture's H.261 bits, entropy-coded on its rank's GPU inside the step) or "
+                        "levels (the int16 levels + records, 768 B/MB: parity debugging)")
     p.add_argument("--eager", action="store_true",
                    help="launch every timed step from Python instead of replaying a captured HIP graph")
     p.add_argument("--spinup-ms", type=int, default=150,
@@ -202,6 +210,33 @@ def gather_outputs(world: int, rank: int, local, bufs):
     byte = lambda t: t.contiguous().view(torch.uint8)  # noqa: E731
     dist.gather(byte(local), gather_list=[byte(b) for b in bufs] if rank == 0 else None, dst=0)
     return bufs
+
+
+def gather_coded(world, rank, out, bits):
+    """--feed root, coded: every rank's entropy-coded pictures to rank 0.
+    out [S, stride] uint8 holds each picture's bits from byte 0 (at its
+    sequence's bit phase), bits [S] int32 their counts incl. the phase.  One
+    MAX all-reduce of the longest picture, then the first nb bytes of every
+    picture (nb = that length, 4-aligned) and the counts, gathered as bytes:
+    ~S x nb bytes per rank instead of S x nmb x 772 for the levels.  Returns
+    on rank 0 ([world] payloads [S, nb], [world] bit counts [S]), else None."""
+    import torch
+    import torch.distributed as dist
+    mx = bits.to(torch.int64).max().reshape(1)
+    if world > 1:
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+    nb = (int(mx.item()) + 7) // 8
+    nb = max(4, (nb + 3) // 4 * 4)
+    payload = out[:, :nb].contiguous()
+    b32 = bits.to(torch.int32).contiguous()
+    if world == 1:
+        return [payload], [b32]
+    pays = [torch.empty_like(payload) for _ in range(world)] if rank == 0 else None
+    bl = [torch.empty_like(b32) for _ in range(world)] if rank == 0 else None
+    dist.gather(payload, gather_list=pays, dst=0)
+    dist.gather(b32.view(torch.uint8), gather_list=[b.view(torch.uint8) for b in bl] if rank == 0 else None,
+                dst=0)
+    return (pays, bl) if rank == 0 else None
 
 
 def free_port() -> int:
@@ -697,10 +732,10 @@ def main(argv=None):
         all_frames = (make_inputs(torch, p64_amd, args.content, w, h, 1, world * S, nslots)
                       if rank == 0 else None)
         frames = torch.empty((nslots, S, pic), dtype=torch.uint8, device="cuda")
+        lv = rank == 0 and args.gather == "levels"
         coef_bufs = ([torch.empty((S, nmb, 6, 64), dtype=torch.int16, device="cuda")
-                      for _ in range(world)] if rank == 0 else None)
-        mb_bufs = ([torch.empty((S, nmb, 4), dtype=torch.int8, device="cuda") for _ in range(world)]
-                   if rank == 0 else None)
+                      for _ in range(world)] if lv else None)
+        mb_bufs = [torch.empty((S, nmb, 4), dtype=torch.int8, device="cuda") for _ in range(world)] if lv else None
     else:
         frames = make_inputs(torch, p64_amd, args.content, w, h, seed0, S, nslots)
 
@@ -726,29 +761,52 @@ def main(argv=None):
         nz_all = torch.empty((ncoef, S, nmb), dtype=torch.uint8, device="cuda")
         mb_all = torch.empty((ncoef, S, nmb, 4), dtype=torch.int8, device="cuda")
         me = torch.empty((S, nmb, 7), dtype=torch.int32, device="cuda")
+        # --feed root --gather coded: the encoder counts the coded bits for the in-step VLC
+        vb_root = (torch.empty((S, nmb, 8), dtype=torch.int16, device="cuda")
+                   if root and args.gather == "coded" else None)
+
         def out_of(t):
             i = slot(t) if keep else (1 if t == vt else (2 if t == last else 0))
-            return p64_amd.FrameBatchOut(coef=coef_all[i], mb=mb_all[i], me=me, nz=nz_all[i])
+            return p64_amd.FrameBatchOut(coef=coef_all[i], mb=mb_all[i], me=me, nz=nz_all[i], vlc_bits=vb_root)
         # the checked pictures' buffers were written by no earlier step
         fresh = {t: (not keep) or (1 + args.warmup + args.steps <= nslots) for t in (vt, last)}
 
         def pre(t):  # --feed root: this step's pictures from rank 0
             scatter_pictures(world, rank, all_frames[slot(t)] if rank == 0 else None, frames[slot(t)])
 
-        def launch(t):
+        def launch(t, vlc_bits=None):  # vlc_bits: the entropy coder's block bits, counted by the encoder
+            o = out_of(t)
+            if vlc_bits is not None:
+                o = dataclasses.replace(o, vlc_bits=vlc_bits)
             p64_amd.encode_frames(frames[slot(t)].reshape(-1), rec[(t + 1) % 2], rec[t % 2], li,
                                   width=w, height=h, intra=(t == 0), quant=args.quant,
-                                  me_mode=mode, search_limit=args.search_limit, out=out_of(t))
+                                  me_mode=mode, search_limit=args.search_limit, out=o)
 
-        def post(t):  # --feed root: levels and records back to rank 0
+        if root and args.gather == "coded":  # each rank entropy-codes its pictures in the step
+            from p64_amd import stream as p64s
+            vbufs = p64s.vlc_buffers(S, w, h)
+            gq = torch.full((S, nmb // 33), args.quant, dtype=torch.uint8, device="cuda")
+            seq_bits = torch.zeros(S, dtype=torch.int64, device="cuda")  # bits so far per sequence
+            coded_last = {}
+
+        def post(t):  # --feed root: the coded pictures (or levels and records) back to rank 0
             o = out_of(t)
-            gather_outputs(world, rank, o.coef, coef_bufs)
-            gather_outputs(world, rank, o.mb, mb_bufs)
+            if args.gather == "levels":
+                gather_outputs(world, rank, o.coef, coef_bufs)
+                gather_outputs(world, rank, o.mb, mb_bufs)
+                return
+            # the picture continues its sequence's stream at bit phase seq_bits % 8
+            phase = (seq_bits & 7).to(torch.uint8)
+            tr = torch.full((S,), t % 32, dtype=torch.int32, device="cuda")
+            out, bits = p64s.vlc_pictures(o.mb, o.coef, gq, tr, width=w, height=h, phase=phase,
+                                          buffers=vbufs, host_bits=False, blk_bits=o.vlc_bits)
+            seq_bits.add_(bits.to(torch.int64) - phase.to(torch.int64))
+            coded_last["gathered"] = gather_coded(world, rank, out, bits)
 
-        def step(t):
+        def step(t, vlc_bits=None):
             if root:
                 pre(t)
-            launch(t)
+            launch(t, vlc_bits)
             if root:
                 post(t)
 
@@ -875,14 +933,17 @@ def main(argv=None):
             "metric": METRICS[args.config], "value": round(value, 1),
             "ms_per_step": round(tmax / args.steps * 1e3, 4),
             "config": {"workload": workload, "content": args.content, "feed": args.feed,
+                       **({"gather": args.gather} if root else {}),
                        "width": w, "height": h, "me": args.mode,
                        "search_limit": args.search_limit, "quant": args.quant,
                        "sequences_per_gpu": S, "macroblocks_per_step_per_gpu": mbs_launch,
                        "distinct_input_pictures": nslots,
                        "parallelism": (f"dp{world} (independent sequences per GPU, no data-path "
                                        f"collective)" if not root else
-                                       f"dp{world} (rank 0 RCCL-scatters pictures, gathers levels "
-                                       f"+ records; roofline times the encode launch alone)")},
+                                       f"dp{world} (rank 0 RCCL-scatters pictures, gathers "
+                                       + ("the entropy-coded pictures (GPU VLC on each rank in the step)"
+                                          if args.gather == "coded" else "levels + records")
+                                       + "; roofline times the encode launch alone)")},
             "roofline": roofline(mbs_launch * BYTES_PER_MB_FIXED + lvl_bytes, kavg, kernel, pmc,
                                  algorithmic_bytes_per_mb=round(BYTES_PER_MB_FIXED + lvl_bytes / mbs_launch, 1),
                                  timing=timing_note(args, root),
@@ -904,6 +965,7 @@ def main(argv=None):
                         "(exact pruning, DESIGN.md 5): see roofline_sad_executed"},
             "roofline_sad_executed": sad_executed(args, key, kme, clk, mbs_launch),
             "valu_busy": (pmc or {}).get("valu_busy"),
+            "valu_busy_note": VALU_BUSY_NOTE,
             "steady_state": clk,
             "with_vlc": with_vlc,
             "verified_vs_oracle": verified,
@@ -1043,14 +1105,17 @@ def measure_vlc(args, torch, p64_amd, step, out_of, S, nmb, w, h):
     """The encode steps followed by entropy coding on the device (p64vlc.hip):
     the whole-encoder rate to .p64 bits, measured after the metric (it re-runs
     steps, so the closed-loop state is not reused).  Per step: the encode
-    launches, the three VLC launches and a copy of every picture's bit count
-    to pinned host memory, the steps captured in one HIP graph (as the
-    metric's steps are) and replayed once, wall-clock timed."""
+    launches -- which also count every transmitted block's coded bits
+    (vlc_bits) -- the entropy coder's header/offset and emit launches from
+    those counts (no count pass over the levels), and a copy of every
+    picture's bit count to pinned host memory; the steps captured in one HIP
+    graph (as the metric's steps are) and replayed once, wall-clock timed."""
     try:
         from p64_amd import stream as p64s
         ngob = nmb // 33
         gq = torch.full((S, ngob), args.quant, dtype=torch.uint8, device="cuda")
         bufs = p64s.vlc_buffers(S, w, h)
+        vb = torch.empty((S, nmb, 8), dtype=torch.int16, device="cuda")  # the encoder's block bits
         vsteps = min(args.steps, 8)
         trs = [torch.full((S,), (1 + args.warmup + k) % 32, dtype=torch.int32, device="cuda")
                for k in range(vsteps)]
@@ -1063,12 +1128,12 @@ def measure_vlc(args, torch, p64_amd, step, out_of, S, nmb, w, h):
 
         def vstep(k, ev=False):
             t = 1 + args.warmup + k
-            step(t)
+            step(t, vb)
             o = out_of(t)
             if ev:
                 vlc_ev[0].record()
             _, bits_dev[k] = p64s.vlc_pictures(o.mb, o.coef, gq, trs[k], width=w, height=h, buffers=bufs,
-                                               host_bits=False)
+                                               host_bits=False, blk_bits=vb)
             if ev:
                 vlc_ev[1].record()
             host[k].copy_(bits_dev[k], non_blocking=True)
@@ -1094,9 +1159,10 @@ def measure_vlc(args, torch, p64_amd, step, out_of, S, nmb, w, h):
                 "ms_per_step": round(dt / vsteps * 1e3, 4),
                 "vlc_ms_last_step": round(vlc_ev[0].elapsed_time(vlc_ev[1]), 4),
                 "avg_bits_per_mb": round(float(hb.sum()) / (S * nmb * vsteps), 2),
-                "note": "encode launches + GPU entropy coding (count, scan, emit) per step, every "
-                        "picture's bit count copied to pinned host memory, the steps replayed as one "
-                        "HIP graph; not part of `value`"}
+                "note": "encode launches (counting each transmitted block's coded bits) + GPU entropy "
+                        "coding (headers + offsets, scan, emit) per step, every picture's bit count "
+                        "copied to pinned host memory, the steps replayed as one HIP graph; not part "
+                        "of `value`"}
     except Exception as e:  # never let the extra measurement cost the bench line
         return {"error": str(e)[:200]}
 
@@ -1156,6 +1222,7 @@ def run_intra(args, torch, dist, np, p64_amd, world, frames, S, nmb, pic, nslots
                                  load_pmc(args.pmc_json, key),
                                  algorithmic_bytes_per_mb=INTRA_BYTES_PER_MB, timing=timing_note(args)),
             "valu_busy": (load_pmc(args.pmc_json, key) or {}).get("valu_busy"),
+            "valu_busy_note": VALU_BUSY_NOTE,
             "steady_state": clk,
             "verified_vs_oracle": verified}
 
@@ -1236,6 +1303,7 @@ def run_decode(args, torch, dist, np, p64_amd, world, enc, S, nmb, pic):
             "roofline": roofline(bpl, kavg, "k_recon_mbg", load_pmc(args.pmc_json, key),
                                  algorithmic_bytes_per_mb=round(bpl / mbs, 1), timing=timing_note(args)),
             "valu_busy": (load_pmc(args.pmc_json, key) or {}).get("valu_busy"),
+            "valu_busy_note": VALU_BUSY_NOTE,
             "steady_state": clk,
             "verified_vs_encoder": {"ok": ok, "note": "last decoded picture == encoder "
                                                       "reconstruction, all sequences"}}

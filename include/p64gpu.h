@@ -48,10 +48,11 @@
  * so inputbuf is exactly: block b's stored levels if its bit is set, else 64
  * zeros (p64gpu_encode_args.coef / .nzmask).
  *
- * ABI version 2 (round 5): p64gpu_encode_args.nzmask (appended); the sparse
- * inter level store of version 1's last revision, now with that mask;
- * p64gpu_vlc_args.flags (was `reserved`, must be 0 or P64GPU_VLC_*) and its
- * scratch of 6*nframes*nmb uint32, 8-byte aligned; synthetic contents.
+ * ABI version 2 (round 5): p64gpu_encode_args.nzmask and .vlc_bits
+ * (appended); the sparse inter level store of version 1's last revision, now
+ * with that mask; p64gpu_vlc_args.flags (was `reserved`, must be 0),
+ * .blk_bits (appended) and its scratch of 6*nframes*nmb uint32, 8-byte
+ * aligned; synthetic contents (p64_synth_content).
  */
 #ifndef P64GPU_H
 #define P64GPU_H
@@ -184,6 +185,15 @@ typedef struct {
                              were stored; clear: the block's levels are all
                              zero).  Intra pictures: 0x3f (the intra DC is
                              1..254)                                         */
+  uint16_t *vlc_bits;     /* NULL or [nframes][nmb][8], 16-byte aligned,
+                             written: entry 1 + b = the coded bits of block b
+                             as the entropy coder writes it (EncodeAC /
+                             CBPEncodeAC codec.c:96-205 incl. EOB, an intra
+                             block's 8-bit DC), 0 if not transmitted; entry 0
+                             and 7 are not written.  Hand it to
+                             p64gpu_vlc_pictures as blk_bits: the coder then
+                             skips its count pass.  Not with
+                             p64gpu_encode_mb_list (P64GPU_E_INVALID)        */
 } p64gpu_encode_args;
 
 /* Alignment: cur, ref, recon and coef 16 bytes; mb and me 4 bytes (the
@@ -247,6 +257,11 @@ typedef struct {
   int64_t out_stride;       /* >= p64gpu_vlc_max_bytes, multiple of 4         */
   uint32_t *bits;           /* [nframes]                                      */
   uint32_t *scratch;        /* [6][nframes][nmb], 8-byte aligned              */
+  uint16_t *blk_bits;       /* NULL, or [nframes][nmb][8] block bits from the
+                               encoder (p64gpu_encode_args.vlc_bits, same
+                               records and levels), 16-byte aligned: the
+                               count pass is skipped; entry 0 is overwritten
+                               with the MB header's bits                     */
 } p64gpu_vlc_args;
 int64_t p64gpu_vlc_max_bytes(int width, int height);
 int p64gpu_vlc_pictures(const p64gpu_vlc_args *args, void *stream);

@@ -75,6 +75,7 @@ class EncodeArgs(ctypes.Structure):
         ("last_intra", ctypes.c_void_p), ("quant_mb", ctypes.c_void_p),
         ("mtype_override", ctypes.c_void_p), ("coef", ctypes.c_void_p),
         ("mb", ctypes.c_void_p), ("me", ctypes.c_void_p), ("nzmask", ctypes.c_void_p),
+        ("vlc_bits", ctypes.c_void_p),
     ]
 
 
@@ -367,6 +368,8 @@ class FrameBatchOut:
     me: object          # int32 [nframes, nmb, 7] or None
     nz: object = None   # uint8 [nframes, nmb] or None: bit 5-b set iff block b
                         # has a nonzero level (its levels were stored)
+    vlc_bits: object = None  # int16 [nframes, nmb, 8] or None: entry 1 + b = block b's
+                        # coded bits for the entropy coder (stream.vlc_pictures blk_bits)
 
 
 def encode_frames(cur, ref, recon, last_intra, *, width: int, height: int, intra: bool,
@@ -410,6 +413,10 @@ def encode_frames(cur, ref, recon, last_intra, *, width: int, height: int, intra
         _dev_check(out.mb, torch.int8, "out.mb")
         if out.coef.numel() < nmb_all * 384 or out.mb.numel() < nmb_all * 4:
             raise P64GpuError("out.coef / out.mb smaller than nframes x nmb records")
+        if out.vlc_bits is not None:
+            _dev_check(out.vlc_bits, torch.int16, "out.vlc_bits")
+            if out.vlc_bits.numel() < nmb_all * 8:
+                raise P64GpuError("out.vlc_bits smaller than nframes x nmb x 8")
         if out.nz is not None:
             _dev_check(out.nz, torch.uint8, "out.nz")
             if out.nz.numel() < nmb_all:
@@ -436,7 +443,8 @@ def encode_frames(cur, ref, recon, last_intra, *, width: int, height: int, intra
                    mtype_override=(mtype_override.data_ptr() if mtype_override is not None else None),
                    coef=out.coef.data_ptr(), mb=out.mb.data_ptr(),
                    me=(me.data_ptr() if me is not None else None),
-                   nzmask=(out.nz.data_ptr() if out.nz is not None else None))
+                   nzmask=(out.nz.data_ptr() if out.nz is not None else None),
+                   vlc_bits=(out.vlc_bits.data_ptr() if out.vlc_bits is not None else None))
     _check(lib().p64gpu_encode_frames(ctypes.byref(a), _stream(torch)))
     return out
 

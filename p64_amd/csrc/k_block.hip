@@ -470,6 +470,63 @@ __device__ __forceinline__ void put_levels(uint8_t *lds, int lane, int k, uint4 
   *reinterpret_cast<uint4 *>(lds + lane * LVL_STRIDE + k * 16) = v;
 }
 
+// ---------------------------------------------------------------------------
+// Coded-bit counts for the entropy coder (p64gpu_encode_args.vlc_bits): a
+// transmitted block's bits -- EncodeAC / CBPEncodeAC codec.c:96-205 incl.
+// EOB, and an intra block's 8-bit DC (EncodeDC codec.c:343) -- counted from
+// the zigzag levels the kernel has just staged in LDS, so the entropy coder
+// needs no count pass over the levels (p64vlc.hip).
+// The TCOEFF code lengths + 1 (sign) by run * 16 + |level| (runs < 27, levels
+// < 16), 20 (ESCAPE 6 + run 6 + level 8) where the table has no code; built on
+// the host from the entropy coder's own tables (p64gpu_abi.hip).
+struct VlcLenTab {
+  uint32_t w[108];  // 432 bytes
+};
+// the positions holding a nonzero level of 16 zigzag level pairs as mask bits
+// 2i, 2i + 1: v_pk_min_u16 against 1, v_dot2 (lo + 2 hi), v_lshl_or
+typedef unsigned short u16x2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t nz2(uint32_t pair) {
+  const u16x2v r = __builtin_elementwise_min(__builtin_bit_cast(u16x2v, pair), (u16x2v){1, 1});
+  return __builtin_amdgcn_udot2(r, (u16x2v){1, 2}, 0u, false);
+}
+// bits of one coded block from its staged levels (lvs, scan order) and its
+// nonzero positions (m0: 0..31, m1: 32..63); cbpt: a type with CBP (the
+// first coefficient may take the short FIRST01 code; no DC of its own),
+// else an intra block (DC as 8 bits, AC from position 1)
+__device__ __forceinline__ int block_vlc_bits(const uint8_t *len, const int16_t *lvs, uint32_t m0, uint32_t m1,
+                                              bool cbpt) {
+  int bits = cbpt ? 2 : 10;  // EOB (+ the intra DC)
+  if (!cbpt) m0 &= ~1u;
+  int last = cbpt ? -1 : 0;
+  bool first = cbpt;
+  while (m0 | m1) {
+    const int p = m0 ? __builtin_ctz(m0) : 32 + __builtin_ctz(m1);
+    if (m0)
+      m0 &= m0 - 1u;
+    else
+      m1 &= m1 - 1u;
+    const int l = lvs[p];
+    const int run = p - last - 1, al = l < 0 ? -l : l;
+    last = p;
+    bits += (first && run == 0 && al == 1) ? 2 : (run < 27 && al < 16 ? (int)len[run * 16 + al] : 20);
+    first = false;
+  }
+  return bits;
+}
+// the table into this wave's LDS copy (108 dwords over the 64 lanes)
+__device__ __forceinline__ void load_vlc_len(const VlcLenTab &vt, uint32_t *dst, int lane) {
+  dst[lane] = vt.w[lane];
+  if (lane < 108 - 64) dst[lane + 64] = vt.w[lane + 64];
+}
+// one uint16 per block into vlc_bits[gmb][1 + b] (slot 0: the entropy coder's)
+__device__ __forceinline__ void store_vlc_bits(const p64gpu_encode_args &a, unsigned nmbs, bool valid, unsigned gmb,
+                                               int b, int bits) {
+  const __amdgpu_buffer_rsrc_t r =
+      __builtin_amdgcn_make_buffer_rsrc((void *)a.vlc_bits, (short)0, (int)(nmbs * 16u), BUF_RSRC_W3);
+  __builtin_amdgcn_raw_buffer_store_b16((uint16_t)bits, r, valid ? (gmb * 8u + 1u + (unsigned)b) * 2u : BUF_OOB, 0,
+                                        0);
+}
+
 struct IntraFetch {
   BlkPos p;
   uint2 rows[8];  // the block's pixels
@@ -506,7 +563,7 @@ struct IntraOut {
 // ChenIDct, reconstruction into `out`
 template <bool CLAMP, bool POW2 = false>
 __device__ __forceinline__ void intra_block(const p64gpu_encode_args &a, const IntraFetch &f, uint8_t *lds,
-                                            int lane, IntraOut &out) {
+                                            int lane, IntraOut &out, uint32_t nzm[2] = nullptr) {
   const int w = a.width, h = a.height;
   const BlkPos &p = f.p;
   const int q = f.q;
@@ -540,6 +597,9 @@ __device__ __forceinline__ void intra_block(const p64gpu_encode_args &a, const I
       uint32_t pk[4];
 #pragma unroll
       for (int j = 0; j < 4; j++) pk[j] = lvl_pair(L, k_zz.inv[8 * k + 2 * j], k_zz.inv[8 * k + 2 * j + 1]);
+      if (nzm)
+#pragma unroll
+        for (int j = 0; j < 4; j++) nzm[k >> 2] |= nz2(pk[j]) << (2 * (4 * (k & 3) + j));
       put_levels(lds, lane, k, make_uint4(pk[0], pk[1], pk[2], pk[3]));
       SCHED_FENCE();
     }
@@ -568,6 +628,7 @@ __device__ __forceinline__ void intra_block(const p64gpu_encode_args &a, const I
         v[e] = l2[i];  // dequantised in pairs by iq_idct_intra_rec
       }
       pk[j] = __builtin_amdgcn_perm((uint32_t)l2[1], (uint32_t)l2[0], 0x05040100u);
+      if (nzm) nzm[k >> 2] |= nz2(pk[j]) << (2 * (4 * (k & 3) + j));
     }
     put_levels(lds, lane, k, make_uint4(pk[0], pk[1], pk[2], pk[3]));
     SCHED_FENCE();
@@ -646,9 +707,11 @@ __device__ __forceinline__ void mbg_store_rows(const p64gpu_encode_args &a, cons
 // looks at its MB's other blocks; levels leave as one contiguous 8-KB run per
 // wave.  (Ten whole MBs per wave, as the inter kernel needs for its CBP
 // ballots, leave lanes 60..63 idle: 6.25% more waves.)
-template <bool QMB, bool CLAMP, bool POW2 = false>
-__global__ __launch_bounds__(64 * MBG_WAVES) void k_intra_mbg(p64gpu_encode_args a, BlkDiv kd, unsigned nmbs) {
+template <bool QMB, bool CLAMP, bool POW2 = false, bool BITS = false>
+__global__ __launch_bounds__(64 * MBG_WAVES) void k_intra_mbg(p64gpu_encode_args a, BlkDiv kd, unsigned nmbs,
+                                                                 VlcLenTab vt) {
   __shared__ __align__(16) uint8_t lvl[MBG_WAVES * LVL_WAVE];
+  __shared__ uint32_t vlen[BITS ? MBG_WAVES * 108 : 1];
   const int lane = threadIdx.x & 63;
   uint8_t *lds = lvl + (threadIdx.x >> 6) * LVL_WAVE;
   const unsigned nblk = 6u * nmbs;
@@ -661,7 +724,16 @@ __global__ __launch_bounds__(64 * MBG_WAVES) void k_intra_mbg(p64gpu_encode_args
   const IntraFetch f = intra_fetch_at<QMB>(a, blk_pos_mb(gmb, b, a.width, a.height, kd));
   PRIO_LOW();
   IntraOut o;
-  intra_block<CLAMP, POW2>(a, f, lds, lane, o);
+  uint32_t nzm[2] = {0u, 0u};
+  intra_block<CLAMP, POW2>(a, f, lds, lane, o, BITS ? nzm : nullptr);
+  if (BITS) {  // every intra block is transmitted: DC + AC codes + EOB
+    uint32_t *vl = vlen + (threadIdx.x >> 6) * 108;
+    load_vlc_len(vt, vl, lane);
+    WAVE_FENCE();
+    const int bb = block_vlc_bits(reinterpret_cast<const uint8_t *>(vl),
+                                  reinterpret_cast<const int16_t *>(lds + lane * LVL_STRIDE), nzm[0], nzm[1], false);
+    store_vlc_bits(a, nmbs, g0 + (unsigned)lane < nblk, gmb, b, bb);
+  }
   // the MB's record and LastIntra (p64.c:909-910: MTYPE 0, CBP 0x3f, LastIntra
   // reset) from the lane of its block 0; every intra block has a nonzero level
   // (the DC, 1..254)
@@ -1073,10 +1145,11 @@ __device__ __forceinline__ void pred_rows(const PredSrc &P, bool filter, uint2 p
 // decision can return (0, 2, 5, 8: decide_mtype) carries coefficients, so
 // the level mask for MC-only types (4, 7) is left out.
 // POW2: a uniform q whose D = 16q is a power of two (qlevel_pk2)
-template <bool QMB, bool OVR, bool POW2 = false>
+template <bool QMB, bool OVR, bool POW2 = false, bool BITS = false>
 __global__ __launch_bounds__(64) OCC4 void k_inter_mbg(p64gpu_encode_args a, BlkDiv kd, unsigned nmbs,
-                                                             const p64_me_rec *me) {
+                                                             const p64_me_rec *me, VlcLenTab vt) {
   __shared__ __align__(16) uint8_t lds[LVL_WAVE];
+  __shared__ uint32_t vlen[BITS ? 108 : 1];
   const int lane = threadIdx.x;
   const unsigned gmb0 = xcd_remap(blockIdx.x, gridDim.x) * MBS_PER_WAVE;
   if (gmb0 >= nmbs) return;  // whole wave
@@ -1211,6 +1284,7 @@ __global__ __launch_bounds__(64) OCC4 void k_inter_mbg(p64gpu_encode_args a, Blk
   // carries no coefficients are 0); sum of l^2 for the CBP decision:
   // sum|l| > 1 <=> sum l^2 > 1 and sum|l| > 0 <=> sum l^2 > 0 for integers
   int ss = 0;
+  uint32_t nzm[2] = {0u, 0u};  // (BITS) the nonzero scan positions
 #pragma unroll
   for (int k = 0; k < 8; k++) {
     uint32_t pk[4];
@@ -1219,6 +1293,7 @@ __global__ __launch_bounds__(64) OCC4 void k_inter_mbg(p64gpu_encode_args a, Blk
       pk[j] = lpair(k_zz.inv[8 * k + 2 * j], k_zz.inv[8 * k + 2 * j + 1]);
       if (OVR) pk[j] &= tcm;
       ss = __builtin_amdgcn_sdot2(__builtin_bit_cast(s16x2, pk[j]), __builtin_bit_cast(s16x2, pk[j]), ss, false);
+      if (BITS) nzm[k >> 2] |= nz2(pk[j]) << (2 * (4 * (k & 3) + j));
     }
     put_levels(lds, lane, k, make_uint4(pk[0], pk[1], pk[2], pk[3]));
     SCHED_FENCE();
@@ -1241,6 +1316,15 @@ __global__ __launch_bounds__(64) OCC4 void k_inter_mbg(p64gpu_encode_args a, Blk
     }
   }
   const bool ck = mt_tcoeff(mt) && ((cbp >> (5 - b)) & 1);
+  if (BITS) {  // the transmitted block's coded bits, from its staged levels (before the slots reuse them)
+    load_vlc_len(vt, vlen, lane);
+    WAVE_FENCE();
+    const int bb = ck ? block_vlc_bits(reinterpret_cast<const uint8_t *>(vlen),
+                                       reinterpret_cast<const int16_t *>(lds + lane * LVL_STRIDE), nzm[0], nzm[1],
+                                       mt_cbp(mt))
+                      : 0;
+    store_vlc_bits(a, nmbs, lane < 6 * MBS_PER_WAVE && gmb0 + (unsigned)(l / 6) < nmbs, gmb, b, bb);
+  }
   // the levels as natural column pairs (unmasked: only coded blocks, whose MB
   // type carries coefficients, use them)
   uint32_t np[8][4];
@@ -1282,45 +1366,70 @@ static unsigned mbg_workgroups(unsigned nmbs, unsigned per = MBG_WAVES) {
   return (waves + per - 1) / per;
 }
 
-hipError_t intra_mbg(const p64gpu_encode_args &a, hipStream_t st) {
+// the instance of k_intra_mbg for the call's options: <QMB, CLAMP, POW2, BITS>
+template <bool BITS>
+static void intra_launch(const p64gpu_encode_args &a, const VlcLenTab &vt, dim3 grid, dim3 block, BlkDiv kd,
+                         unsigned nm, hipStream_t st) {
+  const bool pow2 = !a.quant_mb && (a.quant & (a.quant - 1)) == 0 && make_qint_tab().ac[a.quant].m == 1;
+  if (a.quant_mb)
+    hipLaunchKernelGGL((k_intra_mbg<true, true, false, BITS>), grid, block, 0, st, a, kd, nm, vt);
+  else if (a.quant >= 5 && pow2)  // no BoundDct clamp can act (intra_block), packed quantiser
+    hipLaunchKernelGGL((k_intra_mbg<false, false, true, BITS>), grid, block, 0, st, a, kd, nm, vt);
+  else if (a.quant >= 5)
+    hipLaunchKernelGGL((k_intra_mbg<false, false, false, BITS>), grid, block, 0, st, a, kd, nm, vt);
+  else if (pow2)
+    hipLaunchKernelGGL((k_intra_mbg<false, true, true, BITS>), grid, block, 0, st, a, kd, nm, vt);
+  else
+    hipLaunchKernelGGL((k_intra_mbg<false, true, false, BITS>), grid, block, 0, st, a, kd, nm, vt);
+}
+
+hipError_t intra_mbg(const p64gpu_encode_args &a, const uint32_t *vlc_len, hipStream_t st) {
   const unsigned nm = (unsigned)((int64_t)a.nframes * (a.width / 16) * (a.height / 16));
   const unsigned waves = (6u * nm + 63u) / 64u;  // 64 blocks a wave
   const dim3 grid((waves + MBG_WAVES - 1) / MBG_WAVES), block(64 * MBG_WAVES);
   const BlkDiv kd = blk_div(a.width, a.height);
-  const bool pow2 = !a.quant_mb && (a.quant & (a.quant - 1)) == 0 && make_qint_tab().ac[a.quant].m == 1;
-  if (a.quant_mb)
-    hipLaunchKernelGGL((k_intra_mbg<true, true>), grid, block, 0, st, a, kd, nm);
-  else if (a.quant >= 5 && pow2)  // no BoundDct clamp can act (intra_block), packed quantiser
-    hipLaunchKernelGGL((k_intra_mbg<false, false, true>), grid, block, 0, st, a, kd, nm);
-  else if (a.quant >= 5)
-    hipLaunchKernelGGL((k_intra_mbg<false, false>), grid, block, 0, st, a, kd, nm);
-  else if (pow2)
-    hipLaunchKernelGGL((k_intra_mbg<false, true, true>), grid, block, 0, st, a, kd, nm);
-  else
-    hipLaunchKernelGGL((k_intra_mbg<false, true>), grid, block, 0, st, a, kd, nm);
+  VlcLenTab vt{};
+  if (a.vlc_bits) {
+    for (int i = 0; i < 108; i++) vt.w[i] = vlc_len[i];
+    intra_launch<true>(a, vt, grid, block, kd, nm, st);
+  } else {
+    intra_launch<false>(a, vt, grid, block, kd, nm, st);
+  }
   return hipGetLastError();
 }
 
-hipError_t inter_mbg(const p64gpu_encode_args &a, const p64_me_rec *me, hipStream_t st) {
-  const unsigned nm = (unsigned)((int64_t)a.nframes * (a.width / 16) * (a.height / 16));
-  const dim3 grid(mbg_workgroups(nm, 1)), block(64);
-  const BlkDiv kd = blk_div(a.width, a.height);
+template <bool BITS>
+static void inter_launch(const p64gpu_encode_args &a, const p64_me_rec *me, const VlcLenTab &vt, dim3 grid,
+                         dim3 block, BlkDiv kd, unsigned nm, hipStream_t st) {
   const bool ovr = a.mtype_override != nullptr;
   // a uniform q with D = 16q a power of two: the packed quantiser (multiplier 1)
   const bool pow2 = !a.quant_mb && (a.quant & (a.quant - 1)) == 0 && make_qint_tab().ac[a.quant].m == 1 &&
                     make_qint_tab().dc[a.quant].m == 1;
   if (a.quant_mb && ovr)
-    hipLaunchKernelGGL((k_inter_mbg<true, true>), grid, block, 0, st, a, kd, nm, me);
+    hipLaunchKernelGGL((k_inter_mbg<true, true, false, BITS>), grid, block, 0, st, a, kd, nm, me, vt);
   else if (a.quant_mb)
-    hipLaunchKernelGGL((k_inter_mbg<true, false>), grid, block, 0, st, a, kd, nm, me);
+    hipLaunchKernelGGL((k_inter_mbg<true, false, false, BITS>), grid, block, 0, st, a, kd, nm, me, vt);
   else if (ovr && pow2)
-    hipLaunchKernelGGL((k_inter_mbg<false, true, true>), grid, block, 0, st, a, kd, nm, me);
+    hipLaunchKernelGGL((k_inter_mbg<false, true, true, BITS>), grid, block, 0, st, a, kd, nm, me, vt);
   else if (ovr)
-    hipLaunchKernelGGL((k_inter_mbg<false, true>), grid, block, 0, st, a, kd, nm, me);
+    hipLaunchKernelGGL((k_inter_mbg<false, true, false, BITS>), grid, block, 0, st, a, kd, nm, me, vt);
   else if (pow2)
-    hipLaunchKernelGGL((k_inter_mbg<false, false, true>), grid, block, 0, st, a, kd, nm, me);
+    hipLaunchKernelGGL((k_inter_mbg<false, false, true, BITS>), grid, block, 0, st, a, kd, nm, me, vt);
   else
-    hipLaunchKernelGGL((k_inter_mbg<false, false>), grid, block, 0, st, a, kd, nm, me);
+    hipLaunchKernelGGL((k_inter_mbg<false, false, false, BITS>), grid, block, 0, st, a, kd, nm, me, vt);
+}
+
+hipError_t inter_mbg(const p64gpu_encode_args &a, const p64_me_rec *me, const uint32_t *vlc_len, hipStream_t st) {
+  const unsigned nm = (unsigned)((int64_t)a.nframes * (a.width / 16) * (a.height / 16));
+  const dim3 grid(mbg_workgroups(nm, 1)), block(64);
+  const BlkDiv kd = blk_div(a.width, a.height);
+  VlcLenTab vt{};
+  if (a.vlc_bits) {
+    for (int i = 0; i < 108; i++) vt.w[i] = vlc_len[i];
+    inter_launch<true>(a, me, vt, grid, block, kd, nm, st);
+  } else {
+    inter_launch<false>(a, me, vt, grid, block, kd, nm, st);
+  }
   return hipGetLastError();
 }
 

@@ -22,8 +22,10 @@ hipError_t motion(int mode, int w, int h, int nframes, int64_t stride, const uin
 
 // k_block.hip -- one lane per 8x8 block, 10 macroblocks per wave.  Every
 // buffer of one launch lies within 2 GiB (32-bit buffer offsets).
-hipError_t intra_mbg(const p64gpu_encode_args &a, hipStream_t st);
-hipError_t inter_mbg(const p64gpu_encode_args &a, const p64_me_rec *me, hipStream_t st);
+// vlc_len: 108 dwords, the TCOEFF code lengths of p64gpu_vlc_len_table (read
+// only when a.vlc_bits is given)
+hipError_t intra_mbg(const p64gpu_encode_args &a, const uint32_t *vlc_len, hipStream_t st);
+hipError_t inter_mbg(const p64gpu_encode_args &a, const p64_me_rec *me, const uint32_t *vlc_len, hipStream_t st);
 hipError_t recon_mbg(int w, int h, int nframes, int64_t stride, const uint8_t *ref, uint8_t *recon,
                      const int16_t *coef, const p64_mb_rec *mb, const uint8_t *quant_mb,
                      const uint8_t *coded_mask, hipStream_t st);

@@ -19,6 +19,10 @@
 #include "../../include/p64gpu.h"
 #include "launch.h"
 
+extern "C" int p64gpu_vlc_len_table_(uint32_t *out);
+extern "C" int p64gpu_vlc_block_bits_(int width, int height, int nframes, const p64_mb_rec *mb,
+                                      const int16_t *coef, uint16_t *blk_bits, void *stream);
+
 namespace {
 
 // ---------------------------------------------------------------------------
@@ -172,6 +176,7 @@ p64gpu_encode_args sub_batch(const p64gpu_encode_args &a, int f0, int n) {
   c.mb = a.mb + m0;
   c.me = a.me ? a.me + m0 : nullptr;
   c.nzmask = a.nzmask ? a.nzmask + m0 : nullptr;
+  c.vlc_bits = a.vlc_bits ? a.vlc_bits + m0 * 8 : nullptr;
   return c;
 }
 
@@ -193,6 +198,13 @@ int encode_launch(const p64gpu_encode_args *a, const int32_t *mb_list, int count
   if (a->search_limit < 1 || a->search_limit > 31)
     return fail(P64GPU_E_INVALID, "search_limit %d not in 1..31", a->search_limit);
   if (a->flags & ~P64GPU_FLAG_ME_GIVEN) return fail(P64GPU_E_INVALID, "flags 0x%x: unknown bits", a->flags);
+  if (a->vlc_bits && (mb_list || !aligned(a->vlc_bits, 16)))
+    return fail(P64GPU_E_INVALID, "vlc_bits: 16-byte aligned, and not with an MB list");
+  uint32_t vlc_len[108];
+  if (a->vlc_bits) {
+    const int s2 = p64gpu_vlc_len_table_(vlc_len);
+    if (s2) return s2;
+  }
   const bool me_given = (a->flags & P64GPU_FLAG_ME_GIVEN) != 0;
   if (me_given && (a->intra || !a->me || mb_list))
     return fail(P64GPU_E_INVALID, "P64GPU_FLAG_ME_GIVEN needs an inter picture batch with args->me");
@@ -212,9 +224,9 @@ int encode_launch(const p64gpu_encode_args *a, const int32_t *mb_list, int count
       for (int f0 = 0; f0 < a->nframes; f0 += chunk) {
         const p64gpu_encode_args c = sub_batch(*a, f0, a->nframes - f0 < chunk ? a->nframes - f0 : chunk);
         if (a->intra)
-          HIP_TRY(p64k::intra_mbg(c, st));
+          HIP_TRY(p64k::intra_mbg(c, vlc_len, st));
         else
-          HIP_TRY(p64k::inter_mbg(c, me + (size_t)f0 * nmb, st));
+          HIP_TRY(p64k::inter_mbg(c, me + (size_t)f0 * nmb, vlc_len, st));
       }
       return P64GPU_OK;
     }
@@ -222,6 +234,8 @@ int encode_launch(const p64gpu_encode_args *a, const int32_t *mb_list, int count
   const unsigned grid =
       mb_list ? (unsigned)count : (unsigned)((int64_t)a->nframes * (a->width / 16) * (a->height / 16));
   HIP_TRY(p64k::encode_fused(mode, grid, *a, mb_list, st));
+  if (a->vlc_bits)  // the fused kernel does not count: the entropy coder's count pass does
+    return p64gpu_vlc_block_bits_(a->width, a->height, a->nframes, a->mb, a->coef, a->vlc_bits, stream);
   return P64GPU_OK;
 }
 

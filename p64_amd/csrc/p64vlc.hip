@@ -318,7 +318,7 @@ __global__ __launch_bounds__(64 * VLC_WAVES) void k_vlc_blk(VlcArgs a, VlcTables
     int tot = bb;
 #pragma unroll
     for (int d = 1; d < 6; d++) tot += __shfl(bb, min(lane + d, 63));
-    if (act && b == 0) a.mb_bits[base + j] = hd.bad ? 0x80000000u : (uint32_t)(hd.bits + tot);
+    if (act && b == 0 && a.mb_bits) a.mb_bits[base + j] = hd.bad ? 0x80000000u : (uint32_t)(hd.bits + tot);
   } else {
     if (!act) return;
     // (8-byte loads: blk_bits is 8-byte aligned, 2 nframes nmb words into scratch)
@@ -361,6 +361,28 @@ __global__ __launch_bounds__(64 * VLC_WAVES) void k_vlc_blk(VlcArgs a, VlcTables
       bw.finish();
     }
   }
+}
+
+// With the blocks' bits given (the encoder counted them, p64gpu_encode_args.
+// vlc_bits): one lane per macroblock adds its header bits (WriteMBHeader
+// marker.c:288, the MVD predictor from the previous MB of its GOB row) to
+// them, keeps the header bits in slot 0 for the emit pass and writes the
+// MB's total into mb_bits[stream position] -- the count pass without the
+// level reads.
+__global__ __launch_bounds__(256) void k_vlc_hdr(VlcArgs a, VlcTables T) {
+  const int fi = blockIdx.y, k = blockIdx.x * 256 + threadIdx.x;
+  if (k >= a.nmb) return;
+  const size_t base = (size_t)fi * a.nmb;
+  const p64_mb_rec r = a.mb[base + k];
+  const int j = stream_pos(a.format, k), g = j / 33, m = j - g * 33;
+  const p64_mb_rec rp = a.mb[base + (m % 11 ? k - 1 : k)];
+  const int mq = a.mquant ? (int)a.mquant[base + k] : 0;
+  const Header hd = header_codes(T, r, rp, mq, m);
+  uint16_t *bk = a.blk_bits + (base + k) * 8;
+  const uint4 q = *reinterpret_cast<const uint4 *>(bk);  // slots 0..7 (16-byte aligned)
+  const uint32_t s2 = (q.x >> 16) + (q.y & 0xffffu) + (q.y >> 16) + (q.z & 0xffffu) + (q.z >> 16) + (q.w & 0xffffu);
+  bk[0] = (uint16_t)hd.bits;
+  a.mb_bits[base + j] = hd.bad ? 0x80000000u : (uint32_t)hd.bits + s2;
 }
 
 // stream-order offsets per picture (one wave per picture: each lane sums a
@@ -418,8 +440,10 @@ int p64gpu_vlc_pictures(const p64gpu_vlc_args *x, void *stream) {
   if (x->out_stride < p64gpu_vlc_max_bytes(x->width, x->height) || (x->out_stride & 3) ||
       ((uintptr_t)x->out & 3))
     return p64gpu_fail_(P64GPU_E_INVALID, "vlc: out_stride below p64gpu_vlc_max_bytes or not 4-aligned");
-  if (((uintptr_t)x->scratch & 7) || ((uintptr_t)x->coef & 15) || ((uintptr_t)x->mb & 3))
-    return p64gpu_fail_(P64GPU_E_INVALID, "vlc: scratch must be 8-byte, coef 16-byte, mb 4-byte aligned");
+  if (((uintptr_t)x->scratch & 7) || ((uintptr_t)x->coef & 15) || ((uintptr_t)x->mb & 3) ||
+      ((uintptr_t)x->blk_bits & 15))
+    return p64gpu_fail_(P64GPU_E_INVALID,
+                        "vlc: scratch must be 8-byte, coef and blk_bits 16-byte, mb 4-byte aligned");
   if (!g_tab_ok) {
     const int s = p64s_vlc_tables_(g_tab.t);
     if (s) return s;
@@ -457,15 +481,74 @@ int p64gpu_vlc_pictures(const p64gpu_vlc_args *x, void *stream) {
     uint32_t *scr = x->scratch + 6 * m0;
     a.mb_bits = scr;
     a.mb_off = scr + (size_t)nc * nmb;
-    a.blk_bits = reinterpret_cast<uint16_t *>(scr + 2 * (size_t)nc * nmb);
     const dim3 grid((unsigned)((nmb + VLC_WAVES * VLC_MBS - 1) / (VLC_WAVES * VLC_MBS)), (unsigned)nc);
-    hipLaunchKernelGGL(k_vlc_blk<false>, grid, dim3(64 * VLC_WAVES), 0, st, a, g_tab);
+    if (x->blk_bits) {  // the blocks' bits from the encoder: headers and totals only
+      a.blk_bits = x->blk_bits + m0 * 8;
+      hipLaunchKernelGGL(k_vlc_hdr, dim3((unsigned)((nmb + 255) / 256), (unsigned)nc), dim3(256), 0, st, a, g_tab);
+    } else {
+      a.blk_bits = reinterpret_cast<uint16_t *>(scr + 2 * (size_t)nc * nmb);
+      hipLaunchKernelGGL(k_vlc_blk<false>, grid, dim3(64 * VLC_WAVES), 0, st, a, g_tab);
+    }
     hipLaunchKernelGGL(k_vlc_scan, dim3((unsigned)nc), dim3(64), 0, st, a);
     hipLaunchKernelGGL(k_vlc_blk<true>, grid, dim3(64 * VLC_WAVES), 0, st, a, g_tab);
   }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return p64gpu_fail_(P64GPU_E_HIP, hipGetErrorString(e));
   return P64GPU_OK;
+}
+
+// (library-internal) the TCOEFF length table of the block-layout encoders'
+// bit counts (k_block.hip VlcLenTab): byte run * 16 + |level| = code length + 1
+// (sign), 20 (escape) where there is no code; 108 dwords.  The kernels take
+// FIRST01 as 2 bits, EOB 2, ESCAPE 20 -- checked here against the tables.
+int p64gpu_vlc_len_table_(uint32_t *out) {
+  if (!g_tab_ok) {
+    const int s = p64s_vlc_tables_(g_tab.t);
+    if (s) return s;
+    g_tab_ok = true;
+  }
+  const int lf = (int)(g_tab.t[T_FIRST01] >> 16), le = (int)(g_tab.t[T_EOB] >> 16), lx = (int)(g_tab.t[T_ESC] >> 16);
+  if (lf != 1 || le != 2 || lx != 6) return p64gpu_fail_(P64GPU_E_INVALID, "vlc: unexpected table lengths");
+  uint8_t *b = reinterpret_cast<uint8_t *>(out);
+  for (int i = 0; i < 27 * 16; i++) {
+    const int len = (int)(g_tab.t[T_TC + i] >> 16);
+    b[i] = (uint8_t)(len ? len + 1 : 20);
+  }
+  return P64GPU_OK;
+}
+
+// (library-internal) the blocks' coded bits of an encoded batch into
+// blk_bits[1..6] per MB by the count pass -- for encodes that took the fused
+// kernel (P64GPU_FUSED, capture without ME records), which does not count
+int p64gpu_vlc_block_bits_(int width, int height, int nframes, const p64_mb_rec *mb, const int16_t *coef,
+                           uint16_t *blk_bits, void *stream) {
+  const int fmt = p64s_format_of(width, height);
+  if (fmt < 0) return fmt;
+  uint32_t tab[108];
+  int s = p64gpu_vlc_len_table_(tab);
+  if (s) return s;
+  int ngob = 0;
+  p64s_geometry(fmt, nullptr, nullptr, &ngob);
+  const int nmb = ngob * 33;
+  const int chunk = (int)std::max<int64_t>(1, std::min<int64_t>(nframes, p64gpu_chunk_bytes_() / ((int64_t)nmb * 768)));
+  for (int f0 = 0; f0 < nframes; f0 += chunk) {
+    const int nc = std::min(chunk, nframes - f0);
+    const size_t m0 = (size_t)f0 * nmb;
+    VlcArgs a{};
+    a.width = width;
+    a.height = height;
+    a.nframes = nc;
+    a.format = fmt;
+    a.ngob = ngob;
+    a.nmb = nmb;
+    a.mb = mb + m0;
+    a.coef = coef + m0 * 384;
+    a.blk_bits = blk_bits + m0 * 8;
+    const dim3 grid((unsigned)((nmb + VLC_WAVES * VLC_MBS - 1) / (VLC_WAVES * VLC_MBS)), (unsigned)nc);
+    hipLaunchKernelGGL(k_vlc_blk<false>, grid, dim3(64 * VLC_WAVES), 0, (hipStream_t)stream, a, g_tab);
+  }
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? P64GPU_OK : p64gpu_fail_(P64GPU_E_HIP, hipGetErrorString(e));
 }
 
 }  // extern "C"

@@ -374,7 +374,7 @@ class VlcArgs(ctypes.Structure):
                 ("flags", ctypes.c_int), ("mb", ctypes.c_void_p), ("coef", ctypes.c_void_p),
                 ("gquant", ctypes.c_void_p), ("mquant", ctypes.c_void_p), ("tr", ctypes.c_void_p),
                 ("phase", ctypes.c_void_p), ("out", ctypes.c_void_p), ("out_stride", ctypes.c_int64),
-                ("bits", ctypes.c_void_p), ("scratch", ctypes.c_void_p)]
+                ("bits", ctypes.c_void_p), ("scratch", ctypes.c_void_p), ("blk_bits", ctypes.c_void_p)]
 
 
 def vlc_buffers(n: int, width: int, height: int):
@@ -390,11 +390,13 @@ def vlc_buffers(n: int, width: int, height: int):
 
 
 def vlc_pictures(mb, coef, gquant, tr, *, width: int, height: int, phase=None, mquant=None,
-                 buffers=None, host_bits: bool = True):
+                 buffers=None, host_bits: bool = True, blk_bits=None):
     """H.261 bits of a batch of pictures on the GPU.  All inputs are CUDA(HIP)
     tensors: mb [n, nmb, 4] int8, coef [n, nmb, 6, 64] int16, gquant [n, ngob]
     uint8, tr [n] int32, phase [n] uint8 or None, mquant [n, nmb] uint8 or None.
     buffers: (out, bits, scratch) from vlc_buffers, reused across calls.
+    blk_bits: int16 [n, nmb, 8] from the encoder (FrameBatchOut.vlc_bits of the
+    same records and levels): the coder skips its count pass.
     Returns (out [n, stride] uint8 tensor, bits [n] list of ints) -- or, with
     host_bits=False, the device bits tensor (no synchronisation)."""
     import torch
@@ -405,6 +407,8 @@ def vlc_pictures(mb, coef, gquant, tr, *, width: int, height: int, phase=None, m
     n = int(tr.numel())
     _, _, ngob = geometry(format_of(width, height))
     nmb = ngob * 33
+    if blk_bits is not None and (blk_bits.numel() < n * nmb * 8 or blk_bits.dtype != torch.int16):
+        raise P64GpuError("vlc_pictures: blk_bits must be int16 [n, nmb, 8]")
     if mb.numel() != n * nmb * 4 or coef.numel() != n * nmb * 384 or gquant.numel() != n * ngob:
         raise P64GpuError("vlc_pictures: buffer sizes do not match the picture format")
     out, bits, scratch = buffers if buffers is not None else vlc_buffers(n, width, height)
@@ -416,7 +420,8 @@ def vlc_pictures(mb, coef, gquant, tr, *, width: int, height: int, phase=None, m
                 coef=coef.data_ptr(), gquant=gquant.data_ptr(),
                 mquant=mquant.data_ptr() if mquant is not None else None, tr=tr.data_ptr(),
                 phase=phase.data_ptr() if phase is not None else None, out=out.data_ptr(),
-                out_stride=stride, bits=bits.data_ptr(), scratch=scratch.data_ptr())
+                out_stride=stride, bits=bits.data_ptr(), scratch=scratch.data_ptr(),
+                blk_bits=blk_bits.data_ptr() if blk_bits is not None else None)
     _check(L.p64gpu_vlc_pictures(ctypes.byref(a), _stream(torch)))
     if not host_bits:
         return out, bits[:n]

@@ -60,7 +60,7 @@ int main(void) {
          sizeof(p64_me_rec), sizeof(p64_mb_rec));
   O(width); O(height); O(nframes); O(intra); O(quant); O(me_mode); O(search_limit);
   O(flags); O(frame_stride); O(cur); O(ref); O(recon); O(last_intra); O(quant_mb);
-  O(mtype_override); O(coef); O(mb); O(me); O(nzmask);
+  O(mtype_override); O(coef); O(mb); O(me); O(nzmask); O(vlc_bits);
   return 0;
 }''')
     exe = tmp_path / "layout"
@@ -129,7 +129,7 @@ def test_vlc_args_layout_matches_ctypes(p64, tmp_path):
 int main(void) {
   printf("sizeof_args %zu\n", sizeof(p64gpu_vlc_args));
   O(width); O(height); O(nframes); O(flags); O(mb); O(coef); O(gquant); O(mquant); O(tr);
-  O(phase); O(out); O(out_stride); O(bits); O(scratch);
+  O(phase); O(out); O(out_stride); O(bits); O(scratch); O(blk_bits);
   return 0;
 }''')
     exe = tmp_path / "vlayout"

@@ -206,3 +206,75 @@ def test_bench_refuses_world_mismatch():
     r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--dry", "--gpus", "2",
                         "--steps", "2"], capture_output=True, text=True, timeout=120, env=env)
     assert r.returncode != 0 and "refusing" in r.stderr + r.stdout
+
+
+def _coded_worker(rank, world, port, S, q):
+    """--feed root, coded: each rank entropy-codes its shard's pictures (on the
+    GPU in bench.py; here the host writer over the CPU oracle's records stands
+    in), bench.gather_coded carries the coded bytes + bit counts to rank 0."""
+    import sys
+    sys.path.insert(0, REPO)
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import torch
+
+    import bench
+    import oracle
+    import p64_amd
+    from p64_amd import stream
+
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
+                            world_size=world)
+    w, h = 176, 144
+    seed0, _ = bench.shard_seeds(rank, S)
+    streams = [coded_sequence(oracle, p64_amd, stream, seed0 + k, w, h) for k in range(S)]
+    stride = max(len(x) for x in streams) + 64 * (rank + 1)  # ranks' buffers differ in size
+    out = torch.zeros((S, stride), dtype=torch.uint8)
+    for k, x in enumerate(streams):
+        out[k, :len(x)] = torch.frombuffer(bytearray(x), dtype=torch.uint8)
+    bits = torch.tensor([8 * len(x) for x in streams], dtype=torch.int32)
+    got = bench.gather_coded(world, rank, out, bits)
+    if rank == 0:
+        pays, bl = got
+        q.put([bytes(p[i, :int(b[i]) // 8].numpy().tobytes()) for p, b in zip(pays, bl) for i in range(S)])
+    else:
+        assert got is None
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def coded_sequence(oracle, p64_amd, stream, seed, w, h, n=2):
+    """The .p64 of a short closed-loop sequence: the oracle's records through
+    the host writer (the GPU coder's bits are byte-identical to it,
+    tests/test_gpu_stream.py)."""
+    frames = [p64_amd.synth_frame(seed, t, w, h, content=p64_amd.SYNTH_SURVEY) for t in range(n)]
+    outs = oracle.encode_sequence(frames, w, h, quant=8, me_mode=1, search_limit=31)
+    wr = stream.Writer(stream.format_of(w, h))
+    for t, (coef, mb, _, _) in enumerate(outs):
+        wr.write_picture(t, mb, coef, 8)
+    return wr.end(n)
+
+
+def test_two_rank_root_feed_gathers_coded_streams():
+    """The fed path's coded gather (bench.py --feed root, default --gather
+    coded): the streams rank 0 receives from two ranks equal the .p64 bytes a
+    single process writes for the same sequences."""
+    import sys
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle
+    import p64_amd
+    from p64_amd import stream
+
+    world, S = 2, 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=_coded_worker, args=(r, world, port, S, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert len(got) == world * S
+    for i in range(world * S):
+        assert got[i] == coded_sequence(oracle, p64_amd, stream, 1 + i, 176, 144), i

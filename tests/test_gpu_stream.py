@@ -42,8 +42,9 @@ def cli_flags(z):
 
 
 def cli_stdin(z):
-    """-o reads the program from stdin (the reference's own test.* files are
-    kept as data under tests/golden/progs/)."""
+    """-o reads the program from stdin: the interpreter programs under
+    tests/golden/progs/ are the builder's own (written in the reference's
+    program language, lexer.l), not the reference's test.* files."""
     prog = str(z["oracle"])
     return open(os.path.join(GOLDEN, "progs", prog), "rb") if prog else subprocess.DEVNULL
 
@@ -238,3 +239,58 @@ def test_gpu_vlc_batch_matches_host_writer(p64, torch_dev, monkeypatch, chunk):
         assert bits[i] - int(phases[i]) == host_bits
         assert gpu >> host_bits == 0  # the leading phase bits are zero
         assert gpu >> (host_bits - 8 * len(full)) == int.from_bytes(full, "big")
+
+
+@pytest.mark.parametrize("case", ["inter_q8", "inter_q5", "inter_q31_qmb", "inter_override", "intra_q8",
+                                  "intra_q3_qmb", "fused_inter"])
+def test_gpu_vlc_block_bits_from_encoder(p64, torch_dev, monkeypatch, case):
+    """The encoder's coded-bit counts (p64gpu_encode_args.vlc_bits, counted
+    inside k_inter_mbg / k_intra_mbg from the staged levels; the fused kernel
+    path through the count pass) handed to the entropy coder as blk_bits give
+    the same bits as the coder's own count pass, picture for picture, and
+    those equal the host writer's."""
+    from p64_amd import stream
+    torch = torch_dev
+    if case == "fused_inter":
+        monkeypatch.setenv("P64GPU_FUSED", "1")
+    w, h, S = 176, 144, 6
+    nmb, pic, ngob = 99, w * h * 3 // 2, 3
+    rng = np.random.default_rng(abs(hash(case)) % 1000)
+    fr = p64.synth_frames_device(w, h, 7, S, 0, 2, content=p64.SYNTH_SURVEY if "q8" in case else p64.SYNTH_VNOISE)
+    li = torch.zeros(S * nmb, dtype=torch.uint8, device="cuda")
+    r0 = torch.zeros(S * pic, dtype=torch.uint8, device="cuda")
+    r1 = torch.zeros_like(r0)
+    q = int(case.split("_q")[1].split("_")[0]) if "_q" in case else 8
+    qmb = (torch.from_numpy(rng.integers(1, 32, S * nmb).astype(np.uint8)).cuda() if "qmb" in case else None)
+    ov = (torch.from_numpy(rng.integers(-1, 10, S * nmb).astype(np.int8)).cuda() if "override" in case else None)
+    intra = case.startswith("intra")
+    p64.encode_frames(fr[0].reshape(-1), None, r0, li, width=w, height=h, intra=True, quant=q)
+    out = p64.FrameBatchOut(coef=torch.zeros((S, nmb, 6, 64), dtype=torch.int16, device="cuda"),
+                            mb=torch.empty((S, nmb, 4), dtype=torch.int8, device="cuda"),
+                            me=torch.empty((S, nmb, 7), dtype=torch.int32, device="cuda"),
+                            vlc_bits=torch.full((S, nmb, 8), -1, dtype=torch.int16, device="cuda"))
+    cur = fr[0] if intra else fr[1]
+    p64.encode_frames(cur.reshape(-1), None if intra else r0, r1, li, width=w, height=h, intra=intra,
+                      quant=q, me_mode=p64.ME_FULL, search_limit=31, quant_mb=qmb,
+                      mtype_override=None if intra else ov, out=out)
+    gq = torch.full((S, ngob), q, dtype=torch.uint8, device="cuda")
+    mq = qmb.view(S, nmb) if qmb is not None else None
+    if ov is not None:  # MQUANT types among the overrides: their MQUANT is the uniform q
+        mq = torch.full((S, nmb), q, dtype=torch.uint8, device="cuda")
+    tr = torch.arange(S, dtype=torch.int32, device="cuda")
+    phase = torch.from_numpy(rng.integers(0, 8, S).astype(np.uint8)).cuda()
+    o1, b1 = stream.vlc_pictures(out.mb, out.coef, gq, tr, width=w, height=h, phase=phase, mquant=mq)
+    o1 = o1.cpu().numpy()
+    o2, b2 = stream.vlc_pictures(out.mb, out.coef, gq, tr, width=w, height=h, phase=phase, mquant=mq,
+                                 blk_bits=out.vlc_bits)
+    assert b1 == b2
+    o2 = o2.cpu().numpy()
+    for i in range(S):
+        nb = (b1[i] + 7) // 8
+        np.testing.assert_array_equal(o1[i, :nb], o2[i, :nb], err_msg=f"{case} picture {i}")
+    # the host writer's bits (the reference's, tests/test_stream.py) for the same records
+    mb_h, coef_h = out.mb.cpu().numpy(), out.coef.cpu().numpy()
+    for i in range(S):
+        wr = stream.Writer(stream.QCIF)
+        wr.write_picture(int(tr[i]), mb_h[i], coef_h[i], q, quant_mb=mq[i].cpu().numpy() if mq is not None else None)
+        assert b1[i] - int(phase[i]) == wr.bits()
