@@ -495,13 +495,13 @@ def intra_kernel_name(q):
     """k_intra_mbg's instance for a uniform q (p64k::intra_mbg): <QMB, CLAMP,
     POW2> as rocprof prints it"""
     clamp = "false" if q >= 5 else "true"
-    return f"k_intra_mbg<false, {clamp}, true>" if _pow2_quant(q) else f"k_intra_mbg<false, {clamp}, false>"
+    return f"k_intra_mbg<false, {clamp}, {'true' if _pow2_quant(q) else 'false'}, false>"
 
 
 def inter_kernel_name(q):
-    """k_inter_mbg's instance for a uniform q without overrides
-    (p64k::inter_mbg): <QMB, OVR, POW2>"""
-    return "k_inter_mbg<false, false, %s>" % ("true" if _pow2_quant(q) else "false")
+    """k_inter_mbg's instance for a uniform q without overrides and without
+    the entropy coder's bit counts (p64k::inter_mbg): <QMB, OVR, POW2, BITS>"""
+    return "k_inter_mbg<false, false, %s, false>" % ("true" if _pow2_quant(q) else "false")
 
 
 def content_key(args, base):

@@ -18,6 +18,7 @@
 #include "common.h"
 #include "launch.h"
 #include "quant_int.h"
+#include "vlc_count.h"
 
 namespace {
 
@@ -472,52 +473,14 @@ __device__ __forceinline__ void put_levels(uint8_t *lds, int lane, int k, uint4 
 
 // ---------------------------------------------------------------------------
 // Coded-bit counts for the entropy coder (p64gpu_encode_args.vlc_bits): a
-// transmitted block's bits -- EncodeAC / CBPEncodeAC codec.c:96-205 incl.
-// EOB, and an intra block's 8-bit DC (EncodeDC codec.c:343) -- counted from
-// the zigzag levels the kernel has just staged in LDS, so the entropy coder
-// needs no count pass over the levels (p64vlc.hip).
-// The TCOEFF code lengths + 1 (sign) by run * 16 + |level| (runs < 27, levels
-// < 16), 20 (ESCAPE 6 + run 6 + level 8) where the table has no code; built on
-// the host from the entropy coder's own tables (p64gpu_abi.hip).
-struct VlcLenTab {
-  uint32_t w[108];  // 432 bytes
-};
-// the positions holding a nonzero level of 16 zigzag level pairs as mask bits
-// 2i, 2i + 1: v_pk_min_u16 against 1, v_dot2 (lo + 2 hi), v_lshl_or
-typedef unsigned short u16x2v __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ uint32_t nz2(uint32_t pair) {
-  const u16x2v r = __builtin_elementwise_min(__builtin_bit_cast(u16x2v, pair), (u16x2v){1, 1});
-  return __builtin_amdgcn_udot2(r, (u16x2v){1, 2}, 0u, false);
-}
-// bits of one coded block from its staged levels (lvs, scan order) and its
-// nonzero positions (m0: 0..31, m1: 32..63); cbpt: a type with CBP (the
-// first coefficient may take the short FIRST01 code; no DC of its own),
-// else an intra block (DC as 8 bits, AC from position 1)
-__device__ __forceinline__ int block_vlc_bits(const uint8_t *len, const int16_t *lvs, uint32_t m0, uint32_t m1,
-                                              bool cbpt) {
-  int bits = cbpt ? 2 : 10;  // EOB (+ the intra DC)
-  if (!cbpt) m0 &= ~1u;
-  int last = cbpt ? -1 : 0;
-  bool first = cbpt;
-  while (m0 | m1) {
-    const int p = m0 ? __builtin_ctz(m0) : 32 + __builtin_ctz(m1);
-    if (m0)
-      m0 &= m0 - 1u;
-    else
-      m1 &= m1 - 1u;
-    const int l = lvs[p];
-    const int run = p - last - 1, al = l < 0 ? -l : l;
-    last = p;
-    bits += (first && run == 0 && al == 1) ? 2 : (run < 27 && al < 16 ? (int)len[run * 16 + al] : 20);
-    first = false;
-  }
-  return bits;
-}
-// the table into this wave's LDS copy (108 dwords over the 64 lanes)
-__device__ __forceinline__ void load_vlc_len(const VlcLenTab &vt, uint32_t *dst, int lane) {
-  dst[lane] = vt.w[lane];
-  if (lane < 108 - 64) dst[lane + 64] = vt.w[lane + 64];
-}
+// transmitted block's bits counted from the zigzag levels the kernel has just
+// staged in LDS (vlc_count.h), so the entropy coder needs no count pass over
+// the levels (p64vlc.hip).
+using p64k::VlcLenTab;
+using p64k::nz2;
+using p64k::block_vlc_bits;
+using p64k::load_vlc_len;
+using p64k::VLC_LEN_WORDS;
 // one uint16 per block into vlc_bits[gmb][1 + b] (slot 0: the entropy coder's)
 __device__ __forceinline__ void store_vlc_bits(const p64gpu_encode_args &a, unsigned nmbs, bool valid, unsigned gmb,
                                                int b, int bits) {
@@ -711,7 +674,7 @@ template <bool QMB, bool CLAMP, bool POW2 = false, bool BITS = false>
 __global__ __launch_bounds__(64 * MBG_WAVES) void k_intra_mbg(p64gpu_encode_args a, BlkDiv kd, unsigned nmbs,
                                                                  VlcLenTab vt) {
   __shared__ __align__(16) uint8_t lvl[MBG_WAVES * LVL_WAVE];
-  __shared__ uint32_t vlen[BITS ? MBG_WAVES * 108 : 1];
+  __shared__ uint32_t vlen[BITS ? MBG_WAVES * VLC_LEN_WORDS : 1];
   const int lane = threadIdx.x & 63;
   uint8_t *lds = lvl + (threadIdx.x >> 6) * LVL_WAVE;
   const unsigned nblk = 6u * nmbs;
@@ -727,7 +690,7 @@ __global__ __launch_bounds__(64 * MBG_WAVES) void k_intra_mbg(p64gpu_encode_args
   uint32_t nzm[2] = {0u, 0u};
   intra_block<CLAMP, POW2>(a, f, lds, lane, o, BITS ? nzm : nullptr);
   if (BITS) {  // every intra block is transmitted: DC + AC codes + EOB
-    uint32_t *vl = vlen + (threadIdx.x >> 6) * 108;
+    uint32_t *vl = vlen + (threadIdx.x >> 6) * VLC_LEN_WORDS;
     load_vlc_len(vt, vl, lane);
     WAVE_FENCE();
     const int bb = block_vlc_bits(reinterpret_cast<const uint8_t *>(vl),
@@ -1149,7 +1112,7 @@ template <bool QMB, bool OVR, bool POW2 = false, bool BITS = false>
 __global__ __launch_bounds__(64) OCC4 void k_inter_mbg(p64gpu_encode_args a, BlkDiv kd, unsigned nmbs,
                                                              const p64_me_rec *me, VlcLenTab vt) {
   __shared__ __align__(16) uint8_t lds[LVL_WAVE];
-  __shared__ uint32_t vlen[BITS ? 108 : 1];
+  __shared__ uint32_t vlen[BITS ? VLC_LEN_WORDS : 1];
   const int lane = threadIdx.x;
   const unsigned gmb0 = xcd_remap(blockIdx.x, gridDim.x) * MBS_PER_WAVE;
   if (gmb0 >= nmbs) return;  // whole wave
@@ -1390,7 +1353,7 @@ hipError_t intra_mbg(const p64gpu_encode_args &a, const uint32_t *vlc_len, hipSt
   const BlkDiv kd = blk_div(a.width, a.height);
   VlcLenTab vt{};
   if (a.vlc_bits) {
-    for (int i = 0; i < 108; i++) vt.w[i] = vlc_len[i];
+    for (int i = 0; i < VLC_LEN_WORDS; i++) vt.w[i] = vlc_len[i];
     intra_launch<true>(a, vt, grid, block, kd, nm, st);
   } else {
     intra_launch<false>(a, vt, grid, block, kd, nm, st);
@@ -1425,7 +1388,7 @@ hipError_t inter_mbg(const p64gpu_encode_args &a, const p64_me_rec *me, const ui
   const BlkDiv kd = blk_div(a.width, a.height);
   VlcLenTab vt{};
   if (a.vlc_bits) {
-    for (int i = 0; i < 108; i++) vt.w[i] = vlc_len[i];
+    for (int i = 0; i < VLC_LEN_WORDS; i++) vt.w[i] = vlc_len[i];
     inter_launch<true>(a, me, vt, grid, block, kd, nm, st);
   } else {
     inter_launch<false>(a, me, vt, grid, block, kd, nm, st);

@@ -22,8 +22,8 @@ hipError_t motion(int mode, int w, int h, int nframes, int64_t stride, const uin
 
 // k_block.hip -- one lane per 8x8 block, 10 macroblocks per wave.  Every
 // buffer of one launch lies within 2 GiB (32-bit buffer offsets).
-// vlc_len: 108 dwords, the TCOEFF code lengths of p64gpu_vlc_len_table (read
-// only when a.vlc_bits is given)
+// vlc_len: VLC_LEN_WORDS dwords, the code-length table of
+// p64gpu_vlc_len_table_ (vlc_count.h; read only when a.vlc_bits is given)
 hipError_t intra_mbg(const p64gpu_encode_args &a, const uint32_t *vlc_len, hipStream_t st);
 hipError_t inter_mbg(const p64gpu_encode_args &a, const p64_me_rec *me, const uint32_t *vlc_len, hipStream_t st);
 hipError_t recon_mbg(int w, int h, int nframes, int64_t stride, const uint8_t *ref, uint8_t *recon,

@@ -18,6 +18,7 @@
 
 #include "../../include/p64gpu.h"
 #include "launch.h"
+#include "vlc_count.h"
 
 extern "C" int p64gpu_vlc_len_table_(uint32_t *out);
 extern "C" int p64gpu_vlc_block_bits_(int width, int height, int nframes, const p64_mb_rec *mb,
@@ -200,7 +201,7 @@ int encode_launch(const p64gpu_encode_args *a, const int32_t *mb_list, int count
   if (a->flags & ~P64GPU_FLAG_ME_GIVEN) return fail(P64GPU_E_INVALID, "flags 0x%x: unknown bits", a->flags);
   if (a->vlc_bits && (mb_list || !aligned(a->vlc_bits, 16)))
     return fail(P64GPU_E_INVALID, "vlc_bits: 16-byte aligned, and not with an MB list");
-  uint32_t vlc_len[108];
+  uint32_t vlc_len[p64k::VLC_LEN_WORDS];
   if (a->vlc_bits) {
     const int s2 = p64gpu_vlc_len_table_(vlc_len);
     if (s2) return s2;

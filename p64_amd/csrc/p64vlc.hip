@@ -24,10 +24,12 @@
 
 #include "../../include/p64gpu.h"
 #include "../../include/p64stream.h"
+#include "vlc_count.h"
 
 extern "C" int p64s_vlc_tables_(uint32_t *t);
 extern "C" int p64gpu_fail_(int status, const char *msg);
 extern "C" int64_t p64gpu_chunk_bytes_(void);
+extern "C" int p64gpu_vlc_len_table_(uint32_t *out);
 
 namespace {
 
@@ -197,53 +199,59 @@ __device__ __forceinline__ void nz_masks(const uint32_t lv[32], uint32_t &m0, ui
 }
 
 // the codes of one block's levels (EncodeAC codec.c:96 / CBPEncodeAC
-// codec.c:141), scan positions from 1 for intra blocks (the DC is coded
-// alone: the caller leaves bit 0 out of m0); EMIT: into the writer, else only
-// counted.  Returns the bits, EOB included (0 for a CBP-type block without a
-// level: nothing is written, codec.c:151).  Visits the nonzero positions only
-// (m0/m1, lowest first), each level read from the lane's scan-order copy in
-// LDS (lvs): as many steps as the block has levels, not 64.
-template <bool EMIT>
-__device__ __forceinline__ int block_codes(const VlcTables &T, const uint16_t *lvs, uint32_t m0, uint32_t m1,
-                                           bool cbpt, BitWriter &bw) {
-  const bool any = (m0 | m1) != 0;
-  int bits = 0, last = cbpt ? -1 : 0;
+// codec.c:141) into the writer, scan positions from 1 for intra blocks (the
+// DC is coded alone: the caller leaves bit 0 out of m0), EOB included; a
+// CBP-type block without a level writes nothing (codec.c:151; never a
+// transmitted block).  Visits the nonzero positions only (m0/m1, lowest
+// first), two per step: both levels and both table entries are read
+// together, the codes chosen by selects (FIRST01, the TCOEFF table, ESCAPE).
+__device__ __forceinline__ void code_of(const VlcTables &T, uint32_t e, bool first, int run, int l, uint32_t &v,
+                                        int &n) {
+  const int al = l < 0 ? -l : l;
+  const uint32_t sg = (uint32_t)(l < 0);
+  const Code f = tab(T, T_FIRST01), esc = tab(T, T_ESC);
+  const int elen = (run < 27 && al < 16) ? (int)(e >> 16) : 0;
+  v = (esc.v << 14) | ((uint32_t)run << 8) | ((uint32_t)l & 0xffu);
+  n = esc.len + 14;
+  if (elen) {
+    v = ((e & 0xffffu) << 1) | sg;
+    n = elen + 1;
+  }
+  if (first && run == 0 && al == 1) {
+    v = (f.v << 1) | sg;
+    n = f.len + 1;
+  }
+}
+__device__ __forceinline__ void block_codes(const VlcTables &T, const uint16_t *lvs, uint32_t m0, uint32_t m1,
+                                            bool cbpt, BitWriter &bw) {
+  uint64_t m = ((uint64_t)m1 << 32) | m0;
+  if (cbpt && !m) return;
+  int last = cbpt ? -1 : 0;
   bool first = cbpt;
-  while (m0 | m1) {
-    const int p = m0 ? __builtin_ctz(m0) : 32 + __builtin_ctz(m1);
-    if (m0)
-      m0 &= m0 - 1u;
-    else
-      m1 &= m1 - 1u;
-    const int l = (int)(int16_t)lvs[p];
-    const int run = p - last - 1;
-    last = p;
-    const int al = l < 0 ? -l : l;
+  while (m) {
+    const int p1 = (int)__builtin_ctzll(m);
+    m &= m - 1u;
+    const bool two = m != 0;
+    const int p2 = two ? (int)__builtin_ctzll(m | (1ull << 63)) : p1;
+    m &= m - 1u;
+    const int l1 = (int)(int16_t)lvs[p1], l2 = (int)(int16_t)lvs[p2];
+    const int r1 = p1 - last - 1, r2 = p2 - p1 - 1;
+    last = p2;
+    const int a1 = l1 < 0 ? -l1 : l1, a2 = l2 < 0 ? -l2 : l2;
+    const uint32_t e1 = T.t[T_TC + min(r1, 26) * 16 + min(a1, 15)];
+    const uint32_t e2 = T.t[T_TC + min(r2, 26) * 16 + min(a2, 15)];
     uint32_t v;
     int n;
-    if (first && run == 0 && al == 1) {
-      const Code f = tab(T, T_FIRST01);
-      v = (f.v << 1) | (uint32_t)(l < 0);
-      n = f.len + 1;
-    } else {
-      const Code e = (run < 27 && al < 16) ? tab(T, T_TC + run * 16 + al) : Code{0u, 0};
-      if (e.len) {
-        v = (e.v << 1) | (uint32_t)(l < 0);
-        n = e.len + 1;
-      } else {  // ESCAPE, 6-bit run, 8-bit level
-        const Code esc = tab(T, T_ESC);
-        v = (esc.v << 14) | ((uint32_t)run << 8) | ((uint32_t)l & 0xffu);
-        n = esc.len + 14;
-      }
+    code_of(T, e1, first, r1, l1, v, n);
+    bw.put(v, n);
+    if (two) {
+      code_of(T, e2, false, r2, l2, v, n);
+      bw.put(v, n);
     }
-    if (EMIT) bw.put(v, n);
-    bits += n;
     first = false;
   }
-  if (cbpt && !any) return 0;
   const Code eob = tab(T, T_EOB);
-  if (EMIT) bw.put(eob.v, eob.len);
-  return bits + eob.len;
+  bw.put(eob.v, eob.len);
 }
 
 // Lane-per-block entropy coding: a wave takes 10 raster macroblocks, lane
@@ -258,8 +266,10 @@ __device__ __forceinline__ int block_codes(const VlcTables &T, const uint16_t *l
 //     offset (k_vlc_scan) + its header + the blocks before it
 constexpr int VLC_STAGE = 144;  // bytes per lane of the level copy: 128 + 16 pad (ds_write_b128 without conflicts)
 template <bool EMIT>
-__global__ __launch_bounds__(64 * VLC_WAVES) void k_vlc_blk(VlcArgs a, VlcTables Tg) {
+__global__ __launch_bounds__(64 * VLC_WAVES) void k_vlc_blk(VlcArgs a, VlcTables Tg, p64k::VlcLenTab Lg) {
   __shared__ VlcTables T;  // per-lane table lookups from LDS, loaded once per workgroup
+  __shared__ uint32_t vlen[EMIT ? 1 : p64k::VLC_LEN_WORDS];  // the count's code lengths (vlc_count.h)
+  if (!EMIT && threadIdx.x < 64) p64k::load_vlc_len(Lg, vlen, threadIdx.x);
   __shared__ __align__(16) uint8_t stage[VLC_WAVES * 64 * VLC_STAGE];  // each lane's levels, scan order
   for (int i = threadIdx.x; i < T_N; i += 64 * VLC_WAVES) T.t[i] = Tg.t[i];
   __syncthreads();
@@ -299,7 +309,7 @@ __global__ __launch_bounds__(64 * VLC_WAVES) void k_vlc_blk(VlcArgs a, VlcTables
   // and its levels in LDS for the indexed reads of block_codes
   uint32_t m0, m1;
   nz_masks(lv, m0, m1);
-  if (!cbpt) m0 &= ~1u;
+  if (!cbpt && EMIT) m0 &= ~1u;  // (the count's block_vlc_bits clears it itself)
   if (!coded) m0 = m1 = 0;
   uint8_t *stl = stage + (wv * 64 + lane) * VLC_STAGE;
 #pragma unroll
@@ -310,7 +320,9 @@ __global__ __launch_bounds__(64 * VLC_WAVES) void k_vlc_blk(VlcArgs a, VlcTables
   uint32_t *out = a.out + (size_t)fi * a.out_words;
   if (!EMIT) {
     const Header hd = header_codes(T, r, rp, mq, m);
-    int bb = coded ? block_codes<false>(T, lvs, m0, m1, cbpt, bw) + (cbpt ? 0 : 8) : 0;  // (intra: + DC)
+    const int bb = coded ? p64k::block_vlc_bits(reinterpret_cast<const uint8_t *>(vlen),
+                                                reinterpret_cast<const int16_t *>(lvs), m0, m1, cbpt)
+                         : 0;  // (intra: + DC)
     // the MB's six lanes: header and block bits into blk_bits, the total
     uint16_t *bk = a.blk_bits + (base + k) * 8;
     if (act) bk[1 + b] = (uint16_t)bb;
@@ -357,7 +369,7 @@ __global__ __launch_bounds__(64 * VLC_WAVES) void k_vlc_blk(VlcArgs a, VlcTables
         const int dc = dc0 < 1 ? 1 : (dc0 > 254 ? 254 : dc0);
         bw.put((uint32_t)(dc == 128 ? 255 : dc), 8);
       }
-      block_codes<true>(T, lvs, m0, m1, cbpt, bw);
+      block_codes(T, lvs, m0, m1, cbpt, bw);
       bw.finish();
     }
   }
@@ -417,6 +429,8 @@ __global__ __launch_bounds__(64) void k_vlc_scan(VlcArgs a) {
 
 thread_local VlcTables g_tab;
 thread_local bool g_tab_ok = false;
+thread_local p64k::VlcLenTab g_len;  // the count's code lengths (p64gpu_vlc_len_table_)
+thread_local bool g_len_ok = false;
 
 }  // namespace
 
@@ -444,10 +458,10 @@ int p64gpu_vlc_pictures(const p64gpu_vlc_args *x, void *stream) {
       ((uintptr_t)x->blk_bits & 15))
     return p64gpu_fail_(P64GPU_E_INVALID,
                         "vlc: scratch must be 8-byte, coef and blk_bits 16-byte, mb 4-byte aligned");
-  if (!g_tab_ok) {
-    const int s = p64s_vlc_tables_(g_tab.t);
+  if (!g_len_ok) {  // (fills g_tab too)
+    const int s = p64gpu_vlc_len_table_(g_len.w);
     if (s) return s;
-    g_tab_ok = true;
+    g_len_ok = true;
   }
   int ngob = 0;
   p64s_geometry(fmt, nullptr, nullptr, &ngob);
@@ -487,20 +501,21 @@ int p64gpu_vlc_pictures(const p64gpu_vlc_args *x, void *stream) {
       hipLaunchKernelGGL(k_vlc_hdr, dim3((unsigned)((nmb + 255) / 256), (unsigned)nc), dim3(256), 0, st, a, g_tab);
     } else {
       a.blk_bits = reinterpret_cast<uint16_t *>(scr + 2 * (size_t)nc * nmb);
-      hipLaunchKernelGGL(k_vlc_blk<false>, grid, dim3(64 * VLC_WAVES), 0, st, a, g_tab);
+      hipLaunchKernelGGL(k_vlc_blk<false>, grid, dim3(64 * VLC_WAVES), 0, st, a, g_tab, g_len);
     }
     hipLaunchKernelGGL(k_vlc_scan, dim3((unsigned)nc), dim3(64), 0, st, a);
-    hipLaunchKernelGGL(k_vlc_blk<true>, grid, dim3(64 * VLC_WAVES), 0, st, a, g_tab);
+    hipLaunchKernelGGL(k_vlc_blk<true>, grid, dim3(64 * VLC_WAVES), 0, st, a, g_tab, g_len);
   }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return p64gpu_fail_(P64GPU_E_HIP, hipGetErrorString(e));
   return P64GPU_OK;
 }
 
-// (library-internal) the TCOEFF length table of the block-layout encoders'
-// bit counts (k_block.hip VlcLenTab): byte run * 16 + |level| = code length + 1
-// (sign), 20 (escape) where there is no code; 108 dwords.  The kernels take
-// FIRST01 as 2 bits, EOB 2, ESCAPE 20 -- checked here against the tables.
+// (library-internal) the code-length table of the block bit counts
+// (vlc_count.h VlcLenTab): byte min(run, 27) * 17 + min(|level|, 16) = the
+// TCOEFF code length + 1 (sign), 20 (escape) where there is no code.  The
+// counting takes FIRST01 as 2 bits and EOB as 2 -- checked here against the
+// tables.
 int p64gpu_vlc_len_table_(uint32_t *out) {
   if (!g_tab_ok) {
     const int s = p64s_vlc_tables_(g_tab.t);
@@ -510,10 +525,12 @@ int p64gpu_vlc_len_table_(uint32_t *out) {
   const int lf = (int)(g_tab.t[T_FIRST01] >> 16), le = (int)(g_tab.t[T_EOB] >> 16), lx = (int)(g_tab.t[T_ESC] >> 16);
   if (lf != 1 || le != 2 || lx != 6) return p64gpu_fail_(P64GPU_E_INVALID, "vlc: unexpected table lengths");
   uint8_t *b = reinterpret_cast<uint8_t *>(out);
-  for (int i = 0; i < 27 * 16; i++) {
-    const int len = (int)(g_tab.t[T_TC + i] >> 16);
-    b[i] = (uint8_t)(len ? len + 1 : 20);
-  }
+  for (int i = 0; i < 4 * p64k::VLC_LEN_WORDS; i++) b[i] = 0;
+  for (int r = 0; r < p64k::VLC_LEN_RUNS; r++)
+    for (int l = 0; l < p64k::VLC_LEN_LEVELS; l++) {
+      const int len = (r < 27 && l < 16) ? (int)(g_tab.t[T_TC + r * 16 + l] >> 16) : 0;
+      b[r * p64k::VLC_LEN_LEVELS + l] = (uint8_t)(len ? len + 1 : 20);
+    }
   return P64GPU_OK;
 }
 
@@ -524,8 +541,8 @@ int p64gpu_vlc_block_bits_(int width, int height, int nframes, const p64_mb_rec 
                            uint16_t *blk_bits, void *stream) {
   const int fmt = p64s_format_of(width, height);
   if (fmt < 0) return fmt;
-  uint32_t tab[108];
-  int s = p64gpu_vlc_len_table_(tab);
+  p64k::VlcLenTab lt;
+  int s = p64gpu_vlc_len_table_(lt.w);
   if (s) return s;
   int ngob = 0;
   p64s_geometry(fmt, nullptr, nullptr, &ngob);
@@ -545,7 +562,7 @@ int p64gpu_vlc_block_bits_(int width, int height, int nframes, const p64_mb_rec 
     a.coef = coef + m0 * 384;
     a.blk_bits = blk_bits + m0 * 8;
     const dim3 grid((unsigned)((nmb + VLC_WAVES * VLC_MBS - 1) / (VLC_WAVES * VLC_MBS)), (unsigned)nc);
-    hipLaunchKernelGGL(k_vlc_blk<false>, grid, dim3(64 * VLC_WAVES), 0, (hipStream_t)stream, a, g_tab);
+    hipLaunchKernelGGL(k_vlc_blk<false>, grid, dim3(64 * VLC_WAVES), 0, (hipStream_t)stream, a, g_tab, lt);
   }
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? P64GPU_OK : p64gpu_fail_(P64GPU_E_HIP, hipGetErrorString(e));

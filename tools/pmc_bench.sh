@@ -1,7 +1,7 @@
 #!/bin/bash
 # PMC evidence for bench.py's roofline.traffic and valu_busy (GPU box):
 # one rocprofv3 --pmc pass per counter group (never with tracing), over the
-# default workload (k_motion<2>, k_inter_mbg, k_intra_mbg, k_recon_mbg on synth content)
+# default workload (k_motion<2>, k_inter_mbg, k_intra_mbg, k_recon_mbg on survey and synth content)
 # and the stress contents, plus a calibration pass over tools/ubench_valu
 # (kernels of known VALU issue rate).  tools/pmc_merge.py turns the output
 # into profiles/pmc_traffic.json entries.
@@ -21,7 +21,8 @@ run() {  # tag, program args...
   echo "pmc $tag done"
 }
 B="$R/bench.py --steps 10 --warmup 2 --no-cpu --no-verify --no-vlc --eager --spinup-ms 0"
-for t in calib synth noise pan15 flat; do mkdir -p $OUT/$t; done
+for t in calib survey synth noise pan15 flat; do mkdir -p $OUT/$t; done
 run calib $R/tools/ubench_valu new
-run synth python3 $B
-for c in noise pan15 flat; do run $c python3 $B --content $c --no-extra; done
+run survey python3 $B --content survey
+run synth python3 $B --content synth
+for c in ${STRESS-noise pan15 flat}; do run $c python3 $B --content $c --no-extra; done

@@ -37,18 +37,22 @@ import isa_mix  # noqa: E402
 SIMDS = 1024
 XCDS = 8
 WORKLOADS = {  # pmc_bench.sh tag -> {kernel: bench.py pmc key}
-    "synth": {"k_motion<2>": "352x288_full31_q8_S256_me", "k_inter_mbg<false, false, true>": "352x288_full31_q8_S256_inter",
-              "k_intra_mbg<false, false, true>": "352x288_intra_q8_S256", "k_recon_mbg": "352x288_decode_q8_S256"},
+    "synth": {"k_motion<2>": "352x288_full31_q8_S256_me", "k_inter_mbg<false, false, true, false>": "352x288_full31_q8_S256_inter",
+              "k_intra_mbg<false, false, true, false>": "352x288_intra_q8_S256", "k_recon_mbg": "352x288_decode_q8_S256"},
+    "survey": {"k_motion<2>": "352x288_full31_q8_S256_survey_me",
+               "k_inter_mbg<false, false, true, false>": "352x288_full31_q8_S256_survey_inter",
+               "k_intra_mbg<false, false, true, false>": "352x288_intra_q8_S256_survey",
+               "k_recon_mbg": "352x288_decode_q8_S256_survey"},
     "noise": {"k_motion<2>": "352x288_full31_q8_S256_noise_me",
-              "k_inter_mbg<false, false, true>": "352x288_full31_q8_S256_noise_inter"},
+              "k_inter_mbg<false, false, true, false>": "352x288_full31_q8_S256_noise_inter"},
     "pan15": {"k_motion<2>": "352x288_full31_q8_S256_pan15_me",
-              "k_inter_mbg<false, false, true>": "352x288_full31_q8_S256_pan15_inter"},
+              "k_inter_mbg<false, false, true, false>": "352x288_full31_q8_S256_pan15_inter"},
     "flat": {"k_motion<2>": "352x288_full31_q8_S256_flat_me",
-             "k_inter_mbg<false, false, true>": "352x288_full31_q8_S256_flat_inter"},
+             "k_inter_mbg<false, false, true, false>": "352x288_full31_q8_S256_flat_inter"},
 }
-ASM_LABEL = {"k_encode<2>": "k_encodeILi2E", "k_intra_mbg<false, false, true>": "k_intra_mbgILb0ELb0ELb1E",
+ASM_LABEL = {"k_encode<2>": "k_encodeILi2E", "k_intra_mbg<false, false, true, false>": "k_intra_mbgILb0ELb0ELb1ELb0E",
              "k_recon_blk": "k_recon_blk", "k_recon_mbg": "k_recon_mbg", "k_motion<2>": "k_motionILi2E",
-             "k_inter_mbg<false, false, true>": "k_inter_mbgILb0ELb0ELb1E"}
+             "k_inter_mbg<false, false, true, false>": "k_inter_mbgILb0ELb0ELb1ELb0E"}
 
 
 def short(name):

@@ -1,5 +1,6 @@
 """Counted side build of k_search.hip (development aid, never shipped):
-writes abtest/k_search_sadcount.hip, whose every v_sad_u8 (sad4) also adds 1
+writes abtest/k_search_sadcount.hip, whose every v_sad_u8 (sad4) and
+v_sad_hi_u8 (the bound pass's high halves) also adds 1
 to a per-lane counter in device memory, so a launch's executed v_sad_u8
 work (lane-instructions x 4 byte-absolute-differences) can be read back by
 p64dbg_sadcnt_read().  Control flow is data-dependent only, so the counts are
@@ -13,12 +14,18 @@ s = open(os.path.join(REPO, "p64_amd/csrc/k_search.hip")).read()
 n = s.count("sad4(")
 assert n > 10, n
 s = s.replace("sad4(", "sad4c(")
+# the bound pass's high-half SADs (v_sad_hi_u8: the same 4 byte-absolute-differences)
+s = s.replace("__builtin_amdgcn_sad_hi_u8(", "sad4hic(")
 s = s.replace("namespace {\n", """namespace {
 // one counter per lane of the launch (grid < 131072 one-wave workgroups)
 __device__ unsigned g_sadcnt[1u << 23];
 __device__ __forceinline__ uint32_t sad4c(uint32_t a, uint32_t b, uint32_t acc) {
   g_sadcnt[blockIdx.x * 64u + (threadIdx.x & 63u)] += 1u;
   return __builtin_amdgcn_sad_u8(a, b, acc);
+}
+__device__ __forceinline__ uint32_t sad4hic(uint32_t a, uint32_t b, uint32_t acc) {
+  g_sadcnt[blockIdx.x * 64u + (threadIdx.x & 63u)] += 1u;
+  return __builtin_amdgcn_sad_hi_u8(a, b, acc);
 }
 """, 1)
 s += """
