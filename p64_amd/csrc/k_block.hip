@@ -979,6 +979,69 @@ __device__ __forceinline__ void idct_coded_blocks(bool ck, const uint32_t np[8][
   }
   WAVE_FENCE();
 }
+// IQ (ICCITTQuantize transform.c:400) + ChenIDct + reconstruction of one
+// inter-coded block in its own lane, no LDS: the packed column pass of the
+// intra path (idct_col_pair_pk on dequantised natural column pairs) -- exact
+// when every dequantised value is within +-1,291, the largest box whose every
+// intermediate of that pass stays inside int16
+// (tests/test_intra_dct_bound.py) -- then the row pass on those pairs by
+// v_dot2 (32-bit sums), idct_final and the prediction (recon_row), as
+// idct_coded_blocks computes them.  np: the block's raw natural column pairs
+// (x0c,x4c) (x1c,x7c) (x5c,x3c) (x2c,x6c); prow: prediction in,
+// reconstruction out.
+__device__ __forceinline__ void iq_idct_inter_rec(const uint32_t np[8][4], int q, uint2 prow[8]) {
+  const uint32_t q2 = 0x20002u * (uint32_t)q, qq = 0x10001u * (uint32_t)(q - (int)!(q & 1));
+  s16x2 cp[4][8];  // [column pair (0,4) (1,7) (5,3) (2,6)][row]
+  {
+    constexpr int CA[4] = {0, 1, 5, 2}, CB[4] = {4, 7, 3, 6};
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      uint32_t a[4], b[4];
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        a[k] = dequantise_pk(np[CA[i]][k], q2, qq);
+        b[k] = dequantise_pk(np[CB[i]][k], q2, qq);
+      }
+      idct_col_pair_pk(a, b, cp[i]);
+      SCHED_FENCE();
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 8; r++) {
+    const s16x2 a04 = cp[0][r], a17 = cp[1][r], a53 = cp[2][r], a26 = cp[3][r];
+    const int p0 = ms9(dot2(a17, C7D16, -C1D16)), p3 = ms9(dot2(a17, C1D16, C7D16));
+    const int p1 = ms9(dot2(a53, C3D16, -C5D16)), p2 = ms9(dot2(a53, C5D16, C3D16));
+    const int q0 = ms9(dot2(a04, C1D4, C1D4)), q1 = ms9(dot2(a04, C1D4, -C1D4));
+    const int q2_ = ms9(dot2(a26, C3D8, -C1D8)), q3 = ms9(dot2(a26, C1D8, C3D8));
+    const int e0 = q0 + q3, e1 = q1 + q2_, e2 = q1 - q2_, e3 = q0 - q3;
+    const int f0 = p0 + p1, f1 = p0 - p1, f2 = p3 - p2, f3 = p3 + p2;
+    const int g1 = ms9(kmul<true>(C1D4, f2 - f1)), g2 = ms9(kmul<true>(C1D4, f2 + f1));
+    int o[8] = {e0 + f3, e1 + g2, e2 + g1, e3 + f0, e3 - f0, e2 - g1, e1 - g2, e0 - f3};
+#pragma unroll
+    for (int k = 0; k < 8; k++) o[k] = idct_final(o[k]);
+    prow[r] = recon_row(o, prow[r]);
+    SCHED_FENCE();
+  }
+}
+// the largest level magnitude, squared, whose dequantised value (2|l| + 1) q
+// stays within the +-1,291 of iq_idct_inter_rec's packed column pass, by q
+struct InterIdctLim {
+  int l2[32];
+};
+constexpr InterIdctLim make_inter_idct_lim() {
+  InterIdctLim t{};
+  for (int q = 1; q < 32; q++) {
+    int l = 0;
+    while ((2 * (l + 1) + 1) * q <= 1291) l++;
+    t.l2[q] = l * l;
+  }
+  return t;
+}
+__constant__ InterIdctLim c_idct_lim = make_inter_idct_lim();
+#ifndef INTER_DIRECT_MIN
+#define INTER_DIRECT_MIN 32  // coded blocks in a wave from which each lane runs its own IQ/IDCT
+#endif
+
 // the decoder's reconstruction through idct_coded_blocks
 __device__ __forceinline__ void rec_wave_compact(int w, int h, int64_t stride, __amdgpu_buffer_rsrc_t rec,
                                                  const RecStageA &A, const RecStageB &S, uint32_t *slots,
@@ -1306,8 +1369,18 @@ __global__ __launch_bounds__(64) OCC4 void k_inter_mbg(p64gpu_encode_args a, Blk
   const int pw = pos.plane ? w >> 1 : w;
   const uint32_t ro = (uint32_t)((int64_t)pos.fi * stride) + (uint32_t)plane_offset(pos.plane, w, h) +
                       (uint32_t)mul24(pos.y, pw) + (uint32_t)pos.x;
-  // IQ + ChenIDct + reconstruction of the coded blocks, into their prow
-  idct_coded_blocks(ck, np, q, intra, prow, (uint32_t *)lds, lane);
+  // IQ + ChenIDct + reconstruction of the coded blocks, into their prow: a
+  // wave with many coded blocks (SURVEY.md 8(d)'s content: 46 of 60 on
+  // average) runs one block per lane in registers when every coded block is
+  // an inter one whose levels keep the packed column pass exact (sum l^2 <=
+  // the limit squared bounds max |l|); else the coded-block pass through LDS
+  const int nck = __popcll(__ballot(ck));
+  const bool lane_ok = !ck || (!intra && ss <= c_idct_lim.l2[q]);
+  if (nck >= INTER_DIRECT_MIN && uni(__all(lane_ok))) {
+    if (ck) iq_idct_inter_rec(np, q, prow);
+  } else {
+    idct_coded_blocks(ck, np, q, intra, prow, (uint32_t *)lds, lane);
+  }
   // no levels at all in the MB: the reconstruction is the new prediction
   if (repred) inter_pred(B, w, h, stride, pos, mt, mvx, mvy, prow);
   // p64.c:909-910: the record (transmitted vector only for MC types) and LastIntra

@@ -189,3 +189,52 @@ def test_inter_residual_sum_bound_keeps_the_clamp_inactive():
                 worst_ac = max(worst_ac, v)
     assert worst_ac <= 8 * 1023 + 3, worst_ac
     assert worst_dc <= 8 * (256 * 5 - 1) + 3, worst_dc
+
+
+def test_inter_idct_column_pass_fits_int16():
+    """k_inter_mbg runs its coded blocks' IQ/IDCT one block per lane with the
+    intra path's packed column pass (k_block.hip iq_idct_inter_rec) when every
+    dequantised value is within +-1,291 (the wave-uniform check sum l^2 <=
+    c_idct_lim.l2[q], (2|l| + 1) q <= 1,291): with every input of the pass in
+    that box -- an inter DC is dequantised like an AC and may be negative --
+    each packed value stays inside int16, and 1,292 does not."""
+    def worst(L):
+        class I:
+            def __init__(self, lo, hi):
+                self.lo, self.hi = lo, hi
+
+            def __add__(self, o):
+                return I(self.lo + o.lo, self.hi + o.hi)
+
+            def __sub__(self, o):
+                return I(self.lo - o.hi, self.hi - o.lo)
+
+            def mul(self, c):
+                return I(min(self.lo * c, self.hi * c), max(self.lo * c, self.hi * c))
+
+            def ms9(self):
+                return I(self.lo // 512, self.hi // 512)
+
+            def mag(self):
+                return max(-self.lo, self.hi)
+
+        x = [I(-L, L) for _ in range(8)]
+        d = lambda a, ca, b, cb: (a.mul(ca) + b.mul(cb)).ms9()  # noqa: E731
+        P0, P3 = d(x[1], 4 * C7D16, x[7], -4 * C1D16), d(x[1], 4 * C1D16, x[7], 4 * C7D16)
+        P1, P2 = d(x[5], 4 * C3D16, x[3], -4 * C5D16), d(x[5], 4 * C5D16, x[3], 4 * C3D16)
+        Q0, Q1 = d(x[0], 4 * C1D4, x[4], 4 * C1D4), d(x[0], 4 * C1D4, x[4], -4 * C1D4)
+        Q2, Q3 = d(x[2], 4 * C3D8, x[6], -4 * C1D8), d(x[2], 4 * C1D8, x[6], 4 * C3D8)
+        E = [Q0 + Q3, Q1 + Q2, Q1 - Q2, Q0 - Q3]
+        F = [P0 + P1, P0 - P1, P3 - P2, P3 + P2]
+        Dm, Dp = F[2] - F[1], F[2] + F[1]
+        G1, G2 = Dm.mul(C1D4).ms9(), Dp.mul(C1D4).ms9()
+        O = [E[0] + F[3], E[1] + G2, E[2] + G1, E[3] + F[0], E[3] - F[0], E[2] - G1, E[1] - G2, E[0] - F[3]]
+        return max(v.mag() for v in [P0, P1, P2, P3, Q0, Q1, Q2, Q3] + E + F + [Dm, Dp, G1, G2] + O)
+
+    assert worst(1291) < 2 ** 15
+    assert worst(1292) >= 2 ** 15
+    # the kernel's per-q limit: the largest |l| with (2|l| + 1) q <= 1,291
+    for q in range(1, 32):
+        lmax = max(l for l in range(0, 700) if (2 * l + 1) * q <= 1291)
+        # every dequantised value (2|l| + 1) q - [q even] of |l| <= lmax is inside the box
+        assert (2 * lmax + 1) * q <= 1291 < (2 * lmax + 3) * q
