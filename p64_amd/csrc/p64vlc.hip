@@ -222,8 +222,9 @@ __device__ __forceinline__ void code_of(const VlcTables &T, uint32_t e, bool fir
     n = f.len + 1;
   }
 }
-__device__ __forceinline__ void block_codes(const VlcTables &T, const uint16_t *lvs, uint32_t m0, uint32_t m1,
-                                            bool cbpt, BitWriter &bw) {
+template <typename L>  // the level copy: int8 in LDS (the common case) or the int16 levels themselves
+__device__ __forceinline__ void block_codes(const VlcTables &T, const L *lvs, uint32_t m0, uint32_t m1, bool cbpt,
+                                            BitWriter &bw) {
   uint64_t m = ((uint64_t)m1 << 32) | m0;
   if (cbpt && !m) return;
   int last = cbpt ? -1 : 0;
@@ -234,7 +235,7 @@ __device__ __forceinline__ void block_codes(const VlcTables &T, const uint16_t *
     const bool two = m != 0;
     const int p2 = two ? (int)__builtin_ctzll(m | (1ull << 63)) : p1;
     m &= m - 1u;
-    const int l1 = (int)(int16_t)lvs[p1], l2 = (int)(int16_t)lvs[p2];
+    const int l1 = (int)lvs[p1], l2 = (int)lvs[p2];
     const int r1 = p1 - last - 1, r2 = p2 - p1 - 1;
     last = p2;
     const int a1 = l1 < 0 ? -l1 : l1, a2 = l2 < 0 ? -l2 : l2;
@@ -264,7 +265,12 @@ __device__ __forceinline__ void block_codes(const VlcTables &T, const uint16_t *
 //     into mb_bits[stream position]
 //   emit  (EMIT true):  each block's codes from its bit offset: the MB's
 //     offset (k_vlc_scan) + its header + the blocks before it
-constexpr int VLC_STAGE = 144;  // bytes per lane of the level copy: 128 + 16 pad (ds_write_b128 without conflicts)
+// The levels' LDS copy is int8 (64 + 16 pad bytes per lane: 7 workgroups of
+// four waves per CU, against 4 with the int16 copy); H.261 levels fit it.  A
+// wave with a coded level outside -128..127 (which the reference's quantiser
+// never makes, but the ABI takes) reads the int16 levels from memory instead:
+// the codes stay the host writer's for every int16 value.
+constexpr int VLC_STAGE = 80;
 template <bool EMIT>
 __global__ __launch_bounds__(64 * VLC_WAVES) void k_vlc_blk(VlcArgs a, VlcTables Tg, p64k::VlcLenTab Lg) {
   __shared__ VlcTables T;  // per-lane table lookups from LDS, loaded once per workgroup
@@ -277,25 +283,17 @@ __global__ __launch_bounds__(64 * VLC_WAVES) void k_vlc_blk(VlcArgs a, VlcTables
   const int fi = blockIdx.y;
   const int mb0 = (blockIdx.x * VLC_WAVES + wv) * VLC_MBS;
   if (mb0 >= a.nmb) return;  // whole wave (after the only barrier)
-  if (EMIT && a.bits[fi] == 0xFFFFFFFFu) return;  // invalid record or no room: nothing written
+  const uint32_t pic_bits = EMIT ? a.bits[fi] : 0u;  // (checked once the level loads are out)
   const int l = min(lane, 6 * VLC_MBS - 1), b = l % 6;
   const int k = min(mb0 + l / 6, a.nmb - 1);  // raster MB (tail lanes repeat the last)
   const bool act = lane < 6 * VLC_MBS && mb0 + l / 6 < a.nmb;
   const size_t base = (size_t)fi * a.nmb;
-  const p64_mb_rec r = a.mb[base + k];
-  const int j = stream_pos(a.format, k), g = j / 33, m = j - g * 33;
-  const p64_mb_rec rp = a.mb[base + (m % 11 ? k - 1 : k)];  // MVD predictor (same GOB row)
-  const int mq = a.mquant ? (int)a.mquant[base + k] : 0;
-  const int mt = r.mtype;
-  const bool valid = mt >= 0 && mt <= 9;
-  const bool cbpt = valid && mt_cbp(mt);
-  const int cbp = cbpt ? r.cbp : 0x3f;
-  const bool coded = act && valid && mt_tc(mt) && ((cbp >> (5 - b)) & 1);
+  // every lane's block is loaded, coded or not: the loads need not wait for the record
+  const uint32_t co = (uint32_t)(((base + k) * 6 + b) * 128);
   uint32_t lv[32];
   {
     const __amdgpu_buffer_rsrc_t cr = __builtin_amdgcn_make_buffer_rsrc(
         (void *)a.coef, (short)0, (int)((size_t)a.nframes * a.nmb * 768), 0x00020000);  // < 2 GiB (host split)
-    const uint32_t co = coded ? (uint32_t)(((base + k) * 6 + b) * 128) : 0x80000000u;
 #pragma unroll
     for (int i = 0; i < 8; i++) {
       const auto v = __builtin_amdgcn_raw_buffer_load_b128(cr, co + 16 * i, 0, 0);
@@ -305,24 +303,52 @@ __global__ __launch_bounds__(64 * VLC_WAVES) void k_vlc_blk(VlcArgs a, VlcTables
       lv[4 * i + 3] = v[3];
     }
   }
-  // the block's nonzero positions (the DC of an intra block is coded apart)
-  // and its levels in LDS for the indexed reads of block_codes
+  const p64_mb_rec r = a.mb[base + k];
+  const int j = stream_pos(a.format, k), g = j / 33, m = j - g * 33;
+  const p64_mb_rec rp = a.mb[base + (m % 11 ? k - 1 : k)];  // MVD predictor (same GOB row)
+  const int mq = a.mquant ? (int)a.mquant[base + k] : 0;
+  const int mt = r.mtype;
+  const bool valid = mt >= 0 && mt <= 9;
+  const bool cbpt = valid && mt_cbp(mt);
+  const int cbp = cbpt ? r.cbp : 0x3f;
+  const bool coded = act && valid && mt_tc(mt) && ((cbp >> (5 - b)) & 1);
+  // the block's nonzero positions (the DC of an intra block is coded apart),
+  // its levels as int8 in LDS for the indexed reads of the code loops, and
+  // whether one of them does not fit (+128 per int16 half: a byte or not)
   uint32_t m0, m1;
   nz_masks(lv, m0, m1);
   if (!cbpt && EMIT) m0 &= ~1u;  // (the count's block_vlc_bits clears it itself)
   if (!coded) m0 = m1 = 0;
+  uint32_t wide = 0;
+#pragma unroll
+  for (int i = 0; i < 32; i++) {
+    uint32_t x = __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2_t, lv[i]) + (u16x2_t){128, 128});
+    if (i == 0 && !cbpt) x &= 0xffff0000u;  // (an intra DC is coded from lv[0] itself)
+    wide |= x;
+  }
+  const bool narrow = !__any(coded && (wide & 0xff00ff00u));
   uint8_t *stl = stage + (wv * 64 + lane) * VLC_STAGE;
 #pragma unroll
-  for (int i = 0; i < 8; i++)
-    *reinterpret_cast<uint4 *>(stl + 16 * i) = make_uint4(lv[4 * i], lv[4 * i + 1], lv[4 * i + 2], lv[4 * i + 3]);
-  const uint16_t *lvs = reinterpret_cast<const uint16_t *>(stl);
+  for (int i = 0; i < 4; i++)
+    *reinterpret_cast<uint4 *>(stl + 16 * i) = make_uint4(
+        __builtin_amdgcn_perm(lv[8 * i + 1], lv[8 * i], 0x06040200u),
+        __builtin_amdgcn_perm(lv[8 * i + 3], lv[8 * i + 2], 0x06040200u),
+        __builtin_amdgcn_perm(lv[8 * i + 5], lv[8 * i + 4], 0x06040200u),
+        __builtin_amdgcn_perm(lv[8 * i + 7], lv[8 * i + 6], 0x06040200u));
+  const int8_t *lvs = reinterpret_cast<const int8_t *>(stl);
+  const int16_t *lvg = reinterpret_cast<const int16_t *>(a.coef) + ((base + k) * 6 + b) * 64;
+  if (EMIT && pic_bits == 0xFFFFFFFFu) return;  // invalid record or no room: nothing written
   BitWriter bw;
   uint32_t *out = a.out + (size_t)fi * a.out_words;
   if (!EMIT) {
     const Header hd = header_codes(T, r, rp, mq, m);
-    const int bb = coded ? p64k::block_vlc_bits(reinterpret_cast<const uint8_t *>(vlen),
-                                                reinterpret_cast<const int16_t *>(lvs), m0, m1, cbpt)
-                         : 0;  // (intra: + DC)
+    const uint8_t *len = reinterpret_cast<const uint8_t *>(vlen);
+    int bb = 0;  // (intra: + DC)
+    if (narrow) {
+      if (coded) bb = p64k::block_vlc_bits(len, lvs, m0, m1, cbpt);
+    } else if (coded) {
+      bb = p64k::block_vlc_bits(len, lvg, m0, m1, cbpt);
+    }
     // the MB's six lanes: header and block bits into blk_bits, the total
     uint16_t *bk = a.blk_bits + (base + k) * 8;
     if (act) bk[1 + b] = (uint16_t)bb;
@@ -369,7 +395,10 @@ __global__ __launch_bounds__(64 * VLC_WAVES) void k_vlc_blk(VlcArgs a, VlcTables
         const int dc = dc0 < 1 ? 1 : (dc0 > 254 ? 254 : dc0);
         bw.put((uint32_t)(dc == 128 ? 255 : dc), 8);
       }
-      block_codes(T, lvs, m0, m1, cbpt, bw);
+      if (narrow)
+        block_codes(T, lvs, m0, m1, cbpt, bw);
+      else
+        block_codes(T, lvg, m0, m1, cbpt, bw);
       bw.finish();
     }
   }

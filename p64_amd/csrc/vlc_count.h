@@ -32,15 +32,15 @@ __device__ __forceinline__ uint32_t nz2(uint32_t pair) {
   return __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2_t, r), (u16x2_t){1, 2}, 0u, false);
 }
 
-// bits of one transmitted block from its 64 levels in scan order (lvs, LDS)
+// bits of one transmitted block from its 64 levels in scan order (lvs)
 // and its nonzero positions (m0: 0..31, m1: 32..63).  cbpt: a type with CBP
 // (the first coefficient may take FIRST01, no DC of its own); else an intra
 // block (its DC as 8 bits, the AC codes from position 1).  The loop visits
 // the nonzero positions only, two per step and without branches: both
 // levels and both lengths are read together, so each step waits for two
 // LDS round trips, not four.
-__device__ __forceinline__ int block_vlc_bits(const uint8_t *len, const int16_t *lvs, uint32_t m0, uint32_t m1,
-                                              bool cbpt) {
+template <typename L>  // int16 levels, or an int8 copy of levels that fit it
+__device__ __forceinline__ int block_vlc_bits(const uint8_t *len, const L *lvs, uint32_t m0, uint32_t m1, bool cbpt) {
   int bits = cbpt ? 2 : 10;  // EOB (+ the intra DC)
   if (!cbpt) m0 &= ~1u;
   uint64_t m = ((uint64_t)m1 << 32) | m0;

@@ -294,3 +294,37 @@ def test_gpu_vlc_block_bits_from_encoder(p64, torch_dev, monkeypatch, case):
         wr = stream.Writer(stream.QCIF)
         wr.write_picture(int(tr[i]), mb_h[i], coef_h[i], q, quant_mb=mq[i].cpu().numpy() if mq is not None else None)
         assert b1[i] - int(phase[i]) == wr.bits()
+
+
+@pytest.mark.parametrize("name", ["qcif_intra", "qcif_full31"])
+def test_gpu_vlc_levels_outside_int8(p64, torch_dev, name):
+    """The coder keeps an int8 copy of the levels (p64vlc.hip VLC_STAGE): a
+    picture with levels outside -128..127 (the ABI takes any int16; the
+    reference's quantiser never makes them) codes from the int16 levels and
+    still equals the host writer bit for bit -- the escape's 8-bit field and
+    the table/escape choice by |level|, the intra DC clamp -- through both the
+    coder's count pass and the emit."""
+    from p64_amd import stream
+    torch = torch_dev
+    z = load(f"seq_{name}.npz")
+    mb, coef, gq, uq = fixture_records(z, stream.format_of(176, 144))
+    n = mb.shape[0]
+    rng = np.random.default_rng(5)
+    wide = np.array([128, -129, 200, -250, 250, 256, -256, 300, 1000, -32768, 32767], np.int16)
+    coef = coef.copy()
+    for t in range(0, n, 2):  # every other picture keeps its levels: both paths in one launch
+        k = rng.integers(0, mb.shape[1], 12)
+        coef[t, k, rng.integers(0, 6, 12), rng.integers(1, 64, 12)] = rng.choice(wide, 12)
+        coef[t, k[:3], 0, 0] = [300, -5, 128]  # intra DCs clamp (1..254, 128 -> 255)
+    d = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()  # noqa: E731
+    tr = np.arange(n, dtype=np.int32) % 32
+    out, bits = stream.vlc_pictures(d(mb), d(coef), d(gq), d(tr), width=176, height=144, mquant=d(uq))
+    out = out.cpu().numpy()
+    for t in range(n):
+        wr = stream.Writer(stream.QCIF)
+        wr.write_picture(int(tr[t]), mb[t], coef[t], gq[t], quant_mb=uq[t])
+        full = wr.data()
+        assert bits[t] == wr.bits()
+        nb = (bits[t] + 7) // 8
+        gpu = int.from_bytes(out[t, :nb].tobytes(), "big") >> (nb * 8 - bits[t])
+        assert gpu >> (bits[t] - 8 * len(full)) == int.from_bytes(full, "big"), f"{name} picture {t}"
