@@ -129,6 +129,17 @@ __device__ __forceinline__ int wave_sum_i(int v) {
   return __builtin_amdgcn_readlane(wave_incl_scan(v), 63);
 }
 __device__ __forceinline__ int wave_excl_scan(int v, int) { return wave_incl_scan(v) - v; }
+__device__ __forceinline__ int wave_max_i(int x) {
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) x = max(x, __shfl_xor(x, d));
+  return x;
+}
+// the wave's LDS writes done and visible to its lanes
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
 
 constexpr int VLC_WAVES = 4;  // waves per workgroup
 constexpr int VLC_MBS = 10;   // macroblocks per wave: lane 6m + b codes block b of MB m
@@ -179,6 +190,34 @@ struct BitWriter {
   }
 };
 
+// The same writer into a wave's LDS copy of its bits (words from w0 on, all
+// ORed: the copy was zeroed), written out whole afterwards
+struct LdsBitWriter {
+  uint64_t acc;
+  int nacc;
+  int w;  // word index in the copy
+  uint32_t *buf;
+  int64_t w0;
+  __device__ __forceinline__ void start(uint32_t *b, int64_t pos) {
+    buf = b;
+    w = (int)((pos >> 5) - w0);
+    nacc = (int)(pos & 31);
+    acc = 0;
+  }
+  __device__ __forceinline__ void put(uint32_t v, int n) {
+    acc = (acc << n) | v;
+    nacc += n;
+    if (nacc >= 32) {
+      atomicOr(buf + w, __builtin_bswap32((uint32_t)(acc >> (nacc - 32))));
+      w++;
+      nacc -= 32;
+    }
+  }
+  __device__ __forceinline__ void finish() {
+    if (nacc > 0) atomicOr(buf + w, __builtin_bswap32((uint32_t)(acc << (32 - nacc))));
+  }
+};
+
 // the scan positions of a block holding a nonzero level, as two 32-bit masks
 // (bit p of m0: position p; of m1: position 32 + p) from its 32 packed level
 // pairs: v_pk_min_u16 against 1 (a nonzero int16 is >= 1 as u16), v_dot2
@@ -222,9 +261,9 @@ __device__ __forceinline__ void code_of(const VlcTables &T, uint32_t e, bool fir
     n = f.len + 1;
   }
 }
-template <typename L>  // the level copy: int8 in LDS (the common case) or the int16 levels themselves
+template <typename L, class W>  // L: the level copy, int8 in LDS (the common case) or the int16 levels themselves
 __device__ __forceinline__ void block_codes(const VlcTables &T, const L *lvs, uint32_t m0, uint32_t m1, bool cbpt,
-                                            BitWriter &bw) {
+                                            W &bw) {
   uint64_t m = ((uint64_t)m1 << 32) | m0;
   if (cbpt && !m) return;
   int last = cbpt ? -1 : 0;
@@ -255,37 +294,44 @@ __device__ __forceinline__ void block_codes(const VlcTables &T, const L *lvs, ui
   bw.put(eob.v, eob.len);
 }
 
-// Lane-per-block entropy coding: a wave takes 10 raster macroblocks, lane
-// 6m + b block b of the m-th (the encoder's layout), lane b = 0 also the MB
-// header (and the GOB / picture header before MDU 0 / GOB 0).  Every lane
-// runs its own block's scan serially (no cross-lane step per code), with the
-// block's 64 levels in registers (8 x 16-byte loads; none for blocks the
-// record leaves uncoded).
+// Lane-per-block entropy coding: a wave takes 10 macroblocks consecutive in
+// stream order (GOB by GOB), lane 6m + b block b of the m-th, lane b = 0 also
+// the MB header (and the GOB / picture header before MDU 0 / GOB 0).  Every
+// lane runs its own block's scan serially (no cross-lane step per code), from
+// an LDS copy of the block's levels.
 //   count (EMIT false): header and block bits into blk_bits, the MB's total
 //     into mb_bits[stream position]
 //   emit  (EMIT true):  each block's codes from its bit offset: the MB's
-//     offset (k_vlc_scan) + its header + the blocks before it
-// The levels' LDS copy is int8 (64 + 16 pad bytes per lane: 7 workgroups of
-// four waves per CU, against 4 with the int16 copy); H.261 levels fit it.  A
-// wave with a coded level outside -128..127 (which the reference's quantiser
-// never makes, but the ABI takes) reads the int16 levels from memory instead:
-// the codes stay the host writer's for every int16 value.
+//     offset (k_vlc_scan) + its header + the blocks before it.  The wave's
+//     bits are one contiguous range of the picture: assembled in LDS (ORs of
+//     the lanes' words there), then stored word per lane -- plain stores,
+//     except the range's first and last words, which the neighbouring waves
+//     share (ORed into the words k_vlc_scan zeroed).  A wave whose range
+//     exceeds its LDS copy writes straight to memory, every segment's first
+//     and last word ORed.
+// The levels' LDS copy is int8 (64 + 16 pad bytes per lane); H.261 levels fit
+// it.  A wave with a coded level outside -128..127 (which the reference's
+// quantiser never makes, but the ABI takes) reads the int16 levels from
+// memory instead: the codes stay the host writer's for every int16 value.
 constexpr int VLC_STAGE = 80;
+constexpr int VLC_EMIT_WORDS = 256;  // a wave's bits in LDS: up to 8,192 (10 MBs)
 template <bool EMIT>
 __global__ __launch_bounds__(64 * VLC_WAVES) void k_vlc_blk(VlcArgs a, VlcTables Tg, p64k::VlcLenTab Lg) {
   __shared__ VlcTables T;  // per-lane table lookups from LDS, loaded once per workgroup
   __shared__ uint32_t vlen[EMIT ? 1 : p64k::VLC_LEN_WORDS];  // the count's code lengths (vlc_count.h)
   if (!EMIT && threadIdx.x < 64) p64k::load_vlc_len(Lg, vlen, threadIdx.x);
   __shared__ __align__(16) uint8_t stage[VLC_WAVES * 64 * VLC_STAGE];  // each lane's levels, scan order
+  __shared__ __align__(16) uint32_t wbits[EMIT ? VLC_WAVES * VLC_EMIT_WORDS : 4];
   for (int i = threadIdx.x; i < T_N; i += 64 * VLC_WAVES) T.t[i] = Tg.t[i];
   __syncthreads();
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int fi = blockIdx.y;
-  const int mb0 = (blockIdx.x * VLC_WAVES + wv) * VLC_MBS;
+  const int mb0 = (blockIdx.x * VLC_WAVES + wv) * VLC_MBS;  // first stream position
   if (mb0 >= a.nmb) return;  // whole wave (after the only barrier)
   const uint32_t pic_bits = EMIT ? a.bits[fi] : 0u;  // (checked once the level loads are out)
   const int l = min(lane, 6 * VLC_MBS - 1), b = l % 6;
-  const int k = min(mb0 + l / 6, a.nmb - 1);  // raster MB (tail lanes repeat the last)
+  const int j = min(mb0 + l / 6, a.nmb - 1);  // stream position (tail lanes repeat the last)
+  const int g = j / 33, m = j - g * 33, k = raster(a.format, g, m);
   const bool act = lane < 6 * VLC_MBS && mb0 + l / 6 < a.nmb;
   const size_t base = (size_t)fi * a.nmb;
   // every lane's block is loaded, coded or not: the loads need not wait for the record
@@ -304,7 +350,6 @@ __global__ __launch_bounds__(64 * VLC_WAVES) void k_vlc_blk(VlcArgs a, VlcTables
     }
   }
   const p64_mb_rec r = a.mb[base + k];
-  const int j = stream_pos(a.format, k), g = j / 33, m = j - g * 33;
   const p64_mb_rec rp = a.mb[base + (m % 11 ? k - 1 : k)];  // MVD predictor (same GOB row)
   const int mq = a.mquant ? (int)a.mquant[base + k] : 0;
   const int mt = r.mtype;
@@ -338,7 +383,6 @@ __global__ __launch_bounds__(64 * VLC_WAVES) void k_vlc_blk(VlcArgs a, VlcTables
   const int8_t *lvs = reinterpret_cast<const int8_t *>(stl);
   const int16_t *lvg = reinterpret_cast<const int16_t *>(a.coef) + ((base + k) * 6 + b) * 64;
   if (EMIT && pic_bits == 0xFFFFFFFFu) return;  // invalid record or no room: nothing written
-  BitWriter bw;
   uint32_t *out = a.out + (size_t)fi * a.out_words;
   if (!EMIT) {
     const Header hd = header_codes(T, r, rp, mq, m);
@@ -358,48 +402,82 @@ __global__ __launch_bounds__(64 * VLC_WAVES) void k_vlc_blk(VlcArgs a, VlcTables
     for (int d = 1; d < 6; d++) tot += __shfl(bb, min(lane + d, 63));
     if (act && b == 0 && a.mb_bits) a.mb_bits[base + j] = hd.bad ? 0x80000000u : (uint32_t)(hd.bits + tot);
   } else {
-    if (!act) return;
     // (8-byte loads: blk_bits is 8-byte aligned, 2 nframes nmb words into scratch)
     const uint2 *bp = reinterpret_cast<const uint2 *>(a.blk_bits + (base + k) * 8);
     const uint2 b01 = bp[0], b23 = bp[1];
     const uint32_t bw4[4] = {b01.x, b01.y, b23.x, b23.y};
     const uint16_t *bh = reinterpret_cast<const uint16_t *>(bw4);
-    int64_t pos = (int64_t)a.mb_off[base + j] + bh[0];
+    const int64_t off = a.mb_off[base + j];
+    int64_t pos = off + bh[0];
 #pragma unroll
     for (int d = 0; d < 5; d++) pos += d < b ? bh[1 + d] : 0;
-    if (b == 0) {  // headers: picture (MDU 0 of GOB 0), GOB (MDU 0), MB
-      const int64_t off = a.mb_off[base + j];
-      const Header hd = header_codes(T, r, rp, mq, m);
-      const int64_t s0 = j == 0 ? (a.phase ? a.phase[fi] : 0) : (m == 0 ? off - 26 : off);
-      bw.start(out, s0);
-      if (j == 0) {  // WritePictureHeader marker.c:103-135
-        bw.put(0x10u, 20);
-        bw.put((uint32_t)a.tr[fi] & 31u, 5);
-        bw.put(a.format == P64S_QCIF ? 0u : 4u, 6);
-        if (a.format == P64S_NTSC) bw.put(0x18cu, 9);  // PEI 1, PSPARE 0x8c
-        bw.put(0u, 1);                                   // PEI 0
-      }
-      if (m == 0) {  // WriteGOBHeader marker.c:171-198
-        const uint32_t gn = a.format == P64S_QCIF ? 2 * g + 1 : g + 1;
-        bw.put((1u << 10) | (gn << 6) | ((a.gquant[(size_t)fi * a.ngob + g] & 31u) << 1), 26);
-      }
+    // the lane's segments: headers (b = 0) from s0: the picture header (MDU 0
+    // of GOB 0), the GOB header (MDU 0), the MB header; its block from pos
+    const int64_t s0 = j == 0 ? (a.phase ? a.phase[fi] : 0) : (m == 0 ? off - 26 : off);
+    auto emit = [&](auto &bw, uint32_t *dst) {
+      if (act && b == 0) {
+        const Header hd = header_codes(T, r, rp, mq, m);
+        bw.start(dst, s0);
+        if (j == 0) {  // WritePictureHeader marker.c:103-135
+          bw.put(0x10u, 20);
+          bw.put((uint32_t)a.tr[fi] & 31u, 5);
+          bw.put(a.format == P64S_QCIF ? 0u : 4u, 6);
+          if (a.format == P64S_NTSC) bw.put(0x18cu, 9);  // PEI 1, PSPARE 0x8c
+          bw.put(0u, 1);                                   // PEI 0
+        }
+        if (m == 0) {  // WriteGOBHeader marker.c:171-198
+          const uint32_t gn = a.format == P64S_QCIF ? 2 * g + 1 : g + 1;
+          bw.put((1u << 10) | (gn << 6) | ((a.gquant[(size_t)fi * a.ngob + g] & 31u) << 1), 26);
+        }
 #pragma unroll
-      for (int i = 0; i < 6; i++)
-        if (hd.c[i].len) bw.put(hd.c[i].v, hd.c[i].len);
-      bw.finish();
-    }
-    if (coded) {
-      bw.start(out, pos);
-      if (!cbpt) {  // EncodeDC codec.c:343-352
-        const int dc0 = (int)(int16_t)(lv[0] & 0xffffu);
-        const int dc = dc0 < 1 ? 1 : (dc0 > 254 ? 254 : dc0);
-        bw.put((uint32_t)(dc == 128 ? 255 : dc), 8);
+        for (int i = 0; i < 6; i++)
+          if (hd.c[i].len) bw.put(hd.c[i].v, hd.c[i].len);
+        bw.finish();
       }
-      if (narrow)
-        block_codes(T, lvs, m0, m1, cbpt, bw);
-      else
-        block_codes(T, lvg, m0, m1, cbpt, bw);
-      bw.finish();
+      if (coded) {
+        bw.start(dst, pos);
+        if (!cbpt) {  // EncodeDC codec.c:343-352
+          const int dc0 = (int)(int16_t)(lv[0] & 0xffffu);
+          const int dc = dc0 < 1 ? 1 : (dc0 > 254 ? 254 : dc0);
+          bw.put((uint32_t)(dc == 128 ? 255 : dc), 8);
+        }
+        if (narrow)
+          block_codes(T, lvs, m0, m1, cbpt, bw);
+        else
+          block_codes(T, lvg, m0, m1, cbpt, bw);
+        bw.finish();
+      }
+    };
+    // the wave's range [first, first + span): lane 0 holds the first segment
+    const int64_t first = ((int64_t)__builtin_amdgcn_readfirstlane((int)(s0 >> 32)) << 32) |
+                          (uint32_t)__builtin_amdgcn_readfirstlane((int)s0);
+    const int end = act ? (int)(pos + (coded ? bh[1 + b] : 0) - first) : 0;
+    const int span = wave_max_i(end);
+    const int64_t w0 = first >> 5;
+    const int nw = span > 0 ? (int)(((first + span - 1) >> 5) - w0 + 1) : 0;
+    if (nw <= VLC_EMIT_WORDS) {
+      uint32_t *wb = wbits + wv * VLC_EMIT_WORDS;
+      reinterpret_cast<uint4 *>(wb)[lane] = make_uint4(0, 0, 0, 0);
+      wave_lds_sync();
+      LdsBitWriter bw;
+      bw.w0 = w0;
+      emit(bw, wb);
+      wave_lds_sync();
+#pragma unroll
+      for (int i = 0; i < VLC_EMIT_WORDS / 64; i++) {
+        const int t = lane + 64 * i;
+        if (t < nw) {
+          const uint32_t v = wb[t];
+          if (t == 0 || t == nw - 1) {
+            if (v) atomicOr(out + w0 + t, v);
+          } else {
+            out[w0 + t] = v;
+          }
+        }
+      }
+    } else {
+      BitWriter bw;
+      emit(bw, out);
     }
   }
 }
