@@ -1126,43 +1126,55 @@ def measure_vlc(args, torch, p64_amd, step, out_of, S, nmb, w, h):
         vlc_ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
         bits_dev = [None] * vsteps
 
-        def vstep(k, ev=False):
+        def vstep(k, given, ev=False):
             t = 1 + args.warmup + k
-            step(t, vb)
+            step(t, vb if given else None)
             o = out_of(t)
             if ev:
                 vlc_ev[0].record()
             _, bits_dev[k] = p64s.vlc_pictures(o.mb, o.coef, gq, trs[k], width=w, height=h, buffers=bufs,
-                                               host_bits=False, blk_bits=vb)
+                                               host_bits=False, blk_bits=vb if given else None)
             if ev:
                 vlc_ev[1].record()
             host[k].copy_(bits_dev[k], non_blocking=True)
 
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
-            for k in range(vsteps):
-                vstep(k)
-        torch.cuda.synchronize()
-        g.replay()  # the first replay uploads the graph; the second is timed (its first
-        torch.cuda.synchronize()  # step predicts from the first replay's last picture)
-        t1 = time.perf_counter()
-        g.replay()
-        torch.cuda.synchronize()
-        dt = time.perf_counter() - t1
-        del g
-        vstep(vsteps - 1, ev=True)  # the VLC launches of one step alone, eagerly (vlc_ms_last_step)
-        torch.cuda.synchronize()
-        hb = host.numpy().astype(np.int64) & 0xFFFFFFFF
-        if (hb == 0xFFFFFFFF).any():
-            return {"error": "vlc: invalid record or overflow"}
-        return {"macroblocks_per_s": round(S * nmb * vsteps / dt, 1),
-                "ms_per_step": round(dt / vsteps * 1e3, 4),
-                "vlc_ms_last_step": round(vlc_ev[0].elapsed_time(vlc_ev[1]), 4),
-                "avg_bits_per_mb": round(float(hb.sum()) / (S * nmb * vsteps), 2),
-                "note": "encode launches (counting each transmitted block's coded bits) + GPU entropy "
-                        "coding (headers + offsets, scan, emit) per step, every picture's bit count "
-                        "copied to pinned host memory, the steps replayed as one HIP graph; not part "
-                        "of `value`"}
+        def run(given):
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                for k in range(vsteps):
+                    vstep(k, given)
+            torch.cuda.synchronize()
+            g.replay()  # the first replay uploads the graph; the second is timed (its first
+            torch.cuda.synchronize()  # step predicts from the first replay's last picture)
+            t1 = time.perf_counter()
+            g.replay()
+            torch.cuda.synchronize()
+            dt = time.perf_counter() - t1
+            del g
+            vstep(vsteps - 1, given, ev=True)  # the coder's launches of one step alone, eagerly
+            torch.cuda.synchronize()
+            hb = host.numpy().astype(np.int64) & 0xFFFFFFFF
+            if (hb == 0xFFFFFFFF).any():
+                raise RuntimeError("vlc: invalid record or overflow")
+            return {"macroblocks_per_s": round(S * nmb * vsteps / dt, 1),
+                    "ms_per_step": round(dt / vsteps * 1e3, 4),
+                    "vlc_ms_last_step": round(vlc_ev[0].elapsed_time(vlc_ev[1]), 4),
+                    "avg_bits_per_mb": round(float(hb.sum()) / (S * nmb * vsteps), 2)}
+
+        # the two ways to the bits: the encoder counts every transmitted block's
+        # bits (vlc_bits) and the coder takes them, or the coder counts
+        given, counting = run(True), run(False)
+        best, other = (given, counting) if given["ms_per_step"] <= counting["ms_per_step"] else (counting, given)
+        res = dict(best)
+        res["path"] = "encoder counts (vlc_bits -> blk_bits)" if best is given else "the coder counts"
+        res["other_path"] = dict(other, path="the coder counts" if best is given else
+                                 "encoder counts (vlc_bits -> blk_bits)")
+        res["note"] = ("encode launches + GPU entropy coding (one launch after a status-word memset: "
+                       "each wave of ten MBs counts or takes its bits, finds its start by a decoupled "
+                       "look-back, writes its words) per step, every picture's bit count copied to "
+                       "pinned host memory, the steps replayed as one HIP graph; the faster of the two "
+                       "paths (path / other_path); not part of `value`")
+        return res
     except Exception as e:  # never let the extra measurement cost the bench line
         return {"error": str(e)[:200]}
 

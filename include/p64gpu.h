@@ -192,7 +192,7 @@ typedef struct {
                              block's 8-bit DC), 0 if not transmitted; entry 0
                              and 7 are not written.  Hand it to
                              p64gpu_vlc_pictures as blk_bits: the coder then
-                             skips its count pass.  Not with
+                             does not count the blocks.  Not with
                              p64gpu_encode_mb_list (P64GPU_E_INVALID)        */
 } p64gpu_encode_args;
 
@@ -253,15 +253,16 @@ typedef struct {
   const uint8_t *mquant;    /* NULL or [nframes][nmb] MQUANT (types 1/3/6/9)  */
   const int32_t *tr;        /* [nframes] temporal references                  */
   const uint8_t *phase;     /* NULL (all 0) or [nframes] start bit 0..7       */
-  uint8_t *out;             /* [nframes][out_stride], zeroed by the call      */
+  uint8_t *out;             /* [nframes][out_stride]: every 32-bit word up to
+                               the picture's last bit written (the phase bits
+                               before its first as zeros), later ones left   */
   int64_t out_stride;       /* >= p64gpu_vlc_max_bytes, multiple of 4         */
   uint32_t *bits;           /* [nframes]                                      */
   uint32_t *scratch;        /* [6][nframes][nmb], 8-byte aligned              */
   uint16_t *blk_bits;       /* NULL, or [nframes][nmb][8] block bits from the
                                encoder (p64gpu_encode_args.vlc_bits, same
-                               records and levels), 16-byte aligned: the
-                               count pass is skipped; entry 0 is overwritten
-                               with the MB header's bits                     */
+                               records and levels), 16-byte aligned, read
+                               only: the blocks are not counted again        */
 } p64gpu_vlc_args;
 int64_t p64gpu_vlc_max_bytes(int width, int height);
 int p64gpu_vlc_pictures(const p64gpu_vlc_args *args, void *stream);

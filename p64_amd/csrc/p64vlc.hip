@@ -2,19 +2,11 @@
 //
 // The same bits as the host writer (p64stream.c; the reference's WriteMBHeader
 // marker.c:288, EncodeDC/EncodeAC/CBPEncodeAC codec.c:96-352, WriteGOBHeader
-// marker.c:171, WritePictureHeader marker.c:103), in three passes per batch of
-// pictures:
-//   1. k_vlc_count  one wave per macroblock: code lengths -> bits per MB.  Each
-//                   lane holds one zigzag level; the run before a nonzero level
-//                   is the distance to the next lower set bit of the wave's
-//                   nonzero ballot, so the run-length scan needs no loop.
-//   2. k_vlc_scan   stream-order prefix sum of the MB sizes per picture (GOB /
-//                   MDU order of Bpos io.c:757, headers included).
-//   3. k_vlc_emit   one wave per macroblock again: each lane places its codes
-//                   at its bit offset (wave prefix sum of lengths) with LDS
-//                   atomic ORs into the MB's segment, which is then stored;
-//                   only the two words shared with neighbouring segments are
-//                   ORed into global memory (the scan zeroed the used words).
+// marker.c:171, WritePictureHeader marker.c:103), in one launch per batch of
+// pictures (k_vlc_blk, below): one lane per 8x8 block, a wave per ten
+// macroblocks in stream order; each wave counts its bits (or takes the
+// encoder's counts), finds where they start by a decoupled look-back over the
+// waves before it in its picture, and writes them.
 // A picture starts at bit `phase` of its first byte so that it continues the
 // sequence's bitstream exactly (pictures are not byte aligned in H.261).
 #include <hip/hip_runtime.h>
@@ -50,9 +42,8 @@ struct VlcArgs {
   uint32_t *out;  // [nframes][out_words]
   int64_t out_words;
   uint32_t *bits;     // [nframes]
-  uint32_t *mb_bits;  // [nframes][nmb], stream order
-  uint32_t *mb_off;   // [nframes][nmb], stream order
-  uint16_t *blk_bits; // [nframes][nmb][8], raster order: header bits, the six blocks' bits
+  uint32_t *status;   // [nframes][waves][4]: the look-back's status words (zeroed before the launch)
+  uint16_t *blk_bits; // [nframes][nmb][8], raster order: [1 + b] block b's bits
 };
 
 __device__ __forceinline__ bool mt_quant(int m) { return m == 1 || m == 3 || m == 6 || m == 9; }
@@ -155,32 +146,24 @@ __device__ __forceinline__ int stream_pos(int format, int k) {
 
 // The bit writer of one lane: a segment of the picture's bits starting at
 // bit `pos`, MSB first, big-endian bytes in little-endian words (one bswap
-// per word).  A word wholly inside the segment is stored; the first and the
-// last, which neighbouring segments share, are ORed in (k_vlc_scan zeroed
-// every word of the picture).
+// per word), every word ORed into memory -- for the rare wave whose bits
+// exceed its LDS copy (k_vlc_blk zeroed its words first)
 struct BitWriter {
   uint64_t acc;  // the pending bits, right-aligned
   int nacc;      // how many (< 32 between appends)
   int64_t w;     // picture word the pending bits start in
-  bool first;    // that word is the segment's first (shared)
   uint32_t *out;
   __device__ __forceinline__ void start(uint32_t *o, int64_t pos) {
     out = o;
     w = pos >> 5;
     nacc = (int)(pos & 31);  // the bits before the segment, as zeros
     acc = 0;
-    first = true;
   }
   __device__ __forceinline__ void put(uint32_t v, int n) {  // n <= 32
     acc = (acc << n) | v;
     nacc += n;
     if (nacc >= 32) {
-      const uint32_t word = __builtin_bswap32((uint32_t)(acc >> (nacc - 32)));
-      if (first)
-        atomicOr(out + w, word);
-      else
-        out[w] = word;
-      first = false;
+      atomicOr(out + w, __builtin_bswap32((uint32_t)(acc >> (nacc - 32))));
       w++;
       nacc -= 32;
     }
@@ -190,8 +173,10 @@ struct BitWriter {
   }
 };
 
-// The same writer into a wave's LDS copy of its bits (words from w0 on, all
-// ORed: the copy was zeroed), written out whole afterwards
+// The same writer into a wave's LDS copy of its bits: words w0 ..
+// w0 + VLC_EMIT_WORDS - 1 of the picture (the others dropped), all ORed (the
+// copy was zeroed), stored afterwards
+constexpr int VLC_EMIT_WORDS = 256;  // LDS words of a wave's bits per pass
 struct LdsBitWriter {
   uint64_t acc;
   int nacc;
@@ -208,13 +193,14 @@ struct LdsBitWriter {
     acc = (acc << n) | v;
     nacc += n;
     if (nacc >= 32) {
-      atomicOr(buf + w, __builtin_bswap32((uint32_t)(acc >> (nacc - 32))));
+      if ((unsigned)w < (unsigned)VLC_EMIT_WORDS) atomicOr(buf + w, __builtin_bswap32((uint32_t)(acc >> (nacc - 32))));
       w++;
       nacc -= 32;
     }
   }
   __device__ __forceinline__ void finish() {
-    if (nacc > 0) atomicOr(buf + w, __builtin_bswap32((uint32_t)(acc << (32 - nacc))));
+    if (nacc > 0 && (unsigned)w < (unsigned)VLC_EMIT_WORDS)
+      atomicOr(buf + w, __builtin_bswap32((uint32_t)(acc << (32 - nacc))));
   }
 };
 
@@ -296,39 +282,65 @@ __device__ __forceinline__ void block_codes(const VlcTables &T, const L *lvs, ui
 
 // Lane-per-block entropy coding: a wave takes 10 macroblocks consecutive in
 // stream order (GOB by GOB), lane 6m + b block b of the m-th, lane b = 0 also
-// the MB header (and the GOB / picture header before MDU 0 / GOB 0).  Every
-// lane runs its own block's scan serially (no cross-lane step per code), from
-// an LDS copy of the block's levels.
-//   count (EMIT false): header and block bits into blk_bits, the MB's total
-//     into mb_bits[stream position]
-//   emit  (EMIT true):  each block's codes from its bit offset: the MB's
-//     offset (k_vlc_scan) + its header + the blocks before it.  The wave's
-//     bits are one contiguous range of the picture: assembled in LDS (ORs of
-//     the lanes' words there), then stored word per lane -- plain stores,
-//     except the range's first and last words, which the neighbouring waves
-//     share (ORed into the words k_vlc_scan zeroed).  A wave whose range
-//     exceeds its LDS copy writes straight to memory, every segment's first
-//     and last word ORed.
+// the MB header (and the GOB / picture header before MDU 0 / GOB 0), so the
+// lanes' bits follow each other in lane order.  Every lane runs its own
+// block's scan serially (no cross-lane step per code), from an LDS copy of
+// the block's levels.
+//   VLC_COUNT: the blocks' bits into blk_bits[1..6] (p64gpu_vlc_block_bits_)
+//   VLC_ONE / VLC_GIVEN: the picture's bits in one pass -- the blocks' bits
+//     counted (VLC_ONE) or read from blk_bits (VLC_GIVEN, the encoder's
+//     counts), the wave's total, its start in the picture by a decoupled
+//     look-back over the waves before it, then the codes.  A wave's bits are
+//     one contiguous range of the picture: assembled in LDS 8,192 bits at a
+//     time (ORs of the lanes' words there), then stored word per lane.  The
+//     range's first and last words are shared with the neighbouring waves:
+//     the last one is handed to the next wave through its status word
+//     ("tail"), which ORs it into its first word and stores that -- no word
+//     of the picture is written twice, nothing needs zeroing, and the only
+//     waits are on the previous wave's total and tail.
 // The levels' LDS copy is int8 (64 + 16 pad bytes per lane); H.261 levels fit
 // it.  A wave with a coded level outside -128..127 (which the reference's
 // quantiser never makes, but the ABI takes) reads the int16 levels from
 // memory instead: the codes stay the host writer's for every int16 value.
 constexpr int VLC_STAGE = 80;
-constexpr int VLC_EMIT_WORDS = 256;  // a wave's bits in LDS: up to 8,192 (10 MBs)
-template <bool EMIT>
+enum { VLC_COUNT = 0, VLC_ONE = 1, VLC_GIVEN = 2 };
+// status words, two per wave of a picture (zeroed before the launch):
+// [0] the look-back word: flag (bits 62-63: 1 = the wave's own total,
+//     2 = its end, i.e. the total of every wave up to it + the phase),
+//     bit 32 = an invalid record (own / up to it), bits 0-31 the value;
+// [1] the tail: bit 63 set once published, bits 0-31 the wave's last word
+constexpr uint64_t ST_AGG = 1ull << 62, ST_INCL = 2ull << 62, ST_BAD = 1ull << 32;
+__device__ __forceinline__ uint64_t st_load(const uint64_t *p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_store(uint64_t *p, uint64_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t st_wait(const uint64_t *p) {  // until nonzero (wave-uniform)
+  for (;;) {
+    const uint64_t v = st_load(p);
+    const uint64_t u = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(v >> 32)) << 32) |
+                       (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
+    if (u) return u;
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
+template <int MODE>
 __global__ __launch_bounds__(64 * VLC_WAVES) void k_vlc_blk(VlcArgs a, VlcTables Tg, p64k::VlcLenTab Lg) {
+  constexpr bool EMIT = MODE != VLC_COUNT, COUNT = MODE != VLC_GIVEN;
   __shared__ VlcTables T;  // per-lane table lookups from LDS, loaded once per workgroup
-  __shared__ uint32_t vlen[EMIT ? 1 : p64k::VLC_LEN_WORDS];  // the count's code lengths (vlc_count.h)
-  if (!EMIT && threadIdx.x < 64) p64k::load_vlc_len(Lg, vlen, threadIdx.x);
+  __shared__ uint32_t vlen[COUNT ? p64k::VLC_LEN_WORDS : 1];  // the count's code lengths (vlc_count.h)
+  if (COUNT && threadIdx.x < 64) p64k::load_vlc_len(Lg, vlen, threadIdx.x);
   __shared__ __align__(16) uint8_t stage[VLC_WAVES * 64 * VLC_STAGE];  // each lane's levels, scan order
   __shared__ __align__(16) uint32_t wbits[EMIT ? VLC_WAVES * VLC_EMIT_WORDS : 4];
   for (int i = threadIdx.x; i < T_N; i += 64 * VLC_WAVES) T.t[i] = Tg.t[i];
   __syncthreads();
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int fi = blockIdx.y;
-  const int mb0 = (blockIdx.x * VLC_WAVES + wv) * VLC_MBS;  // first stream position
+  const int wi = blockIdx.x * VLC_WAVES + wv;  // the wave's index in its picture
+  const int mb0 = wi * VLC_MBS;                // its first stream position
   if (mb0 >= a.nmb) return;  // whole wave (after the only barrier)
-  const uint32_t pic_bits = EMIT ? a.bits[fi] : 0u;  // (checked once the level loads are out)
+  const int nwp = (a.nmb + VLC_MBS - 1) / VLC_MBS;  // waves per picture
   const int l = min(lane, 6 * VLC_MBS - 1), b = l % 6;
   const int j = min(mb0 + l / 6, a.nmb - 1);  // stream position (tail lanes repeat the last)
   const int g = j / 33, m = j - g * 33, k = raster(a.format, g, m);
@@ -362,7 +374,7 @@ __global__ __launch_bounds__(64 * VLC_WAVES) void k_vlc_blk(VlcArgs a, VlcTables
   // whether one of them does not fit (+128 per int16 half: a byte or not)
   uint32_t m0, m1;
   nz_masks(lv, m0, m1);
-  if (!cbpt && EMIT) m0 &= ~1u;  // (the count's block_vlc_bits clears it itself)
+  if (!cbpt) m0 &= ~1u;
   if (!coded) m0 = m1 = 0;
   uint32_t wide = 0;
 #pragma unroll
@@ -382,155 +394,167 @@ __global__ __launch_bounds__(64 * VLC_WAVES) void k_vlc_blk(VlcArgs a, VlcTables
         __builtin_amdgcn_perm(lv[8 * i + 7], lv[8 * i + 6], 0x06040200u));
   const int8_t *lvs = reinterpret_cast<const int8_t *>(stl);
   const int16_t *lvg = reinterpret_cast<const int16_t *>(a.coef) + ((base + k) * 6 + b) * 64;
-  if (EMIT && pic_bits == 0xFFFFFFFFu) return;  // invalid record or no room: nothing written
-  uint32_t *out = a.out + (size_t)fi * a.out_words;
-  if (!EMIT) {
-    const Header hd = header_codes(T, r, rp, mq, m);
+  uint16_t *bk = a.blk_bits + (base + k) * 8;
+  int bb = 0;  // the block's bits (an intra block's DC included)
+  if (COUNT) {
     const uint8_t *len = reinterpret_cast<const uint8_t *>(vlen);
-    int bb = 0;  // (intra: + DC)
     if (narrow) {
       if (coded) bb = p64k::block_vlc_bits(len, lvs, m0, m1, cbpt);
     } else if (coded) {
       bb = p64k::block_vlc_bits(len, lvg, m0, m1, cbpt);
     }
-    // the MB's six lanes: header and block bits into blk_bits, the total
-    uint16_t *bk = a.blk_bits + (base + k) * 8;
-    if (act) bk[1 + b] = (uint16_t)bb;
-    if (act && b == 0) bk[0] = (uint16_t)hd.bits;
-    int tot = bb;
-#pragma unroll
-    for (int d = 1; d < 6; d++) tot += __shfl(bb, min(lane + d, 63));
-    if (act && b == 0 && a.mb_bits) a.mb_bits[base + j] = hd.bad ? 0x80000000u : (uint32_t)(hd.bits + tot);
   } else {
-    // (8-byte loads: blk_bits is 8-byte aligned, 2 nframes nmb words into scratch)
-    const uint2 *bp = reinterpret_cast<const uint2 *>(a.blk_bits + (base + k) * 8);
-    const uint2 b01 = bp[0], b23 = bp[1];
-    const uint32_t bw4[4] = {b01.x, b01.y, b23.x, b23.y};
-    const uint16_t *bh = reinterpret_cast<const uint16_t *>(bw4);
-    const int64_t off = a.mb_off[base + j];
-    int64_t pos = off + bh[0];
-#pragma unroll
-    for (int d = 0; d < 5; d++) pos += d < b ? bh[1 + d] : 0;
-    // the lane's segments: headers (b = 0) from s0: the picture header (MDU 0
-    // of GOB 0), the GOB header (MDU 0), the MB header; its block from pos
-    const int64_t s0 = j == 0 ? (a.phase ? a.phase[fi] : 0) : (m == 0 ? off - 26 : off);
-    auto emit = [&](auto &bw, uint32_t *dst) {
-      if (act && b == 0) {
-        const Header hd = header_codes(T, r, rp, mq, m);
-        bw.start(dst, s0);
-        if (j == 0) {  // WritePictureHeader marker.c:103-135
-          bw.put(0x10u, 20);
-          bw.put((uint32_t)a.tr[fi] & 31u, 5);
-          bw.put(a.format == P64S_QCIF ? 0u : 4u, 6);
-          if (a.format == P64S_NTSC) bw.put(0x18cu, 9);  // PEI 1, PSPARE 0x8c
-          bw.put(0u, 1);                                   // PEI 0
-        }
-        if (m == 0) {  // WriteGOBHeader marker.c:171-198
-          const uint32_t gn = a.format == P64S_QCIF ? 2 * g + 1 : g + 1;
-          bw.put((1u << 10) | (gn << 6) | ((a.gquant[(size_t)fi * a.ngob + g] & 31u) << 1), 26);
-        }
-#pragma unroll
-        for (int i = 0; i < 6; i++)
-          if (hd.c[i].len) bw.put(hd.c[i].v, hd.c[i].len);
-        bw.finish();
+    bb = coded ? (int)bk[1 + b] : 0;
+  }
+  if (!EMIT) {
+    if (act) bk[1 + b] = (uint16_t)bb;
+    return;
+  }
+  // the lane's bits: the headers (b = 0: picture header before MDU 0 of GOB 0,
+  // GOB header before MDU 0, the MB header), then its block
+  int hbits = 0;
+  bool hbad = false;
+  if (act && b == 0) {  // (the codes themselves again when they are written)
+    const Header hd = header_codes(T, r, rp, mq, m);
+    hbits = (j == 0 ? 32 + (a.format == P64S_NTSC ? 9 : 0) : 0) + (m == 0 ? 26 : 0) + hd.bits;
+    hbad = hd.bad;
+  }
+  const int lbits = hbits + bb;
+  const int incl = wave_incl_scan(lbits);
+  const int rel = incl - lbits;  // the lane's first bit, from the wave's first
+  const int64_t tot = (uint32_t)__builtin_amdgcn_readlane(incl, 63);
+  const bool bad = __any(hbad);
+  const uint32_t trv = (uint32_t)a.tr[fi] & 31u, gqv = a.gquant[(size_t)fi * a.ngob + g] & 31u;
+  auto emit = [&](auto &bw, uint32_t *dst, int64_t base) {
+    if (act && b == 0) {
+      const Header hd = header_codes(T, r, rp, mq, m);
+      bw.start(dst, base + rel);
+      if (j == 0) {  // WritePictureHeader marker.c:103-135
+        bw.put(0x10u, 20);
+        bw.put(trv, 5);
+        bw.put(a.format == P64S_QCIF ? 0u : 4u, 6);
+        if (a.format == P64S_NTSC) bw.put(0x18cu, 9);  // PEI 1, PSPARE 0x8c
+        bw.put(0u, 1);                                   // PEI 0
       }
-      if (coded) {
-        bw.start(dst, pos);
-        if (!cbpt) {  // EncodeDC codec.c:343-352
-          const int dc0 = (int)(int16_t)(lv[0] & 0xffffu);
-          const int dc = dc0 < 1 ? 1 : (dc0 > 254 ? 254 : dc0);
-          bw.put((uint32_t)(dc == 128 ? 255 : dc), 8);
-        }
-        if (narrow)
-          block_codes(T, lvs, m0, m1, cbpt, bw);
-        else
-          block_codes(T, lvg, m0, m1, cbpt, bw);
-        bw.finish();
+      if (m == 0) {  // WriteGOBHeader marker.c:171-198
+        const uint32_t gn = a.format == P64S_QCIF ? 2 * g + 1 : g + 1;
+        bw.put((1u << 10) | (gn << 6) | (gqv << 1), 26);
       }
-    };
-    // the wave's range [first, first + span): lane 0 holds the first segment
-    const int64_t first = ((int64_t)__builtin_amdgcn_readfirstlane((int)(s0 >> 32)) << 32) |
-                          (uint32_t)__builtin_amdgcn_readfirstlane((int)s0);
-    const int end = act ? (int)(pos + (coded ? bh[1 + b] : 0) - first) : 0;
-    const int span = wave_max_i(end);
-    const int64_t w0 = first >> 5;
-    const int nw = span > 0 ? (int)(((first + span - 1) >> 5) - w0 + 1) : 0;
-    if (nw <= VLC_EMIT_WORDS) {
-      uint32_t *wb = wbits + wv * VLC_EMIT_WORDS;
-      reinterpret_cast<uint4 *>(wb)[lane] = make_uint4(0, 0, 0, 0);
-      wave_lds_sync();
-      LdsBitWriter bw;
-      bw.w0 = w0;
-      emit(bw, wb);
-      wave_lds_sync();
 #pragma unroll
-      for (int i = 0; i < VLC_EMIT_WORDS / 64; i++) {
-        const int t = lane + 64 * i;
-        if (t < nw) {
-          const uint32_t v = wb[t];
-          if (t == 0 || t == nw - 1) {
-            if (v) atomicOr(out + w0 + t, v);
-          } else {
-            out[w0 + t] = v;
-          }
-        }
+      for (int i = 0; i < 6; i++)
+        if (hd.c[i].len) bw.put(hd.c[i].v, hd.c[i].len);
+      bw.finish();
+    }
+    if (coded) {
+      bw.start(dst, base + rel + hbits);
+      if (!cbpt) {  // EncodeDC codec.c:343-352
+        const int dc0 = (int)(int16_t)(lv[0] & 0xffffu);
+        const int dc = dc0 < 1 ? 1 : (dc0 > 254 ? 254 : dc0);
+        bw.put((uint32_t)(dc == 128 ? 255 : dc), 8);
       }
-    } else {
-      BitWriter bw;
-      emit(bw, out);
+      if (narrow)
+        block_codes(T, lvs, m0, m1, cbpt, bw);
+      else
+        block_codes(T, lvg, m0, m1, cbpt, bw);
+      bw.finish();
+    }
+  };
+  // the wave's own total out first; the look-back's first read in flight
+  // while the codes go into LDS at positions from the wave's start (word
+  // aligned; shifted to the start's bit phase when stored)
+  uint64_t *stw = reinterpret_cast<uint64_t *>(a.status) + (size_t)fi * nwp * 2;
+  if (wi > 0 && lane == 0) st_store(stw + 2 * wi, ST_AGG | (bad ? ST_BAD : 0) | (uint64_t)tot);
+  uint64_t s = wi > 0 && wi - 1 - lane >= 0 ? st_load(stw + 2 * (wi - 1 - lane)) : ST_INCL;
+  const bool in_lds = tot <= 32 * VLC_EMIT_WORDS - 32;  // whatever the phase
+  const int nwr = (int)((tot + 31) >> 5);                // words of the aligned copy
+  uint32_t *wb = wbits + wv * VLC_EMIT_WORDS;
+  if (in_lds && tot > 0) {
+    reinterpret_cast<uint4 *>(wb)[lane] = make_uint4(0, 0, 0, 0);
+    wave_lds_sync();
+    LdsBitWriter bw;
+    bw.w0 = 0;
+    emit(bw, wb, 0);
+    wave_lds_sync();
+  }
+  // the wave's start: the phase for the first wave, else the end of the
+  // previous one -- 64 waves at a time, lane i reading wave v - i: the nearest
+  // published end and every wave's own total after it (else read again)
+  int64_t first;
+  bool bad_all = bad;
+  if (wi == 0) {
+    first = a.phase ? a.phase[fi] : 0;
+  } else {
+    first = 0;
+    for (int v = wi - 1;;) {
+      const uint64_t inc = __ballot((s >> 62) == 2), zero = __ballot(s == 0);
+      const int p = inc ? (int)__builtin_ctzll(inc) : 64;  // the nearest end
+      const uint64_t need = p == 64 ? ~0ull : (2ull << p) - 1;
+      if (!(zero & need)) {
+        const bool use = lane <= p;
+        first += wave_sum_i(use ? (int)(uint32_t)s : 0);
+        bad_all |= __any(use && (s & ST_BAD));
+        if (p < 64) break;
+        v -= 64;
+      } else {
+        __builtin_amdgcn_s_sleep(1);
+      }
+      s = v - lane >= 0 ? st_load(stw + 2 * (v - lane)) : ST_INCL;
     }
   }
-}
-
-// With the blocks' bits given (the encoder counted them, p64gpu_encode_args.
-// vlc_bits): one lane per macroblock adds its header bits (WriteMBHeader
-// marker.c:288, the MVD predictor from the previous MB of its GOB row) to
-// them, keeps the header bits in slot 0 for the emit pass and writes the
-// MB's total into mb_bits[stream position] -- the count pass without the
-// level reads.
-__global__ __launch_bounds__(256) void k_vlc_hdr(VlcArgs a, VlcTables T) {
-  const int fi = blockIdx.y, k = blockIdx.x * 256 + threadIdx.x;
-  if (k >= a.nmb) return;
-  const size_t base = (size_t)fi * a.nmb;
-  const p64_mb_rec r = a.mb[base + k];
-  const int j = stream_pos(a.format, k), g = j / 33, m = j - g * 33;
-  const p64_mb_rec rp = a.mb[base + (m % 11 ? k - 1 : k)];
-  const int mq = a.mquant ? (int)a.mquant[base + k] : 0;
-  const Header hd = header_codes(T, r, rp, mq, m);
-  uint16_t *bk = a.blk_bits + (base + k) * 8;
-  const uint4 q = *reinterpret_cast<const uint4 *>(bk);  // slots 0..7 (16-byte aligned)
-  const uint32_t s2 = (q.x >> 16) + (q.y & 0xffffu) + (q.y >> 16) + (q.z & 0xffffu) + (q.z >> 16) + (q.w & 0xffffu);
-  bk[0] = (uint16_t)hd.bits;
-  a.mb_bits[base + j] = hd.bad ? 0x80000000u : (uint32_t)hd.bits + s2;
-}
-
-// stream-order offsets per picture (one wave per picture: each lane sums a
-// run of MBs, a wave scan combines them); bits[fi] = total incl. the phase,
-// or 0xFFFFFFFF if a record was invalid.  Zeroes the words the picture uses.
-__global__ __launch_bounds__(64) void k_vlc_scan(VlcArgs a) {
-  const int fi = blockIdx.x, lane = threadIdx.x;
-  const size_t base = (size_t)fi * a.nmb;
-  const int per = (a.nmb + 63) / 64, j0 = lane * per, j1 = min(j0 + per, a.nmb);
-  int sum = 0, bad = 0;
-  for (int j = j0; j < j1; j++) {
-    const uint32_t b = a.mb_bits[base + j];
-    bad |= (b >> 31) & 1;
-    sum += (int)(b & 0x7fffffffu) + (j % 33 == 0 ? 26 : 0);  // GOB header before MDU 0
+  const int64_t endb = first + tot;
+  if (lane == 0) st_store(stw + 2 * wi, ST_INCL | (bad_all ? ST_BAD : 0) | (uint64_t)(uint32_t)endb);
+  const bool last_wave = wi == nwp - 1;
+  const bool fits = endb + 64 <= a.out_words * 32;
+  if (last_wave && lane == 0) a.bits[fi] = (bad_all || !fits) ? 0xFFFFFFFFu : (uint32_t)endb;
+  if (!fits) return;  // (nor does any later wave of the picture: nothing written)
+  uint32_t *out = a.out + (size_t)fi * a.out_words;
+  // the words [w0, wl]; the first is shared with the previous wave unless the
+  // range starts on a word boundary (or is the picture's start), the last
+  // with the next unless it ends on one (or is the picture's end)
+  const int64_t w0 = first >> 5, wl = (endb - 1) >> 5;
+  const bool sh_first = wi > 0 && (first & 31) != 0;
+  const bool sh_last = !last_wave && (endb & 31) != 0;
+  uint32_t firstv = 0, lastv = 0;
+  if (in_lds && tot > 0) {  // (the common case) the copy shifted by the phase, word per lane
+    const int sh = (int)(first & 31), nw = (int)(wl - w0 + 1);
+    auto word = [&](int t) {  // word t of the range (big-endian bytes, as stored)
+      const uint32_t cur = t < nwr ? __builtin_bswap32(wb[t]) : 0u;
+      const uint32_t prev = t > 0 ? __builtin_bswap32(wb[t - 1]) : 0u;
+      return __builtin_bswap32(sh ? (cur >> sh) | (prev << (32 - sh)) : cur);
+    };
+    firstv = word(0);
+    lastv = word(nw - 1);
+#pragma unroll
+    for (int i = 0; i < VLC_EMIT_WORDS / 64; i++) {
+      const int t = lane + 64 * i;
+      if (t < nw && !(t == 0 && sh_first) && !(t == nw - 1 && sh_last)) out[w0 + t] = word(t);
+    }
+  } else if (tot > 0) {  // more bits than the copy holds: zero the words, OR the codes in memory
+    for (int64_t gw = w0 + lane; gw <= wl; gw += 64) out[gw] = 0;
+    __threadfence();
+    BitWriter bw;
+    emit(bw, out, first);
+    __threadfence();
+    firstv = (uint32_t)__builtin_amdgcn_readfirstlane((int)__hip_atomic_load(out + w0, __ATOMIC_RELAXED,
+                                                                              __HIP_MEMORY_SCOPE_AGENT));
+    lastv = (uint32_t)__builtin_amdgcn_readfirstlane((int)__hip_atomic_load(out + wl, __ATOMIC_RELAXED,
+                                                                             __HIP_MEMORY_SCOPE_AGENT));
   }
-  const int head = (a.phase ? a.phase[fi] : 0) + 32 + (a.format == P64S_NTSC ? 9 : 0);
-  int64_t off = head + wave_excl_scan(sum, lane);
-  for (int j = j0; j < j1; j++) {
-    if (j % 33 == 0) off += 26;
-    a.mb_off[base + j] = (uint32_t)off;
-    off += a.mb_bits[base + j] & 0x7fffffffu;
-  }
-  const int64_t total = __shfl(off, 63);
-  bad = __any(bad);
-  const bool fits = total + 64 <= a.out_words * 32;
-  if (lane == 0) a.bits[fi] = (bad || !fits) ? 0xFFFFFFFFu : (uint32_t)total;
-  if (fits) {
-    uint32_t *out = a.out + (size_t)fi * a.out_words;
-    for (int64_t w = lane; w <= (total >> 5) + 1; w += 64) out[w] = 0;
+  // the shared words: hand the last one on, then take the previous wave's
+  if (tot == 0 || w0 == wl) {  // (one word: the previous wave's tail and ours)
+    uint32_t v = tot > 0 ? firstv : 0u;
+    if (sh_first) v |= (uint32_t)st_wait(stw + 2 * (wi - 1) + 1);
+    if (sh_last) {
+      if (lane == 0) st_store(stw + 2 * wi + 1, (1ull << 63) | v);
+    } else if ((tot > 0 || sh_first) && lane == 0) {
+      out[w0] = v;
+    }
+  } else {
+    if (sh_last && lane == 0) st_store(stw + 2 * wi + 1, (1ull << 63) | lastv);
+    if (sh_first) {
+      const uint32_t pv = (uint32_t)st_wait(stw + 2 * (wi - 1) + 1);
+      if (lane == 0) out[w0] = firstv | pv;
+    }
   }
 }
 
@@ -600,18 +624,18 @@ int p64gpu_vlc_pictures(const p64gpu_vlc_args *x, void *stream) {
     a.bits = x->bits + f0;
     // this chunk's [6][nc][nmb] words of the scratch
     uint32_t *scr = x->scratch + 6 * m0;
-    a.mb_bits = scr;
-    a.mb_off = scr + (size_t)nc * nmb;
-    const dim3 grid((unsigned)((nmb + VLC_WAVES * VLC_MBS - 1) / (VLC_WAVES * VLC_MBS)), (unsigned)nc);
-    if (x->blk_bits) {  // the blocks' bits from the encoder: headers and totals only
+    a.status = scr;  // 4 words per wave of a picture (<= 2 nmb)
+    const int nwp = (nmb + VLC_MBS - 1) / VLC_MBS;
+    const dim3 grid((unsigned)((nwp + VLC_WAVES - 1) / VLC_WAVES), (unsigned)nc);
+    hipError_t me = hipMemsetAsync(scr, 0, (size_t)nc * nwp * 16, st);
+    if (me != hipSuccess) return p64gpu_fail_(P64GPU_E_HIP, hipGetErrorString(me));
+    if (x->blk_bits) {  // the blocks' bits from the encoder: no count
       a.blk_bits = x->blk_bits + m0 * 8;
-      hipLaunchKernelGGL(k_vlc_hdr, dim3((unsigned)((nmb + 255) / 256), (unsigned)nc), dim3(256), 0, st, a, g_tab);
+      hipLaunchKernelGGL(k_vlc_blk<VLC_GIVEN>, grid, dim3(64 * VLC_WAVES), 0, st, a, g_tab, g_len);
     } else {
-      a.blk_bits = reinterpret_cast<uint16_t *>(scr + 2 * (size_t)nc * nmb);
-      hipLaunchKernelGGL(k_vlc_blk<false>, grid, dim3(64 * VLC_WAVES), 0, st, a, g_tab, g_len);
+      a.blk_bits = nullptr;
+      hipLaunchKernelGGL(k_vlc_blk<VLC_ONE>, grid, dim3(64 * VLC_WAVES), 0, st, a, g_tab, g_len);
     }
-    hipLaunchKernelGGL(k_vlc_scan, dim3((unsigned)nc), dim3(64), 0, st, a);
-    hipLaunchKernelGGL(k_vlc_blk<true>, grid, dim3(64 * VLC_WAVES), 0, st, a, g_tab, g_len);
   }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return p64gpu_fail_(P64GPU_E_HIP, hipGetErrorString(e));
@@ -669,7 +693,7 @@ int p64gpu_vlc_block_bits_(int width, int height, int nframes, const p64_mb_rec 
     a.coef = coef + m0 * 384;
     a.blk_bits = blk_bits + m0 * 8;
     const dim3 grid((unsigned)((nmb + VLC_WAVES * VLC_MBS - 1) / (VLC_WAVES * VLC_MBS)), (unsigned)nc);
-    hipLaunchKernelGGL(k_vlc_blk<false>, grid, dim3(64 * VLC_WAVES), 0, (hipStream_t)stream, a, g_tab, lt);
+    hipLaunchKernelGGL(k_vlc_blk<VLC_COUNT>, grid, dim3(64 * VLC_WAVES), 0, (hipStream_t)stream, a, g_tab, lt);
   }
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? P64GPU_OK : p64gpu_fail_(P64GPU_E_HIP, hipGetErrorString(e));

@@ -328,3 +328,49 @@ def test_gpu_vlc_levels_outside_int8(p64, torch_dev, name):
         nb = (bits[t] + 7) // 8
         gpu = int.from_bytes(out[t, :nb].tobytes(), "big") >> (nb * 8 - bits[t])
         assert gpu >> (bits[t] - 8 * len(full)) == int.from_bytes(full, "big"), f"{name} picture {t}"
+
+
+@pytest.mark.parametrize("given", [False, True])
+def test_gpu_vlc_invalid_records(p64, torch_dev, given):
+    """An invalid MB record (MTYPE outside 0..9, or a CBP type with CBP 0)
+    makes its picture's bit count 0xFFFFFFFF (vlc_pictures raises), and only
+    its picture's: the others of the launch equal the host writer.  A picture
+    of nothing but invalid records has waves without a single bit, whose
+    look-back and shared-word hand-over (p64vlc.hip) must still complete."""
+    from p64_amd import stream
+    torch = torch_dev
+    z = load("seq_qcif_full31.npz")
+    mb, coef, gq, uq = fixture_records(z, stream.format_of(176, 144))
+    sel = [1, 2, 3, 4, 5]
+    mb, coef, gq, uq = mb[sel].copy(), coef[sel], gq[sel], uq[sel]
+    mb[1, :, 0] = 12               # every record invalid
+    mb[2, 50, 0] = 10              # one
+    cbpt = np.isin(mb[3, :, 0], [2, 3, 5, 6, 8, 9])
+    k = int(np.flatnonzero(cbpt)[0])
+    mb[3, k, 1] = 0                # a CBP type without a coded block
+    d = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()  # noqa: E731
+    tr = np.arange(len(sel), dtype=np.int32)
+    kw = {}
+    if given:  # the block bits from the coder's own count of the same records
+        vb = torch.zeros((len(sel), 99, 8), dtype=torch.int16, device="cuda")
+        assert p64.lib().p64gpu_vlc_block_bits_(176, 144, len(sel), ctypes_ptr(d(mb)), ctypes_ptr(d(coef)),
+                                                ctypes_ptr(vb), None) == 0
+        kw["blk_bits"] = vb
+    out, bits = stream.vlc_pictures(d(mb), d(coef), d(gq), d(tr), width=176, height=144, mquant=d(uq),
+                                    host_bits=False, **kw)
+    bits = [int(x) & 0xFFFFFFFF for x in bits.cpu().tolist()]
+    assert bits[1] == bits[2] == bits[3] == 0xFFFFFFFF
+    out = out.cpu().numpy()
+    for t in (0, 4):
+        wr = stream.Writer(stream.QCIF)
+        wr.write_picture(int(tr[t]), mb[t], coef[t], gq[t], quant_mb=uq[t])
+        assert bits[t] == wr.bits()
+        full = wr.data()
+        nb = (bits[t] + 7) // 8
+        gpu = int.from_bytes(out[t, :nb].tobytes(), "big") >> (nb * 8 - bits[t])
+        assert gpu >> (bits[t] - 8 * len(full)) == int.from_bytes(full, "big")
+
+
+def ctypes_ptr(t):
+    import ctypes
+    return ctypes.c_void_p(t.data_ptr())

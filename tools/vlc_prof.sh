@@ -15,6 +15,6 @@ for lib in "$@"; do
 import csv,sys
 for r in csv.DictReader(sys.stdin):
     n=r['Name'].replace('(anonymous namespace)::','').split('(')[0]
-    if 'vlc' in n: print(f\"$tag $c {n:22s} calls {int(r['Calls']):4d} avg {float(r['AverageNs'])/1e3:8.1f} us\")"
+    if 'vlc' in n or 'rocclr_fill' in n: print(f\"$tag $c {n:22s} calls {int(r['Calls']):4d} avg {float(r['AverageNs'])/1e3:8.1f} us\")"
   done
 done
