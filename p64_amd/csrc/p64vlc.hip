@@ -317,6 +317,9 @@ __device__ __forceinline__ void st_store(uint64_t *p, uint64_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 __device__ __forceinline__ uint64_t st_wait(const uint64_t *p) {  // until nonzero (wave-uniform)
+#if defined(VLC_PROBE) && (VLC_PROBE & 2)
+  return 1;
+#endif
   for (;;) {
     const uint64_t v = st_load(p);
     const uint64_t u = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(v >> 32)) << 32) |
@@ -481,8 +484,13 @@ __global__ __launch_bounds__(64 * VLC_WAVES) void k_vlc_blk(VlcArgs a, VlcTables
   // published end and every wave's own total after it (else read again)
   int64_t first;
   bool bad_all = bad;
+#if defined(VLC_PROBE) && (VLC_PROBE & 1)
+  if (true) {
+    first = 0;
+#else
   if (wi == 0) {
     first = a.phase ? a.phase[fi] : 0;
+#endif
   } else {
     first = 0;
     for (int v = wi - 1;;) {
