@@ -895,6 +895,9 @@ def main(argv=None):
         with_vlc = None
         if not args.no_vlc:
             with_vlc = measure_vlc(args, torch, p64_amd, step, out_of, S, nmb, w, h)
+        other = None
+        if keep and args.content == "survey" and args.config == "inter":
+            other = measure_content(args, torch, dist, world, p64_amd, "synth", S, seed0, nslots, mode)
 
         mbs_launch = S * nmb
         value = aggregate_rate(world, mbs_launch, args.steps, tmax)
@@ -968,6 +971,7 @@ def main(argv=None):
             "valu_busy_note": VALU_BUSY_NOTE,
             "steady_state": clk,
             "with_vlc": with_vlc,
+            **({"other_content": other} if other else {}),
             "verified_vs_oracle": verified,
         }
         if extra:
@@ -1105,18 +1109,19 @@ def measure_vlc(args, torch, p64_amd, step, out_of, S, nmb, w, h):
     """The encode steps followed by entropy coding on the device (p64vlc.hip):
     the whole-encoder rate to .p64 bits, measured after the metric (it re-runs
     steps, so the closed-loop state is not reused).  Per step: the encode
-    launches -- which also count every transmitted block's coded bits
-    (vlc_bits) -- the entropy coder's header/offset and emit launches from
-    those counts (no count pass over the levels), and a copy of every
+    launches, the entropy coder's launch (counting the blocks' bits itself, or
+    taking the encoder's counts: both measured), and a copy of every
     picture's bit count to pinned host memory; the steps captured in one HIP
-    graph (as the metric's steps are) and replayed once, wall-clock timed."""
+    graph (as the metric's steps are) and replayed once, wall-clock timed.
+    (The copies on a forked side stream, joined at the end, measured slower:
+    0.267 against 0.245 ms per step.)"""
     try:
         from p64_amd import stream as p64s
         ngob = nmb // 33
         gq = torch.full((S, ngob), args.quant, dtype=torch.uint8, device="cuda")
         bufs = p64s.vlc_buffers(S, w, h)
-        vb = torch.empty((S, nmb, 8), dtype=torch.int16, device="cuda")  # the encoder's block bits
         vsteps = min(args.steps, 8)
+        vb = torch.empty((S, nmb, 8), dtype=torch.int16, device="cuda")  # the encoder's block bits
         trs = [torch.full((S,), (1 + args.warmup + k) % 32, dtype=torch.int32, device="cuda")
                for k in range(vsteps)]
         host = torch.empty((vsteps, S), dtype=torch.int32, pin_memory=True)
@@ -1132,7 +1137,8 @@ def measure_vlc(args, torch, p64_amd, step, out_of, S, nmb, w, h):
             o = out_of(t)
             if ev:
                 vlc_ev[0].record()
-            _, bits_dev[k] = p64s.vlc_pictures(o.mb, o.coef, gq, trs[k], width=w, height=h, buffers=bufs,
+            _, bits_dev[k] = p64s.vlc_pictures(o.mb, o.coef, gq, trs[k], width=w, height=h,
+                                               buffers=bufs,
                                                host_bits=False, blk_bits=vb if given else None)
             if ev:
                 vlc_ev[1].record()
@@ -1177,6 +1183,54 @@ def measure_vlc(args, torch, p64_amd, step, out_of, S, nmb, w, h):
         return res
     except Exception as e:  # never let the extra measurement cost the bench line
         return {"error": str(e)[:200]}
+
+
+def measure_content(args, torch, dist, world, p64_amd, content, S, seed0, nslots, mode):
+    """The same inter steps on another content (the secondary line: round 4's
+    headline content `synth`), timed the same way, for comparison across
+    rounds; not part of `value`."""
+    try:
+        w, h = args.width, args.height
+        nmb, pic = (w // 16) * (h // 16), w * h * 3 // 2
+        frames = make_inputs(torch, p64_amd, content, w, h, seed0, S, nslots)
+        rec = [torch.zeros(S * pic, dtype=torch.uint8, device="cuda") for _ in range(2)]
+        li = torch.zeros(S * nmb, dtype=torch.uint8, device="cuda")
+
+        def outs():
+            return p64_amd.FrameBatchOut(coef=torch.empty((S, nmb, 6, 64), dtype=torch.int16, device="cuda"),
+                                         mb=torch.empty((S, nmb, 4), dtype=torch.int8, device="cuda"),
+                                         me=torch.empty((S, nmb, 7), dtype=torch.int32, device="cuda"),
+                                         nz=torch.empty((S, nmb), dtype=torch.uint8, device="cuda"))
+        out = outs()
+
+        def launch(t, r=rec, l=li, o=out):
+            p64_amd.encode_frames(frames[t % nslots].reshape(-1), r[(t + 1) % 2], r[t % 2], l, width=w,
+                                  height=h, intra=(t == 0), quant=args.quant, me_mode=mode,
+                                  search_limit=args.search_limit, out=o)
+        for t in range(1 + args.warmup):
+            launch(t)
+        sp = {}
+
+        def spin_init():
+            sp["rec"], sp["li"], sp["out"] = [torch.empty_like(r) for r in rec], torch.empty_like(li), outs()
+
+        def spin_reset():
+            for a, b in zip(sp["rec"], rec):
+                a.copy_(b)
+            sp["li"].copy_(li)
+
+        elapsed, _, clk = timed_region(torch, dist, world, args.steps, 1 + args.warmup, launch,
+                                       graph=not args.eager, spinup_ms=args.spinup_ms,
+                                       spin={"init": spin_init, "reset": spin_reset,
+                                             "launch": lambda t: launch(t, sp["rec"], sp["li"], sp["out"])})
+        tmax = max_over_ranks(elapsed, world, device="cuda")
+        return {"content": content, "value": round(aggregate_rate(world, S * nmb, args.steps, tmax), 1),
+                "ms_per_step": round(tmax / args.steps * 1e3, 4),
+                "clock_mhz_after": clk.get("clock_mhz_after"),
+                "note": "the same inter steps (closed loop, K steps in one graph) on this content; "
+                        "round 4's headline content was synth"}
+    except Exception as e:  # never let the extra measurement cost the bench line
+        return {"content": content, "error": str(e)[:200]}
 
 
 def run_intra(args, torch, dist, np, p64_amd, world, frames, S, nmb, pic, nslots):

@@ -393,38 +393,6 @@ __device__ __forceinline__ unsigned finish_groups(const Sx &S, int n, int lane) 
   return wave_min(bk);
 }
 
-// full SADs of the listed candidates (keys with the ord in the low bits), one
-// per lane; returns the least key
-template <class G>
-__device__ __forceinline__ unsigned finish_list(const Sx &S, int n, int lane) {
-  unsigned bk = 0xFFFFFFFFu;
-  for (int c0 = 0; c0 < n; c0 += 64) {
-    if (c0 + lane < n) {
-      const unsigned ord = S.list[c0 + lane] & KEY_ORD;
-      int cdx, cdy;
-      ord_pos(ord, cdx, cdy);
-      const int cb = WIN_OX + cdx, csh = cb & 3;
-      const lds_u32 *p0 = lds_base(S.win + (WIN_OY + cdy) * G::WS + (cb >> 2));
-      uint32_t a = 0;
-#pragma unroll
-      for (int r = 0; r < 16; r++) {
-        const lds_u32 *p = p0 + r * G::WS;
-        const uint32_t a0 = p[0], a1 = p[1], a2 = p[2], a3 = p[3], a4 = p[4];
-        // LDS broadcast, re-read per chunk (opaque index: not hoisted out of
-        // the loop into live registers)
-        const uint4 c = reinterpret_cast<const uint4 *>(S.cur)[opaque(r)];
-        a = sad4(align4(a1, a0, csh), c.x, a);
-        a = sad4(align4(a2, a1, csh), c.y, a);
-        a = sad4(align4(a3, a2, csh), c.z, a);
-        a = sad4(align4(a4, a3, csh), c.w, a);
-      }
-      bk = min(bk, (a << KEY_SHIFT) | ord);
-    }
-  }
-  return wave_min(bk);
-}
-
-
 // Two-stage finishing of many survivors (more than 8; SURVEY.md 8(d)'s
 // content leaves ~46 at the median, smooth texture under N(0,4) noise): the
 // first stage computes, one candidate per lane, the exact SAD of rows 0..7
