@@ -289,26 +289,29 @@ __device__ __forceinline__ void block_codes(const VlcTables &T, const L *lvs, ui
 //   VLC_COUNT: the blocks' bits into blk_bits[1..6] (p64gpu_vlc_block_bits_)
 //   VLC_ONE / VLC_GIVEN: the picture's bits in one pass -- the blocks' bits
 //     counted (VLC_ONE) or read from blk_bits (VLC_GIVEN, the encoder's
-//     counts), the wave's total, its start in the picture by a decoupled
-//     look-back over the waves before it, then the codes.  A wave's bits are
-//     one contiguous range of the picture: assembled in LDS 8,192 bits at a
-//     time (ORs of the lanes' words there), then stored word per lane.  The
-//     range's first and last words are shared with the neighbouring waves:
-//     the last one is handed to the next wave through its status word
-//     ("tail"), which ORs it into its first word and stores that -- no word
-//     of the picture is written twice, nothing needs zeroing, and the only
-//     waits are on the previous wave's total and tail.
+//     counts), the workgroup's total (four waves: 40 MBs, one contiguous
+//     range of the picture), its start by a decoupled look-back over the
+//     workgroups before it, then the codes.  Each wave writes its codes into
+//     an LDS copy (ORs of the lanes' words) while wave 0's look-back reads
+//     are in flight; the copies are then stored word per thread, shifted to
+//     the waves' starts and ORed together where two waves share a word.  The
+//     range's first and last words are shared with the neighbouring
+//     workgroups: the last one is handed to the next workgroup through its
+//     status word ("tail"), which ORs it into its first word and stores that
+//     -- no word of the picture is written twice, nothing needs zeroing, and
+//     the only waits are on earlier workgroups' totals and the previous one's
+//     tail.
 // The levels' LDS copy is int8 (64 + 16 pad bytes per lane); H.261 levels fit
 // it.  A wave with a coded level outside -128..127 (which the reference's
 // quantiser never makes, but the ABI takes) reads the int16 levels from
 // memory instead: the codes stay the host writer's for every int16 value.
 constexpr int VLC_STAGE = 80;
 enum { VLC_COUNT = 0, VLC_ONE = 1, VLC_GIVEN = 2 };
-// status words, two per wave of a picture (zeroed before the launch):
-// [0] the look-back word: flag (bits 62-63: 1 = the wave's own total,
-//     2 = its end, i.e. the total of every wave up to it + the phase),
+// status words, two per workgroup of a picture (zeroed before the launch):
+// [0] the look-back word: flag (bits 62-63: 1 = the workgroup's own total,
+//     2 = its end, i.e. the total of every workgroup up to it + the phase),
 //     bit 32 = an invalid record (own / up to it), bits 0-31 the value;
-// [1] the tail: bit 63 set once published, bits 0-31 the wave's last word
+// [1] the tail: bit 63 set once published, bits 0-31 the range's last word
 constexpr uint64_t ST_AGG = 1ull << 62, ST_INCL = 2ull << 62, ST_BAD = 1ull << 32;
 __device__ __forceinline__ uint64_t st_load(const uint64_t *p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -317,9 +320,6 @@ __device__ __forceinline__ void st_store(uint64_t *p, uint64_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 __device__ __forceinline__ uint64_t st_wait(const uint64_t *p) {  // until nonzero (wave-uniform)
-#if defined(VLC_PROBE) && (VLC_PROBE & 2)
-  return 1;
-#endif
   for (;;) {
     const uint64_t v = st_load(p);
     const uint64_t u = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(v >> 32)) << 32) |
@@ -342,8 +342,7 @@ __global__ __launch_bounds__(64 * VLC_WAVES) void k_vlc_blk(VlcArgs a, VlcTables
   const int fi = blockIdx.y;
   const int wi = blockIdx.x * VLC_WAVES + wv;  // the wave's index in its picture
   const int mb0 = wi * VLC_MBS;                // its first stream position
-  if (mb0 >= a.nmb) return;  // whole wave (after the only barrier)
-  const int nwp = (a.nmb + VLC_MBS - 1) / VLC_MBS;  // waves per picture
+  if (!EMIT && mb0 >= a.nmb) return;  // whole wave (the coder's keep to the barriers: no bits)
   const int l = min(lane, 6 * VLC_MBS - 1), b = l % 6;
   const int j = min(mb0 + l / 6, a.nmb - 1);  // stream position (tail lanes repeat the last)
   const int g = j / 33, m = j - g * 33, k = raster(a.format, g, m);
@@ -425,7 +424,7 @@ __global__ __launch_bounds__(64 * VLC_WAVES) void k_vlc_blk(VlcArgs a, VlcTables
   const int lbits = hbits + bb;
   const int incl = wave_incl_scan(lbits);
   const int rel = incl - lbits;  // the lane's first bit, from the wave's first
-  const int64_t tot = (uint32_t)__builtin_amdgcn_readlane(incl, 63);
+  const int tot = __builtin_amdgcn_readlane(incl, 63);
   const bool bad = __any(hbad);
   const uint32_t trv = (uint32_t)a.tr[fi] & 31u, gqv = a.gquant[(size_t)fi * a.ngob + g] & 31u;
   auto emit = [&](auto &bw, uint32_t *dst, int64_t base) {
@@ -462,105 +461,142 @@ __global__ __launch_bounds__(64 * VLC_WAVES) void k_vlc_blk(VlcArgs a, VlcTables
       bw.finish();
     }
   };
-  // the wave's own total out first; the look-back's first read in flight
-  // while the codes go into LDS at positions from the wave's start (word
-  // aligned; shifted to the start's bit phase when stored)
-  uint64_t *stw = reinterpret_cast<uint64_t *>(a.status) + (size_t)fi * nwp * 2;
-  if (wi > 0 && lane == 0) st_store(stw + 2 * wi, ST_AGG | (bad ? ST_BAD : 0) | (uint64_t)tot);
-  uint64_t s = wi > 0 && wi - 1 - lane >= 0 ? st_load(stw + 2 * (wi - 1 - lane)) : ST_INCL;
-  const bool in_lds = tot <= 32 * VLC_EMIT_WORDS - 32;  // whatever the phase
-  const int nwr = (int)((tot + 31) >> 5);                // words of the aligned copy
+  // The workgroup's four waves are one contiguous range of the picture: its
+  // total and invalid flag from the waves' (LDS), then wave 0 publishes the
+  // total and issues the look-back's first read while every wave writes its
+  // codes into its LDS copy at positions from its own start (word aligned)
+  __shared__ int s_tot[VLC_WAVES], s_bad[VLC_WAVES];
+  __shared__ int64_t s_first;
+  if (lane == 0) {
+    s_tot[wv] = tot;
+    s_bad[wv] = bad;
+  }
+  __syncthreads();
+  int wt = 0, off[VLC_WAVES];
+  bool wbad = false, big = false;
+#pragma unroll
+  for (int v = 0; v < VLC_WAVES; v++) {
+    off[v] = wt;
+    wt += s_tot[v];
+    wbad |= s_bad[v] != 0;
+    big |= s_tot[v] > 32 * VLC_EMIT_WORDS - 32;  // (a copy holds 8,160 bits at any phase)
+  }
+  const int G = blockIdx.x, ng = gridDim.x;  // the workgroup's index in its picture, their number
+  uint64_t *stw = reinterpret_cast<uint64_t *>(a.status) + (size_t)fi * ng * 2;
+  uint64_t s = ST_INCL;
+  if (wv == 0 && G > 0) {
+    if (lane == 0) st_store(stw + 2 * G, ST_AGG | (wbad ? ST_BAD : 0) | (uint64_t)(uint32_t)wt);
+    if (G - 1 - lane >= 0) s = st_load(stw + 2 * (G - 1 - lane));
+  }
   uint32_t *wb = wbits + wv * VLC_EMIT_WORDS;
-  if (in_lds && tot > 0) {
+  if (!big) {
     reinterpret_cast<uint4 *>(wb)[lane] = make_uint4(0, 0, 0, 0);
     wave_lds_sync();
-    LdsBitWriter bw;
-    bw.w0 = 0;
-    emit(bw, wb, 0);
-    wave_lds_sync();
+    if (tot > 0) {
+      LdsBitWriter bw;
+      bw.w0 = 0;
+      emit(bw, wb, 0);
+    }
   }
-  // the wave's start: the phase for the first wave, else the end of the
-  // previous one -- 64 waves at a time, lane i reading wave v - i: the nearest
-  // published end and every wave's own total after it (else read again)
-  int64_t first;
-  bool bad_all = bad;
-#if defined(VLC_PROBE) && (VLC_PROBE & 1)
-  if (true) {
-    first = 0;
-#else
-  if (wi == 0) {
-    first = a.phase ? a.phase[fi] : 0;
-#endif
-  } else {
-    first = 0;
-    for (int v = wi - 1;;) {
-      const uint64_t inc = __ballot((s >> 62) == 2), zero = __ballot(s == 0);
-      const int p = inc ? (int)__builtin_ctzll(inc) : 64;  // the nearest end
-      const uint64_t need = p == 64 ? ~0ull : (2ull << p) - 1;
-      if (!(zero & need)) {
-        const bool use = lane <= p;
-        first += wave_sum_i(use ? (int)(uint32_t)s : 0);
-        bad_all |= __any(use && (s & ST_BAD));
-        if (p < 64) break;
-        v -= 64;
-      } else {
-        __builtin_amdgcn_s_sleep(1);
+  // the start (wave 0): the phase for the first workgroup, else the end of the
+  // previous one -- 64 workgroups at a time, lane i reading the one i places
+  // back: the nearest published end and every total after it (else read again)
+  if (wv == 0) {
+    int64_t first = 0;
+    bool bad_all = wbad;
+    if (G == 0) {
+      first = a.phase ? a.phase[fi] : 0;
+    } else {
+      for (int v = G - 1;;) {
+        const uint64_t inc = __ballot((s >> 62) == 2), zero = __ballot(s == 0);
+        const int p = inc ? (int)__builtin_ctzll(inc) : 64;  // the nearest end
+        const uint64_t need = p == 64 ? ~0ull : (2ull << p) - 1;
+        if (!(zero & need)) {
+          const bool use = lane <= p;
+          first += wave_sum_i(use ? (int)(uint32_t)s : 0);
+          bad_all |= __any(use && (s & ST_BAD));
+          if (p < 64) break;
+          v -= 64;
+        } else {
+          __builtin_amdgcn_s_sleep(1);
+        }
+        s = v - lane >= 0 ? st_load(stw + 2 * (v - lane)) : ST_INCL;
       }
-      s = v - lane >= 0 ? st_load(stw + 2 * (v - lane)) : ST_INCL;
+    }
+    const int64_t endb = first + wt;
+    if (lane == 0) {
+      st_store(stw + 2 * G, ST_INCL | (bad_all ? ST_BAD : 0) | (uint64_t)(uint32_t)endb);
+      if (G == ng - 1) a.bits[fi] = (bad_all || endb + 64 > a.out_words * 32) ? 0xFFFFFFFFu : (uint32_t)endb;
+      s_first = first;
     }
   }
-  const int64_t endb = first + tot;
-  if (lane == 0) st_store(stw + 2 * wi, ST_INCL | (bad_all ? ST_BAD : 0) | (uint64_t)(uint32_t)endb);
-  const bool last_wave = wi == nwp - 1;
-  const bool fits = endb + 64 <= a.out_words * 32;
-  if (last_wave && lane == 0) a.bits[fi] = (bad_all || !fits) ? 0xFFFFFFFFu : (uint32_t)endb;
-  if (!fits) return;  // (nor does any later wave of the picture: nothing written)
+  __syncthreads();
+  const int64_t first = s_first, endb = first + wt;
+  if (endb + 64 > a.out_words * 32) return;  // (nor does any later workgroup of the picture write)
   uint32_t *out = a.out + (size_t)fi * a.out_words;
-  // the words [w0, wl]; the first is shared with the previous wave unless the
-  // range starts on a word boundary (or is the picture's start), the last
-  // with the next unless it ends on one (or is the picture's end)
+  // the words [w0, wl]; the first is shared with the previous workgroup
+  // unless the range starts on a word boundary (or is the picture's start),
+  // the last with the next unless it ends on one (or is the picture's end)
   const int64_t w0 = first >> 5, wl = (endb - 1) >> 5;
-  const bool sh_first = wi > 0 && (first & 31) != 0;
-  const bool sh_last = !last_wave && (endb & 31) != 0;
+  const bool sh_first = G > 0 && (first & 31) != 0;
+  const bool sh_last = G < ng - 1 && (endb & 31) != 0;
   uint32_t firstv = 0, lastv = 0;
-  if (in_lds && tot > 0) {  // (the common case) the copy shifted by the phase, word per lane
-    const int sh = (int)(first & 31), nw = (int)(wl - w0 + 1);
-    auto word = [&](int t) {  // word t of the range (big-endian bytes, as stored)
-      const uint32_t cur = t < nwr ? __builtin_bswap32(wb[t]) : 0u;
-      const uint32_t prev = t > 0 ? __builtin_bswap32(wb[t - 1]) : 0u;
-      return __builtin_bswap32(sh ? (cur >> sh) | (prev << (32 - sh)) : cur);
-    };
-    firstv = word(0);
-    lastv = word(nw - 1);
+  if (!big && wt > 0) {  // (the common case) the four copies shifted to their starts, word per thread
+    auto word = [&](int64_t gw) {  // picture word gw of this range: the waves' bits in it
+      uint32_t x = 0;
 #pragma unroll
-    for (int i = 0; i < VLC_EMIT_WORDS / 64; i++) {
-      const int t = lane + 64 * i;
-      if (t < nw && !(t == 0 && sh_first) && !(t == nw - 1 && sh_last)) out[w0 + t] = word(t);
+      for (int v = 0; v < VLC_WAVES; v++) {
+        const int tv = s_tot[v];
+        const int64_t fv = first + off[v];
+        const int64_t t = gw - (fv >> 5);
+        if (tv > 0 && t >= 0 && gw <= (fv + tv - 1) >> 5) {
+          const uint32_t *bv = wbits + v * VLC_EMIT_WORDS;
+          const int sh = (int)(fv & 31), nwr = (tv + 31) >> 5;
+          const uint32_t cur = t < nwr ? __builtin_bswap32(bv[t]) : 0u;
+          const uint32_t prev = t > 0 ? __builtin_bswap32(bv[t - 1]) : 0u;
+          x |= __builtin_bswap32(sh ? (cur >> sh) | (prev << (32 - sh)) : cur);
+        }
+      }
+      return x;
+    };
+    for (int64_t gw = w0 + threadIdx.x; gw <= wl; gw += 64 * VLC_WAVES)
+      if (!(gw == w0 && sh_first) && !(gw == wl && sh_last)) out[gw] = word(gw);
+    if (wv == 0) {
+      firstv = word(w0);
+      lastv = word(wl);
     }
-  } else if (tot > 0) {  // more bits than the copy holds: zero the words, OR the codes in memory
-    for (int64_t gw = w0 + lane; gw <= wl; gw += 64) out[gw] = 0;
+  } else if (wt > 0) {  // a wave past its copy: zero the words, OR the codes in memory
+    for (int64_t gw = w0 + threadIdx.x; gw <= wl; gw += 64 * VLC_WAVES) out[gw] = 0;
     __threadfence();
-    BitWriter bw;
-    emit(bw, out, first);
+    __syncthreads();
+    if (tot > 0) {
+      BitWriter bw;
+      emit(bw, out, first + off[wv]);
+    }
     __threadfence();
-    firstv = (uint32_t)__builtin_amdgcn_readfirstlane((int)__hip_atomic_load(out + w0, __ATOMIC_RELAXED,
-                                                                              __HIP_MEMORY_SCOPE_AGENT));
-    lastv = (uint32_t)__builtin_amdgcn_readfirstlane((int)__hip_atomic_load(out + wl, __ATOMIC_RELAXED,
-                                                                             __HIP_MEMORY_SCOPE_AGENT));
+    __syncthreads();
+    if (wv == 0) {
+      firstv = (uint32_t)__builtin_amdgcn_readfirstlane((int)__hip_atomic_load(out + w0, __ATOMIC_RELAXED,
+                                                                                __HIP_MEMORY_SCOPE_AGENT));
+      lastv = (uint32_t)__builtin_amdgcn_readfirstlane((int)__hip_atomic_load(out + wl, __ATOMIC_RELAXED,
+                                                                               __HIP_MEMORY_SCOPE_AGENT));
+    }
   }
-  // the shared words: hand the last one on, then take the previous wave's
-  if (tot == 0 || w0 == wl) {  // (one word: the previous wave's tail and ours)
-    uint32_t v = tot > 0 ? firstv : 0u;
-    if (sh_first) v |= (uint32_t)st_wait(stw + 2 * (wi - 1) + 1);
+  if (wv != 0) return;
+  // the shared words (wave 0): hand the last one on, then take the previous
+  // workgroup's
+  if (wt == 0 || w0 == wl) {  // (one word: the previous workgroup's tail and ours)
+    uint32_t v = wt > 0 ? firstv : 0u;
+    if (sh_first) v |= (uint32_t)st_wait(stw + 2 * (G - 1) + 1);
     if (sh_last) {
-      if (lane == 0) st_store(stw + 2 * wi + 1, (1ull << 63) | v);
-    } else if ((tot > 0 || sh_first) && lane == 0) {
+      if (lane == 0) st_store(stw + 2 * G + 1, (1ull << 63) | v);
+    } else if ((wt > 0 || sh_first) && lane == 0) {
       out[w0] = v;
     }
   } else {
-    if (sh_last && lane == 0) st_store(stw + 2 * wi + 1, (1ull << 63) | lastv);
+    if (sh_last && lane == 0) st_store(stw + 2 * G + 1, (1ull << 63) | lastv);
     if (sh_first) {
-      const uint32_t pv = (uint32_t)st_wait(stw + 2 * (wi - 1) + 1);
+      const uint32_t pv = (uint32_t)st_wait(stw + 2 * (G - 1) + 1);
       if (lane == 0) out[w0] = firstv | pv;
     }
   }
@@ -632,10 +668,10 @@ int p64gpu_vlc_pictures(const p64gpu_vlc_args *x, void *stream) {
     a.bits = x->bits + f0;
     // this chunk's [6][nc][nmb] words of the scratch
     uint32_t *scr = x->scratch + 6 * m0;
-    a.status = scr;  // 4 words per wave of a picture (<= 2 nmb)
-    const int nwp = (nmb + VLC_MBS - 1) / VLC_MBS;
-    const dim3 grid((unsigned)((nwp + VLC_WAVES - 1) / VLC_WAVES), (unsigned)nc);
-    hipError_t me = hipMemsetAsync(scr, 0, (size_t)nc * nwp * 16, st);
+    a.status = scr;  // 4 words per workgroup of a picture
+    const int nwg = (nmb + VLC_WAVES * VLC_MBS - 1) / (VLC_WAVES * VLC_MBS);  // workgroups per picture
+    const dim3 grid((unsigned)nwg, (unsigned)nc);
+    hipError_t me = hipMemsetAsync(scr, 0, (size_t)nc * nwg * 16, st);
     if (me != hipSuccess) return p64gpu_fail_(P64GPU_E_HIP, hipGetErrorString(me));
     if (x->blk_bits) {  // the blocks' bits from the encoder: no count
       a.blk_bits = x->blk_bits + m0 * 8;
