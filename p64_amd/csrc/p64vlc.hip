@@ -132,7 +132,10 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-constexpr int VLC_WAVES = 4;  // waves per workgroup
+#ifndef VLC_WAVES_N
+#define VLC_WAVES_N 4
+#endif
+constexpr int VLC_WAVES = VLC_WAVES_N;  // waves per workgroup
 constexpr int VLC_MBS = 10;   // macroblocks per wave: lane 6m + b codes block b of MB m
 
 // raster macroblock k -> stream position j = 33 g + m (GOB g, MDU m; the

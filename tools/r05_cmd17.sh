@@ -1,0 +1,8 @@
+#!/bin/bash
+# VLC workgroup size A/B (4, 6, 8 waves), stream tests on the 8-wave build
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+cd $R && mkdir -p gpurun_out
+P64GPU_LIB=$R/abtest/lib_vlcw2.so timeout -k 10 400 python -u -m pytest tests/test_gpu_stream.py -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/t17.log 2>&1 || { tail -30 gpurun_out/t17.log; exit 1; }
+tail -1 gpurun_out/t17.log
+CONTENTS="survey synth" bash tools/vlc_prof.sh abtest/lib_vlc4.so abtest/lib_vlcw2.so abtest/lib_vlcw3.so || exit 1
