@@ -1176,7 +1176,7 @@ def measure_vlc(args, torch, p64_amd, step, out_of, S, nmb, w, h):
         res["other_path"] = dict(other, path="the coder counts" if best is given else
                                  "encoder counts (vlc_bits -> blk_bits)")
         res["note"] = ("encode launches + GPU entropy coding (one launch after a status-word memset: "
-                       "each wave of ten MBs counts or takes its bits, finds its start by a decoupled "
+                       "each workgroup of 40 MBs counts or takes its bits, finds its start by a decoupled "
                        "look-back, writes its words) per step, every picture's bit count copied to "
                        "pinned host memory, the steps replayed as one HIP graph; the faster of the two "
                        "paths (path / other_path); not part of `value`")
