@@ -374,3 +374,34 @@ def test_gpu_vlc_invalid_records(p64, torch_dev, given):
 def ctypes_ptr(t):
     import ctypes
     return ctypes.c_void_p(t.data_ptr())
+
+
+def test_gpu_vlc_graph_replay(p64, torch_dev):
+    """The coder's launch (a memset of its status words + one kernel) captured
+    in a HIP graph and replayed twice gives the eager call's bits: the
+    look-back state is reset by the captured memset, not by the host."""
+    from p64_amd import stream
+    torch = torch_dev
+    z = load("seq_qcif_full31.npz")
+    mb, coef, gq, uq = fixture_records(z, stream.format_of(176, 144))
+    d = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()  # noqa: E731
+    tr = d(np.arange(mb.shape[0], dtype=np.int32) % 32)
+    mbd, cd, gqd, uqd = d(mb), d(coef), d(gq), d(uq)
+    out0, bits0 = stream.vlc_pictures(mbd, cd, gqd, tr, width=176, height=144, mquant=uqd)
+    out0 = out0.cpu().numpy()
+    bufs = stream.vlc_buffers(mb.shape[0], 176, 144)
+    stream.vlc_pictures(mbd, cd, gqd, tr, width=176, height=144, mquant=uqd, buffers=bufs)  # (tables)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        stream.vlc_pictures(mbd, cd, gqd, tr, width=176, height=144, mquant=uqd, buffers=bufs, host_bits=False)
+    for _ in range(2):
+        bufs[0].zero_()
+        g.replay()
+        torch.cuda.synchronize()
+        bits = [int(x) & 0xFFFFFFFF for x in bufs[1][:mb.shape[0]].cpu().tolist()]
+        assert bits == list(bits0)
+        out = bufs[0].cpu().numpy()
+        for t in range(mb.shape[0]):
+            nb = (bits[t] + 7) // 8
+            np.testing.assert_array_equal(out[t, :nb], out0[t, :nb])
