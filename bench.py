@@ -1097,7 +1097,12 @@ def sad_executed(args, key, kme, clk, mbs):
             "kernel_us": us, "kernel_us_source": src,
             "note": "executed v_sad_u8 lane-instructions x 4 (counted by tools/sad_count.py on this "
                     "workload, profiles/sad_executed.json) over k_motion's launch time; the rest of "
-                    "k_motion's issue is the bound map, addressing and reductions (valu_busy)"}
+                    "k_motion's issue is the bound map, addressing and reductions (valu_busy). The "
+                    "fraction falls when the pruning improves (fewer SADs for the same answer): on "
+                    "survey content the bound leaves fewer full SADs than on synth, so 0.16 here "
+                    "against 0.29 there at similar kernel times. k_motion's utilisation is valu_busy "
+                    "(VALU issue, PMC-derived; DESIGN.md 9a item 3 shows +64 VALU per MB costing "
+                    "80-90% of their issue time)"}
 
 
 def strip(r):
