@@ -1229,11 +1229,17 @@ def measure_content(args, torch, dist, world, p64_amd, content, S, seed0, nslots
                                        spin={"init": spin_init, "reset": spin_reset,
                                              "launch": lambda t: launch(t, sp["rec"], sp["li"], sp["out"])})
         tmax = max_over_ranks(elapsed, world, device="cuda")
-        return {"content": content, "value": round(aggregate_rate(world, S * nmb, args.steps, tmax), 1),
-                "ms_per_step": round(tmax / args.steps * 1e3, 4),
-                "clock_mhz_after": clk.get("clock_mhz_after"),
-                "note": "the same inter steps (closed loop, K steps in one graph) on this content; "
-                        "round 4's headline content was synth"}
+        sp.clear()
+        res = {"content": content, "value": round(aggregate_rate(world, S * nmb, args.steps, tmax), 1),
+               "ms_per_step": round(tmax / args.steps * 1e3, 4),
+               "clock_mhz_after": clk.get("clock_mhz_after"),
+               "note": "the same inter steps (closed loop, K steps in one graph) on this content; "
+                       "round 4's headline content was synth"}
+        if not args.no_vlc:  # and the whole encoder to bits on it (round 4's with_vlc was on synth)
+            def step_c(t, vlc_bits=None):
+                launch(t, o=out if vlc_bits is None else dataclasses.replace(out, vlc_bits=vlc_bits))
+            res["with_vlc"] = measure_vlc(args, torch, p64_amd, step_c, lambda t: out, S, nmb, w, h)
+        return res
     except Exception as e:  # never let the extra measurement cost the bench line
         return {"content": content, "error": str(e)[:200]}
 
