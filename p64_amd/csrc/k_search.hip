@@ -512,17 +512,22 @@ __device__ __forceinline__ MeSetup me_setup(int w, int h, int x0, int y0, int sl
   // Validity (me.c:206-212: range and `< W-16`) is folded into the sums: an
   // invalid candidate starts at ME_INVALID, so it never survives and never wins.
   const int hl = sl >> 1;
-  const int px = x0 + u.dx;
-  u.col_ok = u.lane_ok && u.dx >= -hl && u.dx < hl && px >= 0 && px < w - 16;
-  // valid dy: [max(-hl, -y0), min(hl, h-16-y0)), i.e. d in [dlo, dhi) for this group
-  const int dlo = max(-hl, -y0) - u.dy0, dhi = min(hl, h - 16 - y0) - u.dy0;
-  const bool all_rows = dlo <= 0 && dhi >= ND;
-  u.interior = uni(__all(!u.lane_ok || (u.col_ok && all_rows)));
+  // interior: every lane's every candidate valid -- from the MB's position and
+  // the limit alone (scalar: the extreme columns and the extreme dy of the
+  // first and last groups decide it)
+  constexpr int NQ = 64 / LY::DXL;  // dy groups
+  u.interior = -hl <= LY::D0 && LY::D0 + LY::NDX - 1 < hl && x0 + LY::D0 >= 0 && x0 + LY::D0 + LY::NDX - 1 < w - 16 &&
+               max(-hl, -y0) <= LY::D0 && min(hl, h - 16 - y0) >= LY::D0 + ND * NQ;
   // the sums start at 0; invalid candidates are marked afterwards (bit 19 of a
   // sum < 2^17): interior macroblocks only mask the two idle lanes, the others
   // OR in the lane's invalid rows, ~valid [dlo, dhi) (or every row)
   u.inv = 0;
+  u.col_ok = u.lane_ok;
   if (!u.interior) {
+    const int px = x0 + u.dx;
+    u.col_ok = u.lane_ok && u.dx >= -hl && u.dx < hl && px >= 0 && px < w - 16;
+    // valid dy: [max(-hl, -y0), min(hl, h-16-y0)), i.e. d in [dlo, dhi) for this group
+    const int dlo = max(-hl, -y0) - u.dy0, dhi = min(hl, h - 16 - y0) - u.dy0;
     const int lo = min(max(dlo, 0), ND), hi = min(max(dhi, 0), ND);
     u.inv = ~((u.col_ok && hi > lo) ? (1u << hi) - (1u << lo) : 0u);
   }
