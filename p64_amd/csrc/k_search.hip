@@ -399,7 +399,7 @@ __device__ __forceinline__ unsigned finish_groups(const Sx &S, int n, int lane) 
 // only (the current rows 0..7 wave-uniform in SGPRs, no LDS broadcast) and
 // adds the lower bound of rows 8..15 from the sub-block averages, 16 Sbot -
 // 256 (Sbot: the candidate's terms of sub-block rows 2 and 3, carried in its
-// list entry above the ord); a candidate whose
+// list entry's high half); a candidate whose
 //     LB2 = SAD(rows 0..7) + 16 Sbot - 256 > T
 // can neither win nor tie (LB2 <= SAD, per sub-block as in me_full's bound).
 // The few left (c* excluded: its key is known) are compacted in place with
@@ -462,7 +462,7 @@ __device__ __forceinline__ unsigned finish_halves(const Sx &S, const uint8_t *cu
       a = sad4(align4(a3, a2, csh), cs[4 * r + 2], a);
       a = sad4(align4(a4, a3, csh), cs[4 * r + 3], a);
     }
-    const int lb2 = (int)a + 16 * (int)(e >> KEY_SHIFT) - 256;
+    const int lb2 = (int)a + 16 * (int)(e >> 16) - 256;  // (Sbot in the entry's high half)
     const bool sv = act && ord != cstar_ord && lb2 <= (int)T;
     const uint64_t bl = __ballot(sv);
     // compacted in place: every entry of this chunk was read above, and the
@@ -656,8 +656,10 @@ __device__ __forceinline__ void me_full(const Sx &S, const uint8_t *cur_blk, int
       if (bl) {
         const int idx = nsurv + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bl >> 32),
                                                                __builtin_amdgcn_mbcnt_lo((uint32_t)bl, 0u));
-        // the entry: ord | Sbot << KEY_SHIFT (finish_halves)
-        if (sv && idx < ME_LIST_MAX) list[idx] = (base + d) | ((acc[d] >> 16) << KEY_SHIFT);
+        // the entry: ord | Sbot << 16 (finish_halves; acc's high half is
+        // Sbot).  Past ME_LIST_MAX entries the dense pass takes over and the
+        // list is not read: the index is clamped rather than tested
+        if (sv) list[min(idx, ME_LIST_MAX - 1)] = (acc[d] & 0xFFFF0000u) | (base + d);
         nsurv += __popcll(bl);
       }
     }
