@@ -575,7 +575,7 @@ __device__ __forceinline__ void me_full(const Sx &S, const uint8_t *cur_blk, int
   sad0 = uni(sad0);
   sad0_out = sad0;
   unsigned bk = 0xFFFFFFFFu, ckey = 0xFFFFFFFFu, Ts = 0, pk = 0, T = 0;
-  uint32_t acc[ND], sb[ND];  // bound sums packed (low: sub-block rows 0-1, high: 2-3), and S
+  uint32_t acc[ND], accb[ND], sb[ND];  // bound sums of sub-block rows 0-1 and 2-3 (Sbot), and S
   lds_u32 *list = as_lds(S.list);  // (one-MB image: aliases the map once the map is dead)
   int nsurv = 1000;
   // Low-contrast blocks (sub-block averages within a few levels) prune almost
@@ -598,7 +598,7 @@ __device__ __forceinline__ void me_full(const Sx &S, const uint8_t *cur_blk, int
     wsync();
     SECTION("lb_pass");
 #pragma unroll
-    for (int d = 0; d < ND; d++) acc[d] = 0;
+    for (int d = 0; d < ND; d++) acc[d] = accb[d] = 0;
     {
       const int xq = colb >> 2;
       const uint32_t *mrow = S.map + ((colb & 3) * G::MAP_PLANE + (dy0 + WIN_OY) * G::MAP_ROW) / 4 + (xq >> 2);
@@ -610,16 +610,19 @@ __device__ __forceinline__ void me_full(const Sx &S, const uint8_t *cur_blk, int
 #pragma unroll
         for (int j = 0; j < 4; j++) {
           const int d = i - 4 * j;
-          // sub-block rows 0, 1 in the low half, rows 2, 3 (Sbot, finish_halves) in the high half
-          if (d >= 0 && d < ND)
-            acc[d] = j < 2 ? sad4(m4, cm[j], acc[d]) : __builtin_amdgcn_sad_hi_u8(m4, cm[j], acc[d]);
+          // sub-block rows 0, 1 into acc, rows 2, 3 (Sbot, finish_halves) into accb
+          if (d >= 0 && d < ND) {
+            if (j < 2)
+              acc[d] = sad4(m4, cm[j], acc[d]);
+            else
+              accb[d] = sad4(m4, cm[j], accb[d]);
+          }
         }
       }
     }
 #pragma unroll
-    for (int d = 0; d < ND; d++) {  // S = low + high half, one v_dot2_u32_u16
-      typedef unsigned short u16x2_t __attribute__((ext_vector_type(2)));
-      sb[d] = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2_t, acc[d]), (u16x2_t){1, 1}, 0u, false);
+    for (int d = 0; d < ND; d++) {  // S
+      sb[d] = acc[d] + accb[d];
     }
     mark_invalid(sb);
 
@@ -659,7 +662,7 @@ __device__ __forceinline__ void me_full(const Sx &S, const uint8_t *cur_blk, int
         // the entry: ord | Sbot << 16 (finish_halves; acc's high half is
         // Sbot).  Past ME_LIST_MAX entries the dense pass takes over and the
         // list is not read: the index is clamped rather than tested
-        if (sv) list[min(idx, ME_LIST_MAX - 1)] = (acc[d] & 0xFFFF0000u) | (base + d);
+        if (sv) list[min(idx, ME_LIST_MAX - 1)] = (accb[d] << 16) | (base + d);
         nsurv += __popcll(bl);
       }
     }
