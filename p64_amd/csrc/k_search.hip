@@ -292,7 +292,6 @@ __device__ __forceinline__ void build_lb_map(const Sx &S, int lane) {
 // of sub-blocks as one wave-uniform dword cm[j] (byte i = sub-block (i, j),
 // also left as bytes 0..15 of L.cpred); returns their range (max - min)
 __device__ __forceinline__ int cur_lb_map(const Sx &S, int lane, uint32_t cm[4]) {
-  unsigned lo = 255, hi = 0;
   if (lane < 16) {
     const int i = lane & 3, j = lane >> 2;
     const uint32_t *r = S.cur + 16 * j + i;
@@ -300,22 +299,31 @@ __device__ __forceinline__ int cur_lb_map(const Sx &S, int lane, uint32_t cm[4])
     const uint32_t h1 = lerp4(v, v >> 8);
     const uint32_t h2 = lerp4(h1, h1 >> 16);
     reinterpret_cast<uint8_t *>(S.cpred)[lane] = (uint8_t)h2;
-    lo = hi = h2 & 255u;
   }
-  // min and max over DPP row 0 (lanes 0..15)
-  lo = min(lo, dpp<0xB1>(lo));
-  hi = max(hi, dpp<0xB1>(hi));
-  lo = min(lo, dpp<0x4E>(lo));
-  hi = max(hi, dpp<0x4E>(hi));
-  lo = min(lo, dpp<0x141>(lo));
-  hi = max(hi, dpp<0x141>(hi));
-  lo = min(lo, dpp<0x140>(lo));
-  hi = max(hi, dpp<0x140>(hi));
-  const int range = __builtin_amdgcn_readlane((int)(hi - lo), 0);
   wsync();
 #pragma unroll
   for (int j = 0; j < 4; j++) cm[j] = (uint32_t)uni((int)S.cpred[j]);
-  return range;
+  // their range from the wave-uniform dwords: scalar byte extracts, min and
+  // max (the scalar unit, not the VALU the search is bound by; asm, as the
+  // compiler otherwise picks v_min3/v_max3 over SGPR operands)
+  auto smin = [](unsigned a, unsigned b) {
+    unsigned r;
+    asm("s_min_u32 %0, %1, %2" : "=s"(r) : "s"(a), "s"(b));
+    return r;
+  };
+  auto smax = [](unsigned a, unsigned b) {
+    unsigned r;
+    asm("s_max_u32 %0, %1, %2" : "=s"(r) : "s"(a), "s"(b));
+    return r;
+  };
+  unsigned lo = cm[0] & 255u, hi = lo;
+#pragma unroll
+  for (int k = 1; k < 16; k++) {
+    const unsigned b = (cm[k >> 2] >> (8 * (k & 3))) & 255u;
+    lo = smin(lo, b);
+    hi = smax(hi, b);
+  }
+  return (int)(hi - lo);
 }
 
 // SAD(0,0) (OMV, me.c:203/271) and, in the same wave reduction, the current
