@@ -417,13 +417,11 @@ __global__ __launch_bounds__(64 * VLC_WAVES) void k_vlc_blk(VlcArgs a, VlcTables
   }
   // the lane's bits: the headers (b = 0: picture header before MDU 0 of GOB 0,
   // GOB header before MDU 0, the MB header), then its block
-  int hbits = 0;
-  bool hbad = false;
-  if (act && b == 0) {  // (the codes themselves again when they are written)
-    const Header hd = header_codes(T, r, rp, mq, m);
-    hbits = (j == 0 ? 32 + (a.format == P64S_NTSC ? 9 : 0) : 0) + (m == 0 ? 26 : 0) + hd.bits;
-    hbad = hd.bad;
-  }
+  // (the header codes stay in registers for the emission: the workgroup's
+  // LDS, not its registers, sets the occupancy)
+  const Header hd = header_codes(T, r, rp, mq, m);
+  const int hbits = act && b == 0 ? (j == 0 ? 32 + (a.format == P64S_NTSC ? 9 : 0) : 0) + (m == 0 ? 26 : 0) + hd.bits : 0;
+  const bool hbad = act && b == 0 && hd.bad;
   const int lbits = hbits + bb;
   const int incl = wave_incl_scan(lbits);
   const int rel = incl - lbits;  // the lane's first bit, from the wave's first
@@ -432,7 +430,6 @@ __global__ __launch_bounds__(64 * VLC_WAVES) void k_vlc_blk(VlcArgs a, VlcTables
   const uint32_t trv = (uint32_t)a.tr[fi] & 31u, gqv = a.gquant[(size_t)fi * a.ngob + g] & 31u;
   auto emit = [&](auto &bw, uint32_t *dst, int64_t base) {
     if (act && b == 0) {
-      const Header hd = header_codes(T, r, rp, mq, m);
       bw.start(dst, base + rel);
       if (j == 0) {  // WritePictureHeader marker.c:103-135
         bw.put(0x10u, 20);
