@@ -303,7 +303,10 @@ __device__ __forceinline__ void block_codes(const VlcTables &T, const L *lvs, ui
 //     status word ("tail"), which ORs it into its first word and stores that
 //     -- no word of the picture is written twice, nothing needs zeroing, and
 //     the only waits are on earlier workgroups' totals and the previous one's
-//     tail.
+//     tail.  Forward progress: a workgroup waits only on lower-numbered ones
+//     of its picture (same blockIdx.y), which the dispatcher (each XCD in
+//     order over its round-robin share) started before it, so the oldest
+//     unfinished workgroup is always resident and never waits.
 // The levels' LDS copy is int8 (64 + 16 pad bytes per lane); H.261 levels fit
 // it.  A wave with a coded level outside -128..127 (which the reference's
 // quantiser never makes, but the ABI takes) reads the int16 levels from
