@@ -64,3 +64,13 @@ clean:
 	$(MAKE) -C oracle clean
 
 .PHONY: all oracle ref asm clean
+
+# bounds-checked entropy coder (diagnostic aid, tools/vlc_fault_probe.py):
+# the same library with k_vlc_blk's stores range-tested (P64_VLC_CHECK)
+vlccheck: abtest/lib_vlccheck.so
+abtest/lib_vlccheck.so: p64_amd/csrc/p64vlc.hip $(GPU_OBJS) p64_amd/csrc/synth.o p64_amd/csrc/p64stream.o \
+                        p64_amd/csrc/p64seq.o p64_amd/csrc/p64prog.o
+	mkdir -p abtest
+	$(HIPCC) $(HIPFLAGS) -DP64_VLC_CHECK -c $< -o abtest/p64vlc_check.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $(GPU_OBJS) p64_amd/csrc/synth.o p64_amd/csrc/p64stream.o \
+	  p64_amd/csrc/p64seq.o p64_amd/csrc/p64prog.o abtest/p64vlc_check.o

@@ -212,17 +212,21 @@ def gather_outputs(world: int, rank: int, local, bufs):
     return bufs
 
 
-def gather_coded(world, rank, out, bits):
+def gather_coded(world, rank, out, bits, mx=None):
     """--feed root, coded: every rank's entropy-coded pictures to rank 0.
     out [S, stride] uint8 holds each picture's bits from byte 0 (at its
     sequence's bit phase), bits [S] int32 their counts incl. the phase.  One
-    MAX all-reduce of the longest picture, then the first nb bytes of every
-    picture (nb = that length, 4-aligned) and the counts, gathered as bytes:
-    ~S x nb bytes per rank instead of S x nmb x 772 for the levels.  Returns
-    on rank 0 ([world] payloads [S, nb], [world] bit counts [S]), else None."""
+    MAX all-reduce of the longest picture (mx: a [1] int64 tensor holding
+    this rank's longest, else computed here), then the first nb bytes of
+    every picture (nb = that length, 4-aligned) and the counts, gathered as
+    bytes: ~S x nb bytes per rank instead of S x nmb x 772 for the levels.
+    The size is read back with .item() on the CURRENT stream (CodedFeed runs
+    this on a side stream, so the encode stream does not wait).  Returns on
+    rank 0 ([world] payloads [S, nb], [world] bit counts [S]), else None."""
     import torch
     import torch.distributed as dist
-    mx = bits.to(torch.int64).max().reshape(1)
+    if mx is None:
+        mx = bits.to(torch.int64).max().reshape(1)
     if world > 1:
         dist.all_reduce(mx, op=dist.ReduceOp.MAX)
     nb = (int(mx.item()) + 7) // 8
@@ -237,6 +241,139 @@ def gather_coded(world, rank, out, bits):
     dist.gather(b32.view(torch.uint8), gather_list=[b.view(torch.uint8) for b in bl] if rank == 0 else None,
                 dst=0)
     return (pays, bl) if rank == 0 else None
+
+
+def stitch_pieces(writers, pieces, bits):
+    """Rank 0: appends one step's coded pictures to their sequences' streams.
+    writers: {sequence: stream.Writer}; pieces[sequence] the picture's bytes
+    from byte 0, coded at the writer's bit phase (its first byte shares the
+    stream's pending byte), bits[sequence] its bit count incl. that phase
+    (p64s_write_bits: the pending byte ORed, the rest appended; the writer
+    closes the stream with p64s_write_end's padding, stream.c:142-150)."""
+    for s, wr in writers.items():
+        b = int(bits[s])
+        if b == 0xFFFFFFFF or b < 0:
+            raise RuntimeError(f"coded picture of sequence {s}: invalid record or overflow")
+        wr.write_bits(pieces[s], b, wr.phase())
+
+
+class CodedFeed:
+    """--feed root --gather coded: the rank's pictures entropy-coded on its
+    GPU each step, every picture at its sequence's running bit phase
+    (p64gpu_vlc_pictures; p64EncodeSequence's continuous stream, p64.c:524-613),
+    and the coded pictures gathered to rank 0 -- one step LATE, on a side
+    stream: step t's coder writes buffer t % 2 and records the step's longest
+    picture on the device; the gather of step t-1 then waits for that event on
+    the side stream, MAX-reduces the size there and reads it back with a
+    side-stream sync, so the encode stream never waits for the host and the
+    gather overlaps step t's encode (round 6: no per-step .item() on the
+    encode stream).  Before the coder reuses a buffer the encode stream waits
+    for the side stream.  finish() gathers the last step.
+    Rank 0 keeps the pieces of the sequences in `keep` (global indices) for
+    stitch_pieces; verification happens after the timed region."""
+
+    def __init__(self, torch, p64s, world, rank, S, w, h, quant, keep=()):
+        import torch.distributed as dist
+        self.torch, self.p64s, self.dist = torch, p64s, dist
+        self.world, self.rank, self.S, self.w, self.h = world, rank, S, w, h
+        nmb = (w // 16) * (h // 16)
+        self.bufs = [p64s.vlc_buffers(S, w, h) for _ in range(2)]
+        self.gq = torch.full((S, nmb // 33), quant, dtype=torch.uint8, device="cuda")
+        self.trs = [torch.full((S,), t, dtype=torch.int32, device="cuda") for t in range(32)]
+        self.seq_bits = torch.zeros(S, dtype=torch.int64, device="cuda")  # bits so far per sequence
+        self.phase = torch.zeros(S, dtype=torch.uint8, device="cuda")
+        self.mx = [torch.zeros(1, dtype=torch.int64, device="cuda") for _ in range(2)]
+        self.bits = [None, None]
+        self.ev = [torch.cuda.Event(), torch.cuda.Event()]
+        self.side = torch.cuda.Stream()
+        self.pending = None
+        # rank 0: (rank, local row) of each kept global sequence
+        self.keep = {g: (g // S, g % S) for g in keep if g < world * S}
+        self.kept = []  # per coded step: {global sequence: (piece tensor, bits tensor)}
+        self.steps = []
+
+    def code(self, t, o):
+        """Step t's pictures (outputs o of the encode) into bits, then the
+        gather of step t-1."""
+        torch = self.torch
+        main = torch.cuda.current_stream()
+        main.wait_stream(self.side)  # (the gather of step t-2 has read buffer t % 2)
+        k = t % 2
+        ph = (self.seq_bits & 7).to(torch.uint8)
+        self.phase.copy_(ph)
+        _, bits = self.p64s.vlc_pictures(o.mb, o.coef, self.gq, self.trs[t % 32], width=self.w, height=self.h,
+                                         phase=self.phase, buffers=self.bufs[k], host_bits=False,
+                                         blk_bits=o.vlc_bits)
+        self.seq_bits.add_(bits.to(torch.int64) - self.phase.to(torch.int64))
+        self.bits[k] = bits
+        torch.amax(bits.to(torch.int64), dim=0, keepdim=True, out=self.mx[k])
+        self.ev[k].record(main)
+        if self.pending is not None:
+            self._gather(self.pending)
+        self.pending = t
+
+    def finish(self):
+        if self.pending is not None:
+            self._gather(self.pending)
+            self.pending = None
+        self.torch.cuda.current_stream().wait_stream(self.side)
+
+    def _gather(self, t):
+        torch = self.torch
+        k = t % 2
+        with torch.cuda.stream(self.side):
+            self.side.wait_event(self.ev[k])
+            got = gather_coded(self.world, self.rank, self.bufs[k][0], self.bits[k], mx=self.mx[k])
+            if got is not None and self.keep:
+                pays, bls = got
+                self.kept.append({g: (pays[r][i].clone(), bls[r][i].clone()) for g, (r, i) in self.keep.items()})
+                self.steps.append(t)
+
+    def streams(self, fmt, end_tr):
+        """Rank 0, after the run: the kept sequences' stitched .p64 streams
+        ({global sequence: bytes}, closed like p64seq_finish) and bit counts."""
+        self.torch.cuda.synchronize()
+        writers = {g: self.p64s.Writer(fmt) for g in self.keep}
+        for per in self.kept:
+            pieces = {g: per[g][0].cpu().numpy().tobytes() for g in writers}
+            bits = {g: int(per[g][1].item()) & 0xFFFFFFFF for g in writers}
+            stitch_pieces(writers, pieces, bits)
+        out = {}
+        for g, wr in writers.items():
+            nbits = wr.bits()
+            out[g] = (wr.end(end_tr), nbits)
+        return out
+
+
+def verify_coded(args, p64_amd, p64s, src, slot, streams, upto, w, h, mode):
+    """The stitched streams of --feed root against the host writer over the
+    CPU oracle's records of the same sequences (closed loop, pictures
+    0..upto at TR t % 32, GQUANT = the run's q, closed like p64seq_finish):
+    byte-identical .p64 (what the GPU coder writes equals p64s_write_picture,
+    tests/test_gpu_stream.py; p64.c:524-613, stream.c:142-150)."""
+    import hashlib
+    import oracle
+    from concurrent.futures import ThreadPoolExecutor
+    oracle.lib()
+    fmt = p64s.format_of(w, h)
+
+    def one(g):
+        fr = [src[slot(t), g].cpu().numpy() for t in range(upto + 1)]
+        outs = oracle.encode_sequence(fr, w, h, quant=args.quant, me_mode=mode, search_limit=args.search_limit)
+        wr = p64s.Writer(fmt)
+        for t, (coef, mb, _, _) in enumerate(outs):
+            wr.write_picture(t % 32, mb, coef, args.quant)
+        return g, wr.end((upto + 1) % 32)
+
+    with ThreadPoolExecutor(max(1, len(streams))) as ex:
+        want = dict(ex.map(one, sorted(streams)))
+    res = {f"seq{1 + g}": {"ok": streams[g][0] == want[g], "bytes": len(streams[g][0]),
+                           "sha256": hashlib.sha256(streams[g][0]).hexdigest()[:16]} for g in sorted(streams)}
+    return {"ok": all(r["ok"] for r in res.values()), "pictures": upto + 1, "sequences": res,
+            "note": "rank 0 stitched each checked sequence's gathered per-picture pieces (every rank's "
+                    "first sequence and rank 0's checked ones) into its .p64 (p64s_write_bits at the "
+                    "stream's phase, closed by p64s_write_end): equal to the host writer over the "
+                    "CPU oracle's records of the same pictures"}
 
 
 def free_port() -> int:
@@ -541,7 +678,7 @@ def roofline(bytes_per_launch, kavg, kernel, pmc=None, **extra):
 # the timed configurations
 
 def timed_region(torch, dist, world, steps, t_first, launch, pre=None, post=None, graph=True,
-                 spinup_ms=0, spin=None):
+                 spinup_ms=0, spin=None, finish=None):
     """The K timed steps, bracketed by barrier + synchronize on both sides.
 
     launch(t) issues step t's kernel on torch's current stream (the library
@@ -570,6 +707,8 @@ def timed_region(torch, dist, world, steps, t_first, launch, pre=None, post=None
     timed with HIP events; the first kernel's time is the difference.
     A 50-us clock probe after the region reads the clock the chip was left
     at (box-to-box spread).
+    finish(), if given, runs after the last step inside the region (the fed
+    path's gather of its last step, CodedFeed).
     Returns (wall seconds of the timed region, mean kernel seconds per step,
     steady-state record)."""
     import p64_amd
@@ -657,6 +796,8 @@ def timed_region(torch, dist, world, steps, t_first, launch, pre=None, post=None
             ev[k][1].record()
             if post is not None:
                 post(t)
+        if finish is not None:
+            finish()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -782,12 +923,12 @@ def main(argv=None):
                                   width=w, height=h, intra=(t == 0), quant=args.quant,
                                   me_mode=mode, search_limit=args.search_limit, out=o)
 
+        feed = None
         if root and args.gather == "coded":  # each rank entropy-codes its pictures in the step
             from p64_amd import stream as p64s
-            vbufs = p64s.vlc_buffers(S, w, h)
-            gq = torch.full((S, nmb // 33), args.quant, dtype=torch.uint8, device="cuda")
-            seq_bits = torch.zeros(S, dtype=torch.int64, device="cuda")  # bits so far per sequence
-            coded_last = {}
+            keep_seqs = ([i for i in VERIFY_SEQS if i < S] + [r * S for r in range(1, world)]
+                         if rank == 0 and not args.no_verify else [])
+            feed = CodedFeed(torch, p64s, world, rank, S, w, h, args.quant, keep=keep_seqs)
 
         def post(t):  # --feed root: the coded pictures (or levels and records) back to rank 0
             o = out_of(t)
@@ -795,13 +936,7 @@ def main(argv=None):
                 gather_outputs(world, rank, o.coef, coef_bufs)
                 gather_outputs(world, rank, o.mb, mb_bufs)
                 return
-            # the picture continues its sequence's stream at bit phase seq_bits % 8
-            phase = (seq_bits & 7).to(torch.uint8)
-            tr = torch.full((S,), t % 32, dtype=torch.int32, device="cuda")
-            out, bits = p64s.vlc_pictures(o.mb, o.coef, gq, tr, width=w, height=h, phase=phase,
-                                          buffers=vbufs, host_bits=False, blk_bits=o.vlc_bits)
-            seq_bits.add_(bits.to(torch.int64) - phase.to(torch.int64))
-            coded_last["gathered"] = gather_coded(world, rank, out, bits)
+            feed.code(t, o)  # (gathers the previous step's pictures)
 
         def step(t, vlc_bits=None):
             if root:
@@ -862,7 +997,8 @@ def main(argv=None):
                                           graph=not args.eager, spinup_ms=args.spinup_ms,
                                           spin={"init": spin_init, "reset": spin_reset,
                                                 "launch": spin_launch,
-                                                "split": (kme, kin, spin_full, spin_rest)})
+                                                "split": (kme, kin, spin_full, spin_rest)},
+                                          finish=feed.finish if feed is not None else None)
         sp.clear()
         tmax = max_over_ranks(elapsed, world, device="cuda")
         assert last == t_first + args.steps - 1
@@ -877,6 +1013,12 @@ def main(argv=None):
             src = all_frames if root else frames
             verified = verify_sequences(args, p64_amd, src, slot, seqs, snap, fresh, w, h, mode)
             ok = verified["ok"]
+            if feed is not None and feed.keep:  # the gathered coded pictures, stitched per sequence
+                coded = verify_coded(args, p64_amd, p64s, src, slot,
+                                     feed.streams(p64s.format_of(w, h), (last + 1) % 32), last, w, h, mode)
+                verified["coded_verified"] = coded["ok"]
+                verified["coded"] = coded
+                ok = ok and coded["ok"]
         if not all_ranks_ok(ok, world, device="cuda"):
             raise SystemExit("bench: GPU output differs from the oracle -- refusing to report")
 
@@ -894,7 +1036,11 @@ def main(argv=None):
 
         with_vlc = None
         if not args.no_vlc:
-            with_vlc = measure_vlc(args, torch, p64_amd, step, out_of, S, nmb, w, h)
+            def enc_vlc(t, o):
+                p64_amd.encode_frames(frames[slot(t)].reshape(-1), rec[(t + 1) % 2], rec[t % 2], li,
+                                      width=w, height=h, intra=False, quant=args.quant, me_mode=mode,
+                                      search_limit=args.search_limit, out=o)
+            with_vlc = measure_vlc(args, torch, p64_amd, enc_vlc, S, nmb, w, h)
         other = None
         if keep and args.content == "survey" and args.config == "inter":
             other = measure_content(args, torch, dist, world, p64_amd, "synth", S, seed0, nslots, mode)
@@ -1110,50 +1256,68 @@ def strip(r):
     return {k: v for k, v in r.items() if k not in ("with_vlc",)}
 
 
-def measure_vlc(args, torch, p64_amd, step, out_of, S, nmb, w, h):
+def measure_vlc(args, torch, p64_amd, enc, S, nmb, w, h):
     """The encode steps followed by entropy coding on the device (p64vlc.hip):
     the whole-encoder rate to .p64 bits, measured after the metric (it re-runs
-    steps, so the closed-loop state is not reused).  Per step: the encode
-    launches, the entropy coder's launch (counting the blocks' bits itself, or
-    taking the encoder's counts: both measured), and a copy of every
-    picture's bit count to pinned host memory; the steps captured in one HIP
-    graph (as the metric's steps are), replayed for the spin-up, then once
-    more wall-clock timed.  (The copies on a forked side stream, joined at the
-    end, measured slower: 0.267 against 0.245 ms per step.)"""
+    steps, so the closed-loop state is not reused).  enc(t, o) encodes step
+    t's pictures into the FrameBatchOut o (the caller's closed loop).  Per
+    step: the encode launches on the main stream, then the entropy coder's
+    launch (counting the blocks' bits itself, or taking the encoder's counts:
+    both measured) and a copy of every picture's bit count to pinned host
+    memory FORKED onto a side stream, so step t's coder runs concurrently
+    with step t+1's encode (round 6: the coder reads only step t's records
+    and levels; two output sets alternate, and an encode waits for the coder
+    that read its set two steps before); the side stream joins at the end.
+    The steps are captured in one HIP graph (as the metric's steps are),
+    replayed for the spin-up, then once more wall-clock timed.  Afterwards one
+    more step runs eagerly and its coded pictures are compared byte for byte
+    with the host writer over the same records (sequences 0 and S-1): a
+    mismatch ends the bench (SystemExit, no line)."""
     try:
         from p64_amd import stream as p64s
         ngob = nmb // 33
         gq = torch.full((S, ngob), args.quant, dtype=torch.uint8, device="cuda")
         bufs = p64s.vlc_buffers(S, w, h)
         vsteps = min(args.steps, 8)
-        vb = torch.empty((S, nmb, 8), dtype=torch.int16, device="cuda")  # the encoder's block bits
+        outs = [p64_amd.FrameBatchOut(coef=torch.zeros((S, nmb, 6, 64), dtype=torch.int16, device="cuda"),
+                                      mb=torch.empty((S, nmb, 4), dtype=torch.int8, device="cuda"),
+                                      me=torch.empty((S, nmb, 7), dtype=torch.int32, device="cuda"),
+                                      nz=torch.empty((S, nmb), dtype=torch.uint8, device="cuda"),
+                                      vlc_bits=torch.empty((S, nmb, 8), dtype=torch.int16, device="cuda"))
+                for _ in range(2)]
         trs = [torch.full((S,), (1 + args.warmup + k) % 32, dtype=torch.int32, device="cuda")
                for k in range(vsteps)]
         host = torch.empty((vsteps, S), dtype=torch.int32, pin_memory=True)
-        p64s.vlc_pictures(out_of(1).mb, out_of(1).coef, gq, trs[0], width=w, height=h,
+        p64s.vlc_pictures(outs[0].mb, outs[0].coef, gq, trs[0], width=w, height=h,
                           buffers=bufs)  # first call: table upload
         torch.cuda.synchronize()
         vlc_ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
-        bits_dev = [None] * vsteps
+        side = torch.cuda.Stream()
 
-        def vstep(k, given, ev=False):
-            t = 1 + args.warmup + k
-            step(t, vb if given else None)
-            o = out_of(t)
-            if ev:
-                vlc_ev[0].record()
-            _, bits_dev[k] = p64s.vlc_pictures(o.mb, o.coef, gq, trs[k], width=w, height=h,
-                                               buffers=bufs, host_bits=False,
-                                               blk_bits=vb if given else None)
-            if ev:
-                vlc_ev[1].record()
-            host[k].copy_(bits_dev[k], non_blocking=True)
+        def coder(k, o, given):
+            _, bits = p64s.vlc_pictures(o.mb, o.coef, gq, trs[k], width=w, height=h, buffers=bufs,
+                                        host_bits=False, blk_bits=o.vlc_bits if given else None)
+            host[k].copy_(bits, non_blocking=True)
 
         def run(given):
+            def out(k):
+                o = outs[k % 2]
+                return o if given else dataclasses.replace(o, vlc_bits=None)
+            ev_enc = [torch.cuda.Event() for _ in range(vsteps)]
+            ev_done = [torch.cuda.Event() for _ in range(vsteps)]
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
+                main = torch.cuda.current_stream()
                 for k in range(vsteps):
-                    vstep(k, given)
+                    if k >= 2:
+                        main.wait_event(ev_done[k - 2])  # (that coder has read this output set)
+                    enc(1 + args.warmup + k, out(k))
+                    ev_enc[k].record(main)
+                    side.wait_event(ev_enc[k])
+                    with torch.cuda.stream(side):
+                        coder(k, outs[k % 2], given)
+                        ev_done[k].record(side)
+                main.wait_stream(side)
             torch.cuda.synchronize()
             # the first replay uploads the graph; then replays for >= spinup_ms
             # (the chip ramps its clocks over tens of ms, timed_region), the
@@ -1170,11 +1334,19 @@ def measure_vlc(args, torch, p64_amd, step, out_of, S, nmb, w, h):
             torch.cuda.synchronize()
             dt = time.perf_counter() - t1
             del g
-            vstep(vsteps - 1, given, ev=True)  # the coder's launches of one step alone, eagerly
-            torch.cuda.synchronize()
             hb = host.numpy().astype(np.int64) & 0xFFFFFFFF
             if (hb == 0xFFFFFFFF).any():
                 raise RuntimeError("vlc: invalid record or overflow")
+            # one more step eagerly: the coder's launch timed alone, and its
+            # pictures against the host writer
+            k = vsteps - 1
+            o = out(k)
+            enc(1 + args.warmup + k, o)
+            vlc_ev[0].record()
+            coder(k, outs[k % 2], given)
+            vlc_ev[1].record()
+            torch.cuda.synchronize()
+            check_coded(p64s, outs[k % 2], bufs, host[k].numpy(), trs[k], args.quant, w, h, (0, S - 1))
             return {"macroblocks_per_s": round(S * nmb * vsteps / dt, 1),
                     "ms_per_step": round(dt / vsteps * 1e3, 4),
                     "vlc_ms_last_step": round(vlc_ev[0].elapsed_time(vlc_ev[1]), 4),
@@ -1188,14 +1360,37 @@ def measure_vlc(args, torch, p64_amd, step, out_of, S, nmb, w, h):
         res["path"] = "encoder counts (vlc_bits -> blk_bits)" if best is given else "the coder counts"
         res["other_path"] = dict(other, path="the coder counts" if best is given else
                                  "encoder counts (vlc_bits -> blk_bits)")
+        res["coded_checked"] = {"sequences": [1, S], "vs": "host writer (p64s_write_picture) over the same records",
+                                "ok": True}
         res["note"] = ("encode launches + GPU entropy coding (one launch after a status-word memset: "
                        "each workgroup of 40 MBs counts or takes its bits, finds its start by a decoupled "
-                       "look-back, writes its words) per step, every picture's bit count copied to "
-                       "pinned host memory, the steps replayed as one HIP graph after a spin-up; the faster of the two "
+                       "look-back, writes its words) per step, the coder and the bit-count copy to pinned "
+                       "host memory forked onto a side stream (concurrent with the next step's encode), "
+                       "the steps replayed as one HIP graph after a spin-up; the faster of the two "
                        "paths (path / other_path); not part of `value`")
         return res
     except Exception as e:  # never let the extra measurement cost the bench line
         return {"error": str(e)[:200]}
+
+
+def check_coded(p64s, o, bufs, bits, tr, quant, w, h, seqs):
+    """The coder's pictures of sequences `seqs` (bytes in bufs[0], counts in
+    bits) equal the host writer's over the same records, bit for bit (ADVICE
+    r05: a timing-dependent coder fault must not pass unnoticed); SystemExit
+    otherwise."""
+    fmt = p64s.format_of(w, h)
+    data = bufs[0].cpu().numpy()
+    mb, coef, trh = o.mb.cpu().numpy(), o.coef.cpu().numpy(), tr.cpu().numpy()
+    for s in seqs:
+        wr = p64s.Writer(fmt)
+        wr.write_picture(int(trh[s]), mb[s], coef[s], quant)
+        nb, b = wr.bits(), int(bits[s]) & 0xFFFFFFFF
+        full = wr.data()
+        nbytes = (b + 7) // 8
+        gpu = int.from_bytes(data[s, :nbytes].tobytes(), "big") >> (nbytes * 8 - b) if b else 0
+        if b != nb or gpu >> (nb - 8 * len(full)) != int.from_bytes(full, "big"):
+            raise SystemExit(f"bench: GPU entropy coder differs from the host writer (sequence {s + 1}) "
+                             f"-- refusing to report")
 
 
 def measure_content(args, torch, dist, world, p64_amd, content, S, seed0, nslots, mode):
@@ -1244,9 +1439,7 @@ def measure_content(args, torch, dist, world, p64_amd, content, S, seed0, nslots
                "note": "the same inter steps (closed loop, K steps in one graph) on this content; "
                        "round 4's headline content was synth"}
         if not args.no_vlc:  # and the whole encoder to bits on it (round 4's with_vlc was on synth)
-            def step_c(t, vlc_bits=None):
-                launch(t, o=out if vlc_bits is None else dataclasses.replace(out, vlc_bits=vlc_bits))
-            res["with_vlc"] = measure_vlc(args, torch, p64_amd, step_c, lambda t: out, S, nmb, w, h)
+            res["with_vlc"] = measure_vlc(args, torch, p64_amd, lambda t, o: launch(t, o=o), S, nmb, w, h)
         return res
     except Exception as e:  # never let the extra measurement cost the bench line
         return {"content": content, "error": str(e)[:200]}

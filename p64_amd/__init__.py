@@ -139,6 +139,8 @@ def lib() -> ctypes.CDLL:
     L.p64s_writer_data.argtypes = [vp, ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(i64)]
     L.p64s_writer_data.restype = vp
     L.p64s_writer_consume.argtypes = [vp, ctypes.c_size_t]
+    L.p64s_write_bits.argtypes = [vp, vp, i64, i32]
+    L.p64s_writer_phase.argtypes = [vp]
     L.p64s_reader_open.argtypes = [vp, ctypes.c_size_t, ctypes.POINTER(vp)]
     L.p64s_reader_close.argtypes = [vp]
     L.p64s_reader_close.restype = None

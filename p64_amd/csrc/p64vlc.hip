@@ -25,6 +25,17 @@ extern "C" int p64gpu_vlc_len_table_(uint32_t *out);
 
 namespace {
 
+// A bounds-checked build (-DP64_VLC_CHECK, `make vlccheck`; a diagnostic aid,
+// not the product): every global store and status access of k_vlc_blk tests
+// its index against the buffer it was given and, out of range, sets bit
+// `site` of g_vlc_err instead of touching memory.
+#ifdef P64_VLC_CHECK
+__device__ uint32_t g_vlc_err;
+#define VLC_OK(c, site) ((c) ? true : (atomicOr(&g_vlc_err, 1u << (site)), false))
+#else
+#define VLC_OK(c, site) true
+#endif
+
 constexpr int T_MTYPE = 0, T_MVD = 10, T_CBP = 42, T_TC = 106, T_EOB = 538, T_ESC = 539,
               T_FIRST01 = 540, T_N = 541;
 struct VlcTables {
@@ -42,7 +53,7 @@ struct VlcArgs {
   uint32_t *out;  // [nframes][out_words]
   int64_t out_words;
   uint32_t *bits;     // [nframes]
-  uint32_t *status;   // [nframes][waves][4]: the look-back's status words (zeroed before the launch)
+  uint32_t *status;   // [nframes][workgroups][2] uint64 (look-back word, tail), zeroed before the launch
   uint16_t *blk_bits; // [nframes][nmb][8], raster order: [1 + b] block b's bits
 };
 
@@ -150,29 +161,40 @@ __device__ __forceinline__ int stream_pos(int format, int k) {
 // The bit writer of one lane: a segment of the picture's bits starting at
 // bit `pos`, MSB first, big-endian bytes in little-endian words (one bswap
 // per word), every word ORed into memory -- for the rare wave whose bits
-// exceed its LDS copy (k_vlc_blk zeroed its words first)
+// exceed its LDS copy (k_vlc_blk zeroed its words first).  The range's
+// first and last words, when a neighbouring workgroup shares them (s0, s1;
+// -1 if not shared), go to two LDS words instead (sh[0], sh[1]): memory
+// holds only words no other workgroup touches, and the shared ones reach it
+// through the tail hand-over, as in the LDS path.
 struct BitWriter {
   uint64_t acc;  // the pending bits, right-aligned
   int nacc;      // how many (< 32 between appends)
   int64_t w;     // picture word the pending bits start in
   uint32_t *out;
+  int64_t s0 = -1, s1 = -1;  // the shared words
+  uint32_t *sh = nullptr;    // their LDS stand-ins
+  int64_t wlo = 0, whi = 0;  // (P64_VLC_CHECK: the workgroup's words)
   __device__ __forceinline__ void start(uint32_t *o, int64_t pos) {
     out = o;
     w = pos >> 5;
     nacc = (int)(pos & 31);  // the bits before the segment, as zeros
     acc = 0;
   }
+  __device__ __forceinline__ void word(uint32_t v) {
+    if (w == s0 || w == s1 || VLC_OK(w >= wlo && w <= whi, 2))
+      atomicOr(w == s0 ? sh : (w == s1 ? sh + 1 : out + w), __builtin_bswap32(v));
+  }
   __device__ __forceinline__ void put(uint32_t v, int n) {  // n <= 32
     acc = (acc << n) | v;
     nacc += n;
     if (nacc >= 32) {
-      atomicOr(out + w, __builtin_bswap32((uint32_t)(acc >> (nacc - 32))));
+      word((uint32_t)(acc >> (nacc - 32)));
       w++;
       nacc -= 32;
     }
   }
   __device__ __forceinline__ void finish() {  // the last, partial word
-    if (nacc > 0) atomicOr(out + w, __builtin_bswap32((uint32_t)(acc << (32 - nacc))));
+    if (nacc > 0) word((uint32_t)(acc << (32 - nacc)));
   }
 };
 
@@ -412,10 +434,10 @@ __global__ __launch_bounds__(64 * VLC_WAVES) void k_vlc_blk(VlcArgs a, VlcTables
       bb = p64k::block_vlc_bits(len, lvg, m0, m1, cbpt);
     }
   } else {
-    bb = coded ? (int)bk[1 + b] : 0;
+    bb = coded && VLC_OK(a.blk_bits != nullptr, 7) ? (int)bk[1 + b] : 0;
   }
   if (!EMIT) {
-    if (act) bk[1 + b] = (uint16_t)bb;
+    if (act && VLC_OK(a.blk_bits != nullptr && fi < a.nframes && k < a.nmb, 6)) bk[1 + b] = (uint16_t)bb;
     return;
   }
   // the lane's bits: the headers (b = 0: picture header before MDU 0 of GOB 0,
@@ -488,7 +510,7 @@ __global__ __launch_bounds__(64 * VLC_WAVES) void k_vlc_blk(VlcArgs a, VlcTables
   uint64_t *stw = reinterpret_cast<uint64_t *>(a.status) + (size_t)fi * ng * 2;
   uint64_t s = ST_INCL;
   if (wv == 0 && G > 0) {
-    if (lane == 0) st_store(stw + 2 * G, ST_AGG | (wbad ? ST_BAD : 0) | (uint64_t)(uint32_t)wt);
+    if (lane == 0 && VLC_OK(fi < a.nframes && G < ng, 4)) st_store(stw + 2 * G, ST_AGG | (wbad ? ST_BAD : 0) | (uint64_t)(uint32_t)wt);
     if (G - 1 - lane >= 0) s = st_load(stw + 2 * (G - 1 - lane));
   }
   uint32_t *wb = wbits + wv * VLC_EMIT_WORDS;
@@ -527,9 +549,9 @@ __global__ __launch_bounds__(64 * VLC_WAVES) void k_vlc_blk(VlcArgs a, VlcTables
       }
     }
     const int64_t endb = first + wt;
-    if (lane == 0) {
+    if (lane == 0 && VLC_OK(fi < a.nframes && G < ng, 4)) {
       st_store(stw + 2 * G, ST_INCL | (bad_all ? ST_BAD : 0) | (uint64_t)(uint32_t)endb);
-      if (G == ng - 1) a.bits[fi] = (bad_all || endb + 64 > a.out_words * 32) ? 0xFFFFFFFFu : (uint32_t)endb;
+      if (G == ng - 1 && VLC_OK(fi < a.nframes, 5)) a.bits[fi] = (bad_all || endb + 64 > a.out_words * 32) ? 0xFFFFFFFFu : (uint32_t)endb;
       s_first = first;
     }
   }
@@ -563,26 +585,38 @@ __global__ __launch_bounds__(64 * VLC_WAVES) void k_vlc_blk(VlcArgs a, VlcTables
       return x;
     };
     for (int64_t gw = w0 + threadIdx.x; gw <= wl; gw += 64 * VLC_WAVES)
-      if (!(gw == w0 && sh_first) && !(gw == wl && sh_last)) out[gw] = word(gw);
+      if (!(gw == w0 && sh_first) && !(gw == wl && sh_last) && VLC_OK(gw >= 0 && gw < a.out_words, 0))
+        out[gw] = word(gw);
     if (wv == 0) {
       firstv = word(w0);
       lastv = word(wl);
     }
-  } else if (wt > 0) {  // a wave past its copy: zero the words, OR the codes in memory
-    for (int64_t gw = w0 + threadIdx.x; gw <= wl; gw += 64 * VLC_WAVES) out[gw] = 0;
+  } else if (wt > 0) {  // a wave past its copy: zero our words, OR the codes in memory
+    // (never a word a neighbour shares: the previous workgroup may still be
+    // ORing into it in this same path, or the next one already have; the
+    // shared words collect in s_shw and leave by the hand-over below.
+    // A big range spans > 8,000 bits, so w0 < wl.)
+    __shared__ uint32_t s_shw[2];
+    const int64_t s0 = sh_first ? w0 : -1, s1 = sh_last ? wl : -1;
+    if (threadIdx.x < 2) s_shw[threadIdx.x] = 0;
+    for (int64_t gw = w0 + threadIdx.x; gw <= wl; gw += 64 * VLC_WAVES)
+      if (gw != s0 && gw != s1 && VLC_OK(gw >= 0 && gw < a.out_words, 1)) out[gw] = 0;
     __threadfence();
     __syncthreads();
     if (tot > 0) {
       BitWriter bw;
+      bw.s0 = s0;
+      bw.s1 = s1;
+      bw.sh = s_shw;
+      bw.wlo = w0;
+      bw.whi = wl;
       emit(bw, out, first + off[wv]);
     }
     __threadfence();
     __syncthreads();
-    if (wv == 0) {
-      firstv = (uint32_t)__builtin_amdgcn_readfirstlane((int)__hip_atomic_load(out + w0, __ATOMIC_RELAXED,
-                                                                                __HIP_MEMORY_SCOPE_AGENT));
-      lastv = (uint32_t)__builtin_amdgcn_readfirstlane((int)__hip_atomic_load(out + wl, __ATOMIC_RELAXED,
-                                                                               __HIP_MEMORY_SCOPE_AGENT));
+    if (wv == 0) {  // (only read where shared: the others are in memory already)
+      firstv = s_shw[0];
+      lastv = s_shw[1];
     }
   }
   if (wv != 0) return;
@@ -593,14 +627,14 @@ __global__ __launch_bounds__(64 * VLC_WAVES) void k_vlc_blk(VlcArgs a, VlcTables
     if (sh_first) v |= (uint32_t)st_wait(stw + 2 * (G - 1) + 1);
     if (sh_last) {
       if (lane == 0) st_store(stw + 2 * G + 1, (1ull << 63) | v);
-    } else if ((wt > 0 || sh_first) && lane == 0) {
+    } else if ((wt > 0 || sh_first) && lane == 0 && VLC_OK(w0 >= 0 && w0 < a.out_words, 3)) {
       out[w0] = v;
     }
   } else {
     if (sh_last && lane == 0) st_store(stw + 2 * G + 1, (1ull << 63) | lastv);
     if (sh_first) {
       const uint32_t pv = (uint32_t)st_wait(stw + 2 * (G - 1) + 1);
-      if (lane == 0) out[w0] = firstv | pv;
+      if (lane == 0 && VLC_OK(w0 >= 0 && w0 < a.out_words, 3)) out[w0] = firstv | pv;
     }
   }
 }
@@ -613,6 +647,18 @@ thread_local bool g_len_ok = false;
 }  // namespace
 
 extern "C" {
+
+#ifdef P64_VLC_CHECK
+// (bounds-checked build only) the sites k_vlc_blk found out of range since
+// the last call (bit i = site i of VLC_OK), then cleared; synchronises
+int p64gpu_vlc_check_errors_(uint32_t *err) {
+  const uint32_t z = 0;
+  if (hipDeviceSynchronize() != hipSuccess || hipMemcpyFromSymbol(err, HIP_SYMBOL(g_vlc_err), 4) != hipSuccess ||
+      hipMemcpyToSymbol(HIP_SYMBOL(g_vlc_err), &z, 4) != hipSuccess)
+    return p64gpu_fail_(P64GPU_E_HIP, "vlc check: symbol copy");
+  return P64GPU_OK;
+}
+#endif
 
 int64_t p64gpu_vlc_max_bytes(int width, int height) {
   const int64_t nmb = (int64_t)(width / 16) * (height / 16);
@@ -671,7 +717,7 @@ int p64gpu_vlc_pictures(const p64gpu_vlc_args *x, void *stream) {
     a.bits = x->bits + f0;
     // this chunk's [6][nc][nmb] words of the scratch
     uint32_t *scr = x->scratch + 6 * m0;
-    a.status = scr;  // 4 words per workgroup of a picture
+    a.status = scr;  // [nc][nwg][2] uint64: the look-back word and the tail
     const int nwg = (nmb + VLC_WAVES * VLC_MBS - 1) / (VLC_WAVES * VLC_MBS);  // workgroups per picture
     const dim3 grid((unsigned)nwg, (unsigned)nc);
     hipError_t me = hipMemsetAsync(scr, 0, (size_t)nc * nwg * 16, st);

@@ -73,6 +73,17 @@ class Writer:
                                         qm.ctypes.data if qm is not None else None,
                                         mb.ctypes.data, coef.ctypes.data))
 
+    def write_bits(self, data, bits: int, phase: int) -> None:
+        """Appends a picture coded on the GPU (vlc_pictures) at bit `phase` of
+        data[0]: phase must be this writer's phase(), bits counts the phase
+        bits too (p64s_write_bits)."""
+        buf = np.frombuffer(bytes(data[:(bits + 7) // 8]), np.uint8)
+        _check(lib().p64s_write_bits(self._h, buf.ctypes.data if buf.size else None, int(bits), int(phase)))
+
+    def phase(self) -> int:
+        """The stream's position within its current byte (0..7)."""
+        return int(lib().p64s_writer_phase(self._h))
+
     def bits(self) -> int:
         n, b = ctypes.c_size_t(), ctypes.c_int64()
         lib().p64s_writer_data(self._h, ctypes.byref(n), ctypes.byref(b))

@@ -20,6 +20,20 @@ def free_port():
     return p
 
 
+def queue_get(q, procs, timeout=240):
+    """The result a worker puts on q; fails at once when a worker died first."""
+    import queue
+    import time
+    t0 = time.time()
+    while time.time() - t0 < timeout:
+        try:
+            return q.get(timeout=2)
+        except queue.Empty:
+            dead = [p.exitcode for p in procs if p.exitcode not in (None, 0)]
+            assert not dead, f"a worker exited with {dead}"
+    raise AssertionError("no result from the workers")
+
+
 def encode_digest(seed, w=176, h=144, nframes=2):
     """Per-sequence work stand-in: the CPU oracle encoding one short sequence."""
     import sys
@@ -278,3 +292,96 @@ def test_two_rank_root_feed_gathers_coded_streams():
     assert len(got) == world * S
     for i in range(world * S):
         assert got[i] == coded_sequence(oracle, p64_amd, stream, 1 + i, 176, 144), i
+
+
+def picture_piece(stream, fmt, tr, mb, coef, q, phase):
+    """CPU stand-in for the GPU coder's output (p64gpu_vlc_pictures): one
+    picture's bits from bit `phase` of byte 0 (the phase bits zero), padded
+    to a byte, and the bit count including the phase."""
+    wr = stream.Writer(fmt)
+    if phase:
+        wr.write_bits(b"\0", phase, 0)
+    wr.write_picture(tr, mb, coef, q)
+    nbits = wr.bits()
+    if wr.phase():
+        wr.write_bits(b"\0", 8, wr.phase())
+    return wr.data(), nbits
+
+
+def _pieces_worker(rank, world, port, S, n, q):
+    """--feed root, coded, as bench.py runs it: every step each rank codes
+    its sequences' next picture at each sequence's running bit phase and
+    gathers the pieces to rank 0 (bench.gather_coded, sized by the MAX
+    all-reduce of the longest piece); rank 0 stitches them per sequence
+    (bench.stitch_pieces)."""
+    import sys
+    sys.path.insert(0, REPO)
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import torch
+
+    import bench
+    import oracle
+    import p64_amd
+    from p64_amd import stream
+
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
+                            world_size=world)
+    w, h = 176, 144
+    fmt = stream.format_of(w, h)
+    seed0, _ = bench.shard_seeds(rank, S)
+    recs = []
+    for k in range(S):
+        frames = [p64_amd.synth_frame(seed0 + k, t, w, h, content=p64_amd.SYNTH_SURVEY) for t in range(n)]
+        recs.append(oracle.encode_sequence(frames, w, h, quant=8, me_mode=1, search_limit=31))
+    seq_bits = [0] * S
+    writers = {g: stream.Writer(fmt) for g in range(world * S)} if rank == 0 else None
+    stride = 16384 + 64 * rank  # (ranks' buffers differ in size)
+    for t in range(n):
+        out = torch.zeros((S, stride), dtype=torch.uint8)
+        bits = torch.zeros(S, dtype=torch.int32)
+        for k in range(S):
+            coef, mb, _, _ = recs[k][t]
+            data, nb = picture_piece(stream, fmt, t % 32, mb, coef, 8, seq_bits[k] & 7)
+            out[k, :len(data)] = torch.frombuffer(bytearray(data), dtype=torch.uint8)
+            bits[k] = nb
+            seq_bits[k] += nb - (seq_bits[k] & 7)
+        mx = bits.to(torch.int64).max().reshape(1) if t % 2 else None  # (both ways to the size)
+        got = bench.gather_coded(world, rank, out, bits, mx=mx)
+        if rank == 0:
+            pays, bls = got
+            pieces = {r * S + i: pays[r][i].numpy().tobytes() for r in range(world) for i in range(S)}
+            nbits = {r * S + i: int(bls[r][i]) for r in range(world) for i in range(S)}
+            bench.stitch_pieces(writers, pieces, nbits)
+        else:
+            assert got is None
+    if rank == 0:
+        q.put([writers[g].end(n % 32) for g in range(world * S)])
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_root_feed_stitches_per_picture_pieces():
+    """The fed path's per-picture pieces, each coded at its sequence's bit
+    phase, gathered step by step from two ranks and stitched on rank 0 equal
+    the .p64 a single process writes for the same sequences (p64.c:524-613,
+    stream.c:142-150)."""
+    import sys
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle
+    import p64_amd
+    from p64_amd import stream
+
+    world, S, n = 2, 2, 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=_pieces_worker, args=(r, world, port, S, n, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = queue_get(q, procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert len(got) == world * S
+    for i in range(world * S):
+        assert got[i] == coded_sequence(oracle, p64_amd, stream, 1 + i, 176, 144, n=n), i

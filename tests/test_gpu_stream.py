@@ -405,3 +405,109 @@ def test_gpu_vlc_graph_replay(p64, torch_dev):
         for t in range(mb.shape[0]):
             nb = (bits[t] + 7) // 8
             np.testing.assert_array_equal(out[t, :nb], out0[t, :nb])
+
+
+@pytest.mark.parametrize("given", [False, True])
+def test_gpu_vlc_big_path_stress(p64, torch_dev, given):
+    """The coder's big path (a wave past its 8,160-bit LDS copy writes its
+    words straight into memory) next to big and small neighbours, in many
+    pictures per launch at every phase: dense random levels (escapes, up to
+    ~5,000 bits per MB) in some 40-MB stretches, sparse ones in others.
+    Every picture equals the host writer bit for bit, over repeated launches
+    (the round-5 big path zeroed and ORed the words it shares with its
+    neighbours in memory: a race; tests/test_vlc_protocol.py
+    models the interleavings)."""
+    from p64_amd import stream
+    torch = torch_dev
+    w, h, n, nmb, ngob = 352, 288, 48, 396, 12
+    rng = np.random.default_rng(11)
+    mb = np.zeros((n, nmb, 4), np.int8)
+    mb[..., 1] = 0x3f
+    coef = np.zeros((n, nmb, 6, 64), np.int16)
+    for t in range(n):
+        dense = rng.random(nmb // 20 + 1) < 0.5  # stretches of 20 raster MBs
+        for k in range(nmb):
+            if dense[k // 20]:
+                coef[t, k] = rng.integers(-127, 128, (6, 64))
+                coef[t, k, :, rng.integers(1, 64, 6)] = 0
+            else:
+                coef[t, k, rng.integers(0, 6, 2), rng.integers(1, 64, 2)] = rng.integers(-3, 4, 2)
+            coef[t, k, :, 0] = rng.integers(1, 255, 6)
+    gq = np.full((n, ngob), 1, np.uint8)
+    tr = np.arange(n, dtype=np.int32) % 32
+    d = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()  # noqa: E731
+    mbd, cd = d(mb), d(coef)
+    host = []
+    for t in range(n):
+        wr = stream.Writer(stream.CIF)
+        wr.write_picture(int(tr[t]), mb[t], coef[t], gq[t])
+        host.append((wr.bits(), wr.data()))
+    kw = {}
+    if given:
+        vb = torch.zeros((n, nmb, 8), dtype=torch.int16, device="cuda")
+        assert p64.lib().p64gpu_vlc_block_bits_(w, h, n, ctypes_ptr(mbd), ctypes_ptr(cd), ctypes_ptr(vb),
+                                                None) == 0
+        kw["blk_bits"] = vb
+    bufs = stream.vlc_buffers(n, w, h)
+    for rep in range(4):
+        phases = rng.integers(0, 8, n).astype(np.uint8)
+        bufs[0].fill_(0xA5)  # (stale bytes: every word up to the last bit must be written)
+        out, bits = stream.vlc_pictures(mbd, cd, d(gq), d(tr), width=w, height=h, phase=d(phases),
+                                        buffers=bufs, **kw)
+        out = out.cpu().numpy()
+        for t in range(n):
+            hb, full = host[t]
+            assert bits[t] - int(phases[t]) == hb, (rep, t)
+            nb = (bits[t] + 7) // 8
+            gpu = int.from_bytes(out[t, :nb].tobytes(), "big") >> (nb * 8 - bits[t])
+            assert gpu >> hb == 0, (rep, t)
+            assert gpu >> (hb - 8 * len(full)) == int.from_bytes(full, "big"), (rep, t)
+
+
+@pytest.mark.parametrize("given", [False, True])
+def test_fed_path_stitched_streams(p64, torch_dev, tmp_path, given):
+    """bench.py --feed root --gather coded at world 1: each step's pictures
+    coded on the GPU at their sequences' bit phases (bench.CodedFeed), gathered
+    one step late on the side stream, stitched on rank 0 (stitch_pieces):
+    byte-identical to the host writer over the same records
+    (p64s_write_picture) and to the .p64 the CLI writes for those pictures
+    (p64.c:524-613, stream.c:142-150, 193)."""
+    import sys
+    sys.path.insert(0, REPO)
+    import bench
+    from p64_amd import stream
+    torch = torch_dev
+    w, h, S, n = 352, 288, 4, 6
+    nmb, pic = 396, w * h * 3 // 2
+    fr = p64.synth_frames_device(w, h, 3, S, 0, n, content=p64.SYNTH_SURVEY)
+    rec = [torch.zeros(S * pic, dtype=torch.uint8, device="cuda") for _ in range(2)]
+    li = torch.zeros(S * nmb, dtype=torch.uint8, device="cuda")
+    out = p64.FrameBatchOut(coef=torch.zeros((S, nmb, 6, 64), dtype=torch.int16, device="cuda"),
+                            mb=torch.empty((S, nmb, 4), dtype=torch.int8, device="cuda"),
+                            me=torch.empty((S, nmb, 7), dtype=torch.int32, device="cuda"),
+                            vlc_bits=(torch.empty((S, nmb, 8), dtype=torch.int16, device="cuda")
+                                      if given else None))
+    feed = bench.CodedFeed(torch, stream, 1, 0, S, w, h, 8, keep=range(S))
+    fmt = stream.format_of(w, h)
+    host = [stream.Writer(fmt) for _ in range(S)]
+    for t in range(n):
+        p64.encode_frames(fr[t].reshape(-1), rec[(t + 1) % 2], rec[t % 2], li, width=w, height=h,
+                          intra=(t == 0), quant=8, me_mode=p64.ME_FULL, search_limit=31, out=out)
+        feed.code(t, out)
+        mb, coef = out.mb.cpu().numpy(), out.coef.cpu().numpy()
+        for s in range(S):
+            host[s].write_picture(t % 32, mb[s], coef[s], 8)
+        out.coef.zero_()  # (inter pictures store only their nonzero blocks)
+    feed.finish()
+    got = feed.streams(fmt, n % 32)
+    for s in range(S):
+        data, nbits = got[s]
+        assert nbits == host[s].bits(), s
+        assert data == host[s].end(n % 32), s
+    frames = fr.cpu().numpy()
+    for s in (0, S - 1):
+        write_y4m(tmp_path / f"in{s}.y4m", [frames[t, s] for t in range(n)], w, h)
+        subprocess.run([CLI, "-CIF", "-y4m", "-a", "0", "-b", str(n - 1), "-q", "8", "-i", "31", "-full",
+                        str(tmp_path / f"in{s}"), "-z", ".y4m", "-s", str(tmp_path / f"o{s}.p64")],
+                       check=True, stdout=subprocess.DEVNULL, timeout=300)
+        assert (tmp_path / f"o{s}.p64").read_bytes() == got[s][0], s
