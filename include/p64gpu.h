@@ -241,9 +241,14 @@ int p64gpu_decode_recon(int width, int height, int nframes, int64_t frame_stride
  * byte -- the bit position the sequence's stream has reached -- so the host
  * appends it by OR-ing the first byte into its pending byte.  bits[i] receives
  * the bit count including the phase, or 0xFFFFFFFF if a record was invalid.
- * All pointers are device pointers; scratch holds 6*nframes*nmb uint32 and is
- * 8-byte aligned, coef 16-byte, mb 4-byte (else P64GPU_E_INVALID).  Batches
- * whose levels exceed 2 GiB are coded in several launches. */
+ * Every pointer must be device-addressable: device memory, managed memory, or
+ * host memory pinned by hipHostMalloc/hipHostRegister (e.g. `bits` straight
+ * into pinned host memory, also under graph capture and replay: the kernel is
+ * given the device pointer HIP reports for it); pageable host memory is
+ * refused with P64GPU_E_INVALID (hipPointerGetAttributes, every call).
+ * scratch holds 6*nframes*nmb uint32 and is 8-byte aligned, coef 16-byte, mb
+ * 4-byte (else P64GPU_E_INVALID).  Batches whose levels exceed 2 GiB are
+ * coded in several launches. */
 typedef struct {
   int width, height, nframes;
   int flags;                /* 0 (was `reserved` before ABI version 2)        */

@@ -639,6 +639,26 @@ __global__ __launch_bounds__(64 * VLC_WAVES) void k_vlc_blk(VlcArgs a, VlcTables
   }
 }
 
+// Every pointer of p64gpu_vlc_args must be memory the device can address:
+// device memory, host memory pinned by hipHostMalloc / hipHostRegister (torch
+// pin_memory) or managed memory.  Pinned host memory is addressed through the
+// device pointer HIP reports for it (the same address for hipHostMalloc,
+// measured: tools/vlc_fault_probe.py stage A); pageable host memory
+// (hipMemoryTypeUnregistered), which the kernel's stores would fault on, is
+// refused.  Returns the pointer to pass to the kernel, or nullptr.
+template <class T>
+T *device_addressable(T *p) {
+  if (!p) return p;
+  hipPointerAttribute_t at;
+  if (hipPointerGetAttributes(&at, (const void *)p) != hipSuccess) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  if (at.type == hipMemoryTypeDevice || at.type == hipMemoryTypeManaged) return p;
+  if (at.type == hipMemoryTypeHost && at.devicePointer) return reinterpret_cast<T *>(at.devicePointer);
+  return nullptr;
+}
+
 thread_local VlcTables g_tab;
 thread_local bool g_tab_ok = false;
 thread_local p64k::VlcLenTab g_len;  // the count's code lengths (p64gpu_vlc_len_table_)
@@ -682,6 +702,14 @@ int p64gpu_vlc_pictures(const p64gpu_vlc_args *x, void *stream) {
       ((uintptr_t)x->blk_bits & 15))
     return p64gpu_fail_(P64GPU_E_INVALID,
                         "vlc: scratch must be 8-byte, coef and blk_bits 16-byte, mb 4-byte aligned");
+  p64gpu_vlc_args y = *x;  // the pointers as the device addresses them
+#define VLC_ADDR(f)                                                                                         \
+  if (x->f && !(y.f = device_addressable(x->f)))                                                            \
+    return p64gpu_fail_(P64GPU_E_INVALID, "vlc: " #f " is not device-addressable memory (pageable host memory?)");
+  VLC_ADDR(mb) VLC_ADDR(coef) VLC_ADDR(gquant) VLC_ADDR(mquant) VLC_ADDR(tr) VLC_ADDR(phase) VLC_ADDR(out)
+  VLC_ADDR(bits) VLC_ADDR(scratch) VLC_ADDR(blk_bits)
+#undef VLC_ADDR
+  x = &y;
   if (!g_len_ok) {  // (fills g_tab too)
     const int s = p64gpu_vlc_len_table_(g_len.w);
     if (s) return s;

@@ -511,3 +511,60 @@ def test_fed_path_stitched_streams(p64, torch_dev, tmp_path, given):
                         str(tmp_path / f"in{s}"), "-z", ".y4m", "-s", str(tmp_path / f"o{s}.p64")],
                        check=True, stdout=subprocess.DEVNULL, timeout=300)
         assert (tmp_path / f"o{s}.p64").read_bytes() == got[s][0], s
+
+
+def test_gpu_vlc_bits_in_pinned_host_memory(p64, torch_dev):
+    """p64gpu_vlc_args.bits in hipHostMalloc'd (pinned) host memory: the coder
+    writes the bit counts there directly, eagerly and captured in a HIP graph
+    replayed several times (the round-5 with_vlc variant that ended in an
+    illegal-address fault wrote them into a torch pin_memory tensor;
+    tools/vlc_fault_probe.py reconstructs it).  Pageable host memory is
+    refused by the ABI (include/p64gpu.h), not handed to the kernel."""
+    import ctypes
+    from p64_amd import stream
+    torch = torch_dev
+    z = load("seq_qcif_full31.npz")
+    mb, coef, gq, uq = fixture_records(z, stream.format_of(176, 144))
+    n = mb.shape[0]
+    d = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()  # noqa: E731
+    tr = d(np.arange(n, dtype=np.int32) % 32)
+    mbd, cd, gqd, uqd = d(mb), d(coef), d(gq), d(uq)
+    _, want = stream.vlc_pictures(mbd, cd, gqd, tr, width=176, height=144, mquant=uqd)
+    hip = None
+    with open("/proc/self/maps") as f:
+        for line in f:
+            if "libamdhip64" in line:
+                hip = ctypes.CDLL(line.split()[-1])
+                break
+    hp = ctypes.c_void_p()
+    assert hip.hipHostMalloc(ctypes.byref(hp), ctypes.c_size_t(4 * n), 0) == 0
+    try:
+        host = np.frombuffer((ctypes.c_uint32 * n).from_address(hp.value), np.uint32)
+        out, _, scr = stream.vlc_buffers(n, 176, 144)
+
+        def call(bits_ptr):
+            a = stream.VlcArgs(width=176, height=144, nframes=n, flags=0, mb=mbd.data_ptr(), coef=cd.data_ptr(),
+                               gquant=gqd.data_ptr(), mquant=uqd.data_ptr(), tr=tr.data_ptr(), phase=None,
+                               out=out.data_ptr(), out_stride=int(out.shape[1]), bits=bits_ptr,
+                               scratch=scr.data_ptr(), blk_bits=None)
+            return p64.lib().p64gpu_vlc_pictures(ctypes.byref(a), p64._stream(torch))
+
+        host[:] = 0
+        assert call(hp.value) == 0
+        torch.cuda.synchronize()
+        assert host.tolist() == list(want)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            assert call(hp.value) == 0
+        for _ in range(3):
+            host[:] = 0
+            g.replay()
+            torch.cuda.synchronize()
+            assert host.tolist() == list(want)
+        del g
+        pageable = np.zeros(n, np.uint32)
+        assert call(pageable.ctypes.data) == -1  # P64GPU_E_INVALID
+        assert b"device-addressable" in p64.lib().p64gpu_last_error()
+        assert not pageable.any()
+    finally:
+        hip.hipHostFree(hp)
