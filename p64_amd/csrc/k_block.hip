@@ -1173,7 +1173,7 @@ __device__ __forceinline__ void pred_rows(const PredSrc &P, bool filter, uint2 p
 // POW2: a uniform q whose D = 16q is a power of two (qlevel_pk2)
 template <bool QMB, bool OVR, bool POW2 = false, bool BITS = false>
 __global__ __launch_bounds__(64) OCC4 void k_inter_mbg(p64gpu_encode_args a, BlkDiv kd, unsigned nmbs,
-                                                             const p64_me_rec *me, VlcLenTab vt) {
+                                                             p64_me_rec *me, VlcLenTab vt) {
   __shared__ __align__(16) uint8_t lds[LVL_WAVE];
   __shared__ uint32_t vlen[BITS ? VLC_LEN_WORDS : 1];
   const int lane = threadIdx.x;
@@ -1193,14 +1193,11 @@ __global__ __launch_bounds__(64) OCC4 void k_inter_mbg(p64gpu_encode_args a, Blk
       __builtin_amdgcn_make_buffer_rsrc((void *)me, (short)0, (int)(nmbs * sizeof(p64_me_rec)), BUF_RSRC_W3);
   const uint32_t mo = gmb * (uint32_t)sizeof(p64_me_rec);
   InterMe m;
-  const auto r0 = __builtin_amdgcn_raw_buffer_load_b128(mer, mo, 0, 0);    // mx my sad sad0
-  const auto r1 = __builtin_amdgcn_raw_buffer_load_b64(mer, mo + 16, 0, 0);  // var varor
+  const auto r0 = __builtin_amdgcn_raw_buffer_load_b128(mer, mo, 0, 0);  // mx my sad sad0
   m.mx = (int)r0[0];
   m.my = (int)r0[1];
   m.sad = (int)r0[2];
   m.sad0 = (int)r0[3];
-  m.var = (int)r1[0];
-  m.varor = (int)r1[1];
   // LastIntra and the -o override by buffer loads (an absent override array
   // reads as out of range: no branch around a load)
   const __amdgpu_buffer_rsrc_t lir =
@@ -1210,6 +1207,44 @@ __global__ __launch_bounds__(64) OCC4 void k_inter_mbg(p64gpu_encode_args a, Blk
   const int li = __builtin_amdgcn_raw_buffer_load_b8(lir, gmb, 0, 0);
   const int ov = OVR ? (int)(int8_t)__builtin_amdgcn_raw_buffer_load_b8(ovr, gmb, 0, 0) : -1;
   const IntraFetch f = intra_fetch_at<QMB>(a, pos);  // current rows, q
+  const int mvx = m.mx, mvy = m.my;
+  // the source at the ME vector (luma MV, chroma MV/2, as an MC type reads
+  // it): the prediction of every MC type, and on the luma lanes the block the
+  // decision statistics are taken on (round 6: moved here from k_motion,
+  // which no longer computes them for this path)
+  RecStageA A1;
+  A1.p = pos;
+  A1.m = 5u | ((uint32_t)(mvx & 0xff) << 16) | ((uint32_t)(mvy & 0xff) << 24);
+  A1.q = 0;
+  A1.coded = 1;
+  const RecStageB S1 = rec_stage_b<false>(B, w, h, stride, A1);
+  PRIO_LOW();  // the loads are out
+  // VAR, VAROR, MWOR at the chosen vector (me.c:229-245 == 313-329): per luma
+  // lane the sums over its 8x8 quadrant by byte dot products, sum (r-c)^2 =
+  // r.r - 2 r.c + c.c (exact in u32), then the MB's four luma lanes added
+  // (lanes 6m..6m+3) and the results handed to its six lanes
+  uint32_t rr = 0, rc = 0, cc = 0, rs = 0;
+#pragma unroll
+  for (int r = 0; r < 8; r++) {
+    const uint32_t w0 = align4(S1.pred.d[r][1], S1.pred.d[r][0], S1.pred.sh);
+    const uint32_t w1 = align4(S1.pred.d[r][2], S1.pred.d[r][1], S1.pred.sh);
+    const uint32_t c0 = f.rows[r].x, c1 = f.rows[r].y;
+    rr = __builtin_amdgcn_udot4(w1, w1, __builtin_amdgcn_udot4(w0, w0, rr, false), false);
+    rc = __builtin_amdgcn_udot4(w1, c1, __builtin_amdgcn_udot4(w0, c0, rc, false), false);
+    cc = __builtin_amdgcn_udot4(c1, c1, __builtin_amdgcn_udot4(c0, c0, cc, false), false);
+    rs = sad4(w1, 0u, sad4(w0, 0u, rs));
+  }
+  const bool luma = b < 4;
+  uint32_t e2 = luma ? rr + cc - 2 * rc : 0u;
+  rr = luma ? rr : 0u;
+  rs = luma ? rs : 0u;
+  e2 += __shfl_down(e2, 1) + __shfl_down(e2, 2) + __shfl_down(e2, 3);
+  rr += __shfl_down(rr, 1) + __shfl_down(rr, 2) + __shfl_down(rr, 3);
+  rs += __shfl_down(rs, 1) + __shfl_down(rs, 2) + __shfl_down(rs, 3);
+  const int src = lane - b;  // the MB's lane 0 holds its totals
+  const int var = (int)(__shfl(e2, src) / 256u);
+  const uint32_t rs_mb = __shfl(rs, src);
+  const int varor = (int)(__shfl(rr, src) / 256u) - (int)(rs_mb / 256u) * (int)(rs_mb / 256u);
 
   // MTYPE (p64.c:734-772): the decision, the -o override, the intra refresh
   MeOut mo_;
@@ -1217,15 +1252,44 @@ __global__ __launch_bounds__(64) OCC4 void k_inter_mbg(p64gpu_encode_args a, Blk
   mo_.my = m.my;
   mo_.sad = m.sad;
   mo_.sad0 = m.sad0;
-  mo_.var = m.var;
-  mo_.varor = m.varor;
-  mo_.mwor = 0;
+  mo_.var = var;
+  mo_.varor = varor;
+  mo_.mwor = (int)rs_mb;
   int mt = decide_mtype(mo_);
   if (ov >= 0) mt = ov;
   if (li > 131) mt = 0;
-  const int mvx = m.mx, mvy = m.my;
+  // the prediction: MC types from the source already loaded; the non-MC
+  // inter types (2, 3) from the zero vector, loaded now where the ME vector
+  // is not (0,0); intra none
   uint2 prow[8];
-  inter_pred(B, w, h, stride, pos, mt, mvx, mvy, prow);  // (drops the priority)
+  {
+    const bool need0 = !mt_intra(mt) && !mt_mf(mt) && (mvx | mvy) != 0;
+    PredSrc P = S1.pred;
+    if (uni(__any(need0))) {
+      RecStageA A0;
+      A0.p = pos;
+      A0.m = 2u;
+      A0.q = 0;
+      A0.coded = need0 ? 1 : 0;  // (others: out of range, no traffic)
+      const RecStageB S0 = rec_stage_b<false>(B, w, h, stride, A0);
+      if (need0) P = S0.pred;
+    }
+    pred_rows(P, mt_filter(mt), prow);
+    if (mt_intra(mt)) {
+#pragma unroll
+      for (int r = 0; r < 8; r++) prow[r] = make_uint2(0u, 0u);
+    }
+  }
+  // the statistics into the ME record (p64_me_rec var, varor, mwor)
+  {
+    const bool rl0 = b == 0 && lane < 6 * MBS_PER_WAVE && gmb0 + (unsigned)(l / 6) < nmbs;
+    typedef unsigned int u32x3 __attribute__((ext_vector_type(3)));
+    u32x3 st;
+    st[0] = (uint32_t)var;
+    st[1] = (uint32_t)varor;
+    st[2] = rs_mb;
+    __builtin_amdgcn_raw_buffer_store_b96(st, mer, rl0 ? mo + 16 : BUF_OOB, 0, 0);
+  }
 
   const bool intra = mt_intra(mt), tc = mt_tcoeff(mt);
   const int q = f.q;
@@ -1435,7 +1499,7 @@ hipError_t intra_mbg(const p64gpu_encode_args &a, const uint32_t *vlc_len, hipSt
 }
 
 template <bool BITS>
-static void inter_launch(const p64gpu_encode_args &a, const p64_me_rec *me, const VlcLenTab &vt, dim3 grid,
+static void inter_launch(const p64gpu_encode_args &a, p64_me_rec *me, const VlcLenTab &vt, dim3 grid,
                          dim3 block, BlkDiv kd, unsigned nm, hipStream_t st) {
   const bool ovr = a.mtype_override != nullptr;
   // a uniform q with D = 16q a power of two: the packed quantiser (multiplier 1)
@@ -1455,7 +1519,7 @@ static void inter_launch(const p64gpu_encode_args &a, const p64_me_rec *me, cons
     hipLaunchKernelGGL((k_inter_mbg<false, false, false, BITS>), grid, block, 0, st, a, kd, nm, me, vt);
 }
 
-hipError_t inter_mbg(const p64gpu_encode_args &a, const p64_me_rec *me, const uint32_t *vlc_len, hipStream_t st) {
+hipError_t inter_mbg(const p64gpu_encode_args &a, p64_me_rec *me, const uint32_t *vlc_len, hipStream_t st) {
   const unsigned nm = (unsigned)((int64_t)a.nframes * (a.width / 16) * (a.height / 16));
   const dim3 grid(mbg_workgroups(nm, 1)), block(64);
   const BlkDiv kd = blk_div(a.width, a.height);

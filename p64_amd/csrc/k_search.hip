@@ -797,9 +797,13 @@ __device__ __forceinline__ void me_stats(const Sx &S, int lane, MeOut &o) {
 }
 
 
+// stats: the decision statistics too (me_stats); the split encoder's
+// k_inter_mbg computes them itself from its prediction source (round 6), so
+// its k_motion launch leaves them out (uniform)
 template <class G, int MODE, bool PRE = false>  // MODE 1 = TSS, 2 = FULL
 __device__ __forceinline__ MeOut motion_estimate(const Sx &S, const uint8_t *cur_y, int w, int h,
-                                                 int x0, int y0, int sl, int lane, const CurMap &pre = CurMap{}) {
+                                                 int x0, int y0, int sl, int lane, const CurMap &pre = CurMap{},
+                                                 bool stats = true) {
   MeOut o;
   if (MODE == 2) {
     if (sl <= 15)  // (uniform: one search limit per launch)
@@ -815,10 +819,13 @@ __device__ __forceinline__ MeOut motion_estimate(const Sx &S, const uint8_t *cur
   o.mx = uni(o.mx);
   o.my = uni(o.my);
   o.sad = uni(o.sad);
-  me_stats<G>(S, lane, o);
-  o.var = uni(o.var);
-  o.varor = uni(o.varor);
-  o.mwor = uni(o.mwor);
+  o.var = o.varor = o.mwor = 0;
+  if (stats) {
+    me_stats<G>(S, lane, o);
+    o.var = uni(o.var);
+    o.varor = uni(o.varor);
+    o.mwor = uni(o.mwor);
+  }
   return o;
 }
 
@@ -1169,11 +1176,14 @@ __global__ __launch_bounds__(64, 1) void k_encode(p64gpu_encode_args a, const in
   encode_mb<MODE>(a, a.cur, L, lane, gid, kd, f);
 }
 
-// ME only (MotionEstimation me.c:340-363 over a batch of luma planes)
+// ME only (MotionEstimation me.c:340-363 over a batch of luma planes).
+// stats = 0 (the split encoder, whose k_inter_mbg computes VAR / VAROR /
+// MWOR from the prediction source it loads anyway): those fields are not
+// written here
 template <int MODE>
 __global__ __launch_bounds__(64, 1) void k_motion(int w, int h, int64_t stride, const uint8_t *ref_y,
                                                const uint8_t *cur_y, int sl, p64_me_rec *out,
-                                               MbDiv kd) {
+                                               MbDiv kd, int stats) {
   __shared__ MbLds L;
   const int lane = threadIdx.x;
   const int mbw = w >> 4, nmb = mbw * (h >> 4);
@@ -1205,18 +1215,22 @@ __global__ __launch_bounds__(64, 1) void k_motion(int w, int h, int64_t stride, 
   __syncthreads();
   SECTION("m_fetched");
   const MeOut me = motion_estimate<Geo1, MODE, MODE == 2>(sx_of(L), cur_y + (size_t)fi * stride, w, h, x0, y0,
-                                                          sl, lane, cmap);
+                                                          sl, lane, cmap, stats != 0);
   SECTION("m_me_done");
   if (lane == 0) {
-    p64_me_rec o;
-    o.mx = me.mx;
-    o.my = me.my;
-    o.sad = me.sad;
-    o.sad0 = me.sad0;
-    o.var = me.var;
-    o.varor = me.varor;
-    o.mwor = me.mwor;
-    out[gid] = o;
+    if (stats) {
+      p64_me_rec o;
+      o.mx = me.mx;
+      o.my = me.my;
+      o.sad = me.sad;
+      o.sad0 = me.sad0;
+      o.var = me.var;
+      o.varor = me.varor;
+      o.mwor = me.mwor;
+      out[gid] = o;
+    } else {
+      *reinterpret_cast<int4 *>(&out[gid].mx) = make_int4(me.mx, me.my, me.sad, me.sad0);
+    }
   }
 }
 
@@ -1238,14 +1252,14 @@ hipError_t encode_fused(int mode, unsigned grid, const p64gpu_encode_args &a, co
 }
 
 hipError_t motion(int mode, int w, int h, int nframes, int64_t stride, const uint8_t *ref_y,
-                  const uint8_t *cur_y, int sl, p64_me_rec *out, hipStream_t st) {
+                  const uint8_t *cur_y, int sl, p64_me_rec *out, bool stats, hipStream_t st) {
   const unsigned grid = (unsigned)((int64_t)nframes * (w / 16) * (h / 16));
   if (mode == 2)
     hipLaunchKernelGGL(k_motion<2>, dim3(grid), dim3(64), 0, st, w, h, stride, ref_y, cur_y, sl, out,
-                       mb_div(w, h));
+                       mb_div(w, h), (int)stats);
   else
     hipLaunchKernelGGL(k_motion<1>, dim3(grid), dim3(64), 0, st, w, h, stride, ref_y, cur_y, sl, out,
-                       mb_div(w, h));
+                       mb_div(w, h), (int)stats);
   return hipGetLastError();
 }
 

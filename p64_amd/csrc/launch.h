@@ -18,14 +18,14 @@ hipError_t encode_fused(int mode, unsigned grid, const p64gpu_encode_args &a, co
                         hipStream_t st);
 // ME records of every macroblock of nframes luma planes (mode 1 TSS, 2 FULL)
 hipError_t motion(int mode, int w, int h, int nframes, int64_t stride, const uint8_t *ref_y,
-                  const uint8_t *cur_y, int sl, p64_me_rec *out, hipStream_t st);
+                  const uint8_t *cur_y, int sl, p64_me_rec *out, bool stats, hipStream_t st);
 
 // k_block.hip -- one lane per 8x8 block, 10 macroblocks per wave.  Every
 // buffer of one launch lies within 2 GiB (32-bit buffer offsets).
 // vlc_len: VLC_LEN_WORDS dwords, the code-length table of
 // p64gpu_vlc_len_table_ (vlc_count.h; read only when a.vlc_bits is given)
 hipError_t intra_mbg(const p64gpu_encode_args &a, const uint32_t *vlc_len, hipStream_t st);
-hipError_t inter_mbg(const p64gpu_encode_args &a, const p64_me_rec *me, const uint32_t *vlc_len, hipStream_t st);
+hipError_t inter_mbg(const p64gpu_encode_args &a, p64_me_rec *me, const uint32_t *vlc_len, hipStream_t st);
 hipError_t recon_mbg(int w, int h, int nframes, int64_t stride, const uint8_t *ref, uint8_t *recon,
                      const int16_t *coef, const p64_mb_rec *mb, const uint8_t *quant_mb,
                      const uint8_t *coded_mask, hipStream_t st);

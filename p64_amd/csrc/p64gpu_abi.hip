@@ -220,7 +220,7 @@ int encode_launch(const p64gpu_encode_args *a, const int32_t *mb_list, int count
     if (a->intra || me) {
       if (!a->intra && !me_given)
         HIP_TRY(p64k::motion(mode, a->width, a->height, a->nframes, a->frame_stride, a->ref, a->cur,
-                             a->search_limit, me, st));
+                             a->search_limit, me, /*stats: k_inter_mbg's*/ false, st));
       const int chunk = pictures_per_launch(a->width, a->height, a->frame_stride);
       for (int f0 = 0; f0 < a->nframes; f0 += chunk) {
         const p64gpu_encode_args c = sub_batch(*a, f0, a->nframes - f0 < chunk ? a->nframes - f0 : chunk);
@@ -343,7 +343,7 @@ int p64gpu_motion_estimation(int w, int h, int nframes, int64_t stride, const ui
   if (!aligned(out, 4)) return fail(P64GPU_E_INVALID, "records must be 4-byte aligned");
   if (mode != P64GPU_ME_TSS && mode != P64GPU_ME_FULL) return fail(P64GPU_E_INVALID, "me mode %d", mode);
   if (sl < 1 || sl > 31) return fail(P64GPU_E_INVALID, "search_limit %d not in 1..31", sl);
-  HIP_TRY(p64k::motion(mode == P64GPU_ME_FULL ? 2 : 1, w, h, nframes, stride, ref_y, cur_y, sl, out,
+  HIP_TRY(p64k::motion(mode == P64GPU_ME_FULL ? 2 : 1, w, h, nframes, stride, ref_y, cur_y, sl, out, true,
                        (hipStream_t)stream));
   return P64GPU_OK;
 }
