@@ -1241,7 +1241,7 @@ __global__ __launch_bounds__(64) OCC4 void k_inter_mbg(p64gpu_encode_args a, Blk
   e2 += __shfl_down(e2, 1) + __shfl_down(e2, 2) + __shfl_down(e2, 3);
   rr += __shfl_down(rr, 1) + __shfl_down(rr, 2) + __shfl_down(rr, 3);
   rs += __shfl_down(rs, 1) + __shfl_down(rs, 2) + __shfl_down(rs, 3);
-  const int src = lane - b;  // the MB's lane 0 holds its totals
+  const int src = l - b;  // the MB's lane 0 holds its totals (tail lanes 60..63 copy lane 59)
   const int var = (int)(__shfl(e2, src) / 256u);
   const uint32_t rs_mb = __shfl(rs, src);
   const int varor = (int)(__shfl(rr, src) / 256u) - (int)(rs_mb / 256u) * (int)(rs_mb / 256u);
