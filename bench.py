@@ -294,10 +294,17 @@ class CodedFeed:
 
     def code(self, t, o):
         """Step t's pictures (outputs o of the encode) into bits, then the
-        gather of step t-1."""
+        gather of step t-1 (code_gpu + code_host)."""
+        self.torch.cuda.current_stream().wait_stream(self.side)  # (the gather of step t-2 has read buffer t % 2)
+        self.code_gpu(t, o)
+        self.code_host(t)
+
+    def code_gpu(self, t, o):
+        """The device work of step t's coding on the current stream (no host
+        synchronisation, capturable in a HIP graph): the pictures' bit phases,
+        the coder, the running bit counts, the longest picture.  The caller
+        has made the stream wait for the side stream first."""
         torch = self.torch
-        main = torch.cuda.current_stream()
-        main.wait_stream(self.side)  # (the gather of step t-2 has read buffer t % 2)
         k = t % 2
         ph = (self.seq_bits & 7).to(torch.uint8)
         self.phase.copy_(ph)
@@ -307,7 +314,11 @@ class CodedFeed:
         self.seq_bits.add_(bits.to(torch.int64) - self.phase.to(torch.int64))
         self.bits[k] = bits
         torch.amax(bits.to(torch.int64), dim=0, keepdim=True, out=self.mx[k])
-        self.ev[k].record(main)
+
+    def code_host(self, t):
+        """After step t's device work is issued: its event, and the gather of
+        step t-1 on the side stream."""
+        self.ev[t % 2].record(self.torch.cuda.current_stream())
         if self.pending is not None:
             self._gather(self.pending)
         self.pending = t
@@ -659,6 +670,8 @@ def load_pmc(path, workload_key):
 
 
 def timing_note(args, root=False):
+    if root and args.gather == "coded" and not args.eager:
+        return "HIP events around each step's graph replay (encode + entropy coder)"
     if args.eager or root:
         return "HIP events around each launch (kernel + launch gap)"
     return "HIP events around the replay of a graph of the K launches, / K (includes the inter-kernel boundary)"
@@ -903,8 +916,7 @@ def main(argv=None):
         mb_all = torch.empty((ncoef, S, nmb, 4), dtype=torch.int8, device="cuda")
         me = torch.empty((S, nmb, 7), dtype=torch.int32, device="cuda")
         # --feed root --gather coded: the encoder counts the coded bits for the in-step VLC
-        vb_root = (torch.empty((S, nmb, 8), dtype=torch.int16, device="cuda")
-                   if root and args.gather == "coded" else None)
+        vb_root = None  # (--feed root codes with the coder's own counts: with_vlc measures it faster)
 
         def out_of(t):
             i = slot(t) if keep else (1 if t == vt else (2 if t == last else 0))
@@ -985,6 +997,30 @@ def main(argv=None):
 
         for t in range(1 + args.warmup):  # intra picture + warmup, untimed
             step(t)
+        timed_launch, timed_post = launch, (post if root else None)
+        if feed is not None and not args.eager:
+            # --feed root, coded: each timed step's device work (encode + coder
+            # + the phase bookkeeping) captured as its own HIP graph before the
+            # region and replayed in the step, so the host issues four calls a
+            # step (scatter, replay, event, the previous step's gather) instead
+            # of ~15 launches; nothing is skipped: every graph runs once, in
+            # order, inside the timed region (the scatter and gather stay eager:
+            # they are the collectives)
+            step_graphs = {}
+            for t in range(1 + args.warmup, 1 + args.warmup + args.steps):
+                torch.cuda.synchronize()
+                gr = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(gr):
+                    launch(t)
+                    feed.code_gpu(t, out_of(t))
+                step_graphs[t] = gr
+            torch.cuda.synchronize()
+
+            def timed_launch(t):
+                torch.cuda.current_stream().wait_stream(feed.side)
+                step_graphs[t].replay()
+                feed.code_host(t)
+            timed_post = None
         # the checked sequences (VERIFY_SEQS: one of each synth seed class) after
         # the warmup, checked against the oracle after the timed region
         seqs = [i for i in VERIFY_SEQS if i < S]
@@ -992,8 +1028,8 @@ def main(argv=None):
         if rank == 0 and not args.no_verify:
             snap[vt] = snapshot(out_of(vt), me, rec[vt % 2], seqs, pic)
         t_first = 1 + args.warmup
-        elapsed, kavg, clk = timed_region(torch, dist, world, args.steps, t_first, launch,
-                                          pre if root else None, post if root else None,
+        elapsed, kavg, clk = timed_region(torch, dist, world, args.steps, t_first, timed_launch,
+                                          pre if root else None, timed_post,
                                           graph=not args.eager, spinup_ms=args.spinup_ms,
                                           spin={"init": spin_init, "reset": spin_reset,
                                                 "launch": spin_launch,
@@ -1092,7 +1128,9 @@ def main(argv=None):
                                        f"dp{world} (rank 0 RCCL-scatters pictures, gathers "
                                        + ("the entropy-coded pictures (GPU VLC on each rank in the step)"
                                           if args.gather == "coded" else "levels + records")
-                                       + "; roofline times the encode launch alone)")},
+                                       + ("; roofline times each step's device work: encode + coder, one "
+                                          "graph replay per step" if feed is not None and not args.eager
+                                          else "; roofline times the encode launch alone") + ")")},
             "roofline": roofline(mbs_launch * BYTES_PER_MB_FIXED + lvl_bytes, kavg, kernel, pmc,
                                  algorithmic_bytes_per_mb=round(BYTES_PER_MB_FIXED + lvl_bytes / mbs_launch, 1),
                                  timing=timing_note(args, root),
@@ -1288,8 +1326,8 @@ def measure_vlc(args, torch, p64_amd, enc, S, nmb, w, h):
         trs = [torch.full((S,), (1 + args.warmup + k) % 32, dtype=torch.int32, device="cuda")
                for k in range(vsteps)]
         host = torch.empty((vsteps, S), dtype=torch.int32, pin_memory=True)
-        p64s.vlc_pictures(outs[0].mb, outs[0].coef, gq, trs[0], width=w, height=h,
-                          buffers=bufs)  # first call: table upload
+        p64s.vlc_pictures(outs[0].mb, outs[0].coef, gq, trs[0], width=w, height=h, buffers=bufs,
+                          host_bits=False)  # first call: table upload (records not yet written)
         torch.cuda.synchronize()
         vlc_ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
         side = torch.cuda.Stream()
@@ -1527,7 +1565,12 @@ def encode_all(args, torch, p64_amd, frames, S, nmb, pic, nslots, mode):
 def run_decode(args, torch, dist, np, p64_amd, world, enc, S, nmb, pic):
     """configs[4]: decoder reconstruction of every encoded picture in order
     (closed loop from the decoded picture 0); the last decoded picture must equal
-    the encoder's reconstruction of it, for every sequence."""
+    the encoder's reconstruction of it, for every sequence.  The levels go to
+    the decoder PACKED (p64gpu_decode_recon_packed, ABI v3: the transmitted
+    blocks only + a per-64-block index, what p64s_pack_levels makes of the
+    host reader's output; built here on the device from the encoder's levels,
+    outside the timed region) -- the line's kernel is k_recon_pk; the dense
+    entry (k_recon_mbg) is timed the same way beside it (`dense`)."""
     w, h = args.width, args.height
     ncoef = enc["coef"].shape[0]
     last = enc["last"]
@@ -1536,38 +1579,52 @@ def run_decode(args, torch, dist, np, p64_amd, world, enc, S, nmb, pic):
                 "error": f"decode needs all {last + 1} steps' levels resident (MAX_SLOTS {ncoef})"}
     qmb = torch.full((S * nmb,), args.quant, dtype=torch.uint8, device="cuda")
     mask = torch.ones(S * nmb, dtype=torch.uint8, device="cuda")
-    dec = [torch.zeros(S * pic, dtype=torch.uint8, device="cuda") for _ in range(2)]
-    nbytes = []
-
-    def step(t):
-        p64_amd.decode_recon(dec[(t + 1) % 2], dec[t % 2], enc["coef"][t], enc["mb"][t], qmb, mask,
-                             width=w, height=h)
-
     first = last - args.steps + 1
-    for t in range(first):  # pictures before the timed ones, untimed
-        step(t)
+    # the packed layout of every picture (the reader's job in a decoder)
+    pk = {}
+    for t in range(last + 1):
+        lv, n, ix = p64_amd.pack_levels_device(enc["coef"][t], enc["mb"][t], mask, w, h)
+        pk[t] = (lv if n else torch.zeros((1, 64), dtype=torch.int16, device="cuda"), n, ix)
+    nbytes = []
+    ngr = (6 * nmb + 63) // 64
     for t in range(first, last + 1):
-        nbytes.append(decode_bytes(torch, enc["mb"][t], S * nmb))
-    sp = {}
+        nbytes.append(decode_bytes(torch, enc["mb"][t], S * nmb) + 16 * S * ngr)
 
-    def spin_init():
-        sp["dec"] = [torch.empty_like(d) for d in dec]
+    def measure(packed):
+        dec = [torch.zeros(S * pic, dtype=torch.uint8, device="cuda") for _ in range(2)]
 
-    def spin_reset():
-        for a, b in zip(sp["dec"], dec):
-            a.copy_(b)
+        def dec_step(t, d=dec):
+            if packed:
+                lv, n, ix = pk[t]
+                p64_amd.decode_recon_packed(d[(t + 1) % 2], d[t % 2], lv, n, ix, enc["mb"][t], qmb, mask,
+                                            width=w, height=h)
+            else:
+                p64_amd.decode_recon(d[(t + 1) % 2], d[t % 2], enc["coef"][t], enc["mb"][t], qmb, mask,
+                                     width=w, height=h)
 
-    def spin_step(t):
-        p64_amd.decode_recon(sp["dec"][(t + 1) % 2], sp["dec"][t % 2], enc["coef"][t], enc["mb"][t], qmb,
-                             mask, width=w, height=h)
+        for t in range(first):  # pictures before the timed ones, untimed
+            dec_step(t)
+        sp = {}
 
-    elapsed, kavg, clk = timed_region(torch, dist, world, args.steps, first, step, graph=not args.eager,
-                                      spinup_ms=args.spinup_ms,
-                                      spin={"init": spin_init, "reset": spin_reset, "launch": spin_step})
-    sp.clear()
+        def spin_init():
+            sp["dec"] = [torch.empty_like(d) for d in dec]
+
+        def spin_reset():
+            for a, b in zip(sp["dec"], dec):
+                a.copy_(b)
+
+        elapsed, kavg, clk = timed_region(torch, dist, world, args.steps, first, dec_step, graph=not args.eager,
+                                          spinup_ms=args.spinup_ms,
+                                          spin={"init": spin_init, "reset": spin_reset,
+                                                "launch": lambda t: dec_step(t, sp["dec"])})
+        sp.clear()
+        ok = bool(torch.equal(dec[last % 2], enc["recon_last"]))
+        return elapsed, kavg, clk, ok
+
+    elapsed, kavg, clk, ok = measure(True)
+    d_el, d_kavg, _, d_ok = measure(False)
     tmax = max_over_ranks(elapsed, world, device="cuda")
-    ok = bool(torch.equal(dec[last % 2], enc["recon_last"]))
-    if not all_ranks_ok(ok, world, device="cuda"):
+    if not all_ranks_ok(ok and d_ok, world, device="cuda"):
         raise SystemExit("bench: decoded pictures differ from the encoder's reconstruction")
     mbs = S * nmb
     bpl = sum(nbytes) / len(nbytes)
@@ -1576,15 +1633,20 @@ def run_decode(args, torch, dist, np, p64_amd, world, enc, S, nmb, pic):
             "ms_per_step": round(tmax / args.steps * 1e3, 4),
             "config": {"workload": f"{w}x{h} decoder reconstruction of a GPU-encoded stream "
                                    f"(FULL SL={args.search_limit}, q={args.quant}, content "
-                                   f"{args.content}), {S} sequences/GPU, closed loop",
+                                   f"{args.content}), {S} sequences/GPU, closed loop, packed levels "
+                                   f"(p64gpu_decode_recon_packed)",
                        "macroblocks_per_step_per_gpu": mbs},
-            "roofline": roofline(bpl, kavg, "k_recon_mbg", load_pmc(args.pmc_json, key),
+            "roofline": roofline(bpl, kavg, "k_recon_pk", load_pmc(args.pmc_json, key),
                                  algorithmic_bytes_per_mb=round(bpl / mbs, 1), timing=timing_note(args)),
+            "dense": {"kernel": "k_recon_mbg (p64gpu_decode_recon, dense levels)",
+                      "kernel_avg_us": round(d_kavg * 1e6, 2),
+                      "frac": round(bpl / d_kavg / 1e9 / HBM_PEAK_GBS, 4),
+                      "macroblocks_per_s": round(aggregate_rate(world, mbs, args.steps, d_el), 1)},
             "valu_busy": (load_pmc(args.pmc_json, key) or {}).get("valu_busy"),
             "valu_busy_note": VALU_BUSY_NOTE,
             "steady_state": clk,
-            "verified_vs_encoder": {"ok": ok, "note": "last decoded picture == encoder "
-                                                      "reconstruction, all sequences"}}
+            "verified_vs_encoder": {"ok": ok and d_ok, "note": "last decoded picture == encoder "
+                                                               "reconstruction, all sequences (both entries)"}}
 
 
 def dry_main(args, rank, world):

@@ -53,6 +53,11 @@
  * with that mask; p64gpu_vlc_args.flags (was `reserved`, must be 0),
  * .blk_bits (appended) and its scratch of 6*nframes*nmb uint32, 8-byte
  * aligned; synthetic contents (p64_synth_content).
+ *
+ * ABI version 3 (round 6): p64gpu_decode_recon_packed (packed levels +
+ * per-group index, p64s_pack_levels in p64stream.h); p64gpu_vlc_pictures
+ * accepts any device-addressable pointer (pinned host memory included) and
+ * refuses pageable host memory.
  */
 #ifndef P64GPU_H
 #define P64GPU_H
@@ -64,7 +69,7 @@
 extern "C" {
 #endif
 
-#define P64GPU_ABI_VERSION 2
+#define P64GPU_ABI_VERSION 3
 
 enum p64gpu_status {
   P64GPU_OK = 0,
@@ -232,6 +237,23 @@ int p64gpu_decode_recon(int width, int height, int nframes, int64_t frame_stride
                         const uint8_t *ref, uint8_t *recon, const int16_t *coef,
                         const p64_mb_rec *mb, const uint8_t *quant_mb,
                         const uint8_t *coded_mask, void *stream);
+
+/* The same from PACKED levels (ABI v3): `levels` holds only the transmitted
+ * blocks' 64 zigzag levels each (nlevels blocks: MB present in coded_mask,
+ * MTYPE with coefficients, its CBP bit set -- what the stream carries),
+ * contiguous in (picture, MB, block) raster order; `index` holds, for each
+ * group of 64 consecutive blocks of a picture (group j of picture f covers
+ * its blocks 64j .. 64j+63, block = 6*mb + b; ceil(6*nmb/64) groups per
+ * picture), four uint32: the index in `levels` of the group's first
+ * transmitted block, 0, and the group's 64-bit transmitted-block mask (bit i
+ * = block 64j + i), low word first.  p64s_pack_levels (p64stream.h) builds
+ * both from p64s_read_picture's output.  The kernel loads a group's levels
+ * from its index entry without waiting for the records.
+ * levels and index 16-byte aligned; nlevels < 2^24 per call. */
+int p64gpu_decode_recon_packed(int width, int height, int nframes, int64_t frame_stride,
+                               const uint8_t *ref, uint8_t *recon, const int16_t *levels,
+                               int64_t nlevels, const uint32_t *index, const p64_mb_rec *mb,
+                               const uint8_t *quant_mb, const uint8_t *coded_mask, void *stream);
 
 /* ---- entropy coding on the device (p64vlc.hip) -------------------------- */
 /* The H.261 bits of nframes coded pictures (QCIF/CIF/NTSC), identical to

@@ -122,6 +122,15 @@ int p64s_reader_info(const p64s_reader *r, p64s_picture_info *info);
 int p64s_read_picture(p64s_reader *r, p64s_picture_info *info, p64_mb_rec *mb,
                       uint8_t *quant_mb, uint8_t *coded, int16_t *coef);
 
+/* The packed level layout of p64gpu_decode_recon_packed (p64gpu.h) from
+ * nframes pictures of p64s_read_picture output (mb, coded, coef as that
+ * call writes them, pictures consecutive): the transmitted blocks' levels
+ * into `levels` (room for up to nframes*nmb*6 blocks), contiguous in raster
+ * order, and the per-group index (nframes * ceil(6*nmb/64) * 4 uint32).
+ * Returns the number of blocks written (>= 0) or a negative status. */
+int64_t p64s_pack_levels(int format, int nframes, const p64_mb_rec *mb, const uint8_t *coded,
+                         const int16_t *coef, int16_t *levels, uint32_t *index);
+
 #ifdef __cplusplus
 }
 #endif

@@ -35,7 +35,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # P64GPU_LIB lets development A/B runs point at an alternative build.
 LIB_PATH = os.environ.get("P64GPU_LIB", os.path.join(_HERE, "libp64gpu.so"))
 
-ABI_VERSION = 2  # include/p64gpu.h P64GPU_ABI_VERSION
+ABI_VERSION = 3  # include/p64gpu.h P64GPU_ABI_VERSION
 ME_TSS = 0
 ME_FULL = 1
 
@@ -115,6 +115,9 @@ def lib() -> ctypes.CDLL:
     L.p64gpu_motion_estimation.argtypes = [i32, i32, i32, i64, vp, vp, i32, i32, vp, vp]
     L.p64gpu_encode_frames.argtypes = [ctypes.POINTER(EncodeArgs), vp]
     L.p64gpu_decode_recon.argtypes = [i32, i32, i32, i64, vp, vp, vp, vp, vp, vp, vp]
+    L.p64gpu_decode_recon_packed.argtypes = [i32, i32, i32, i64, vp, vp, vp, i64, vp, vp, vp, vp, vp]
+    L.p64s_pack_levels.argtypes = [i32, i32, vp, vp, vp, vp, vp]
+    L.p64s_pack_levels.restype = i64
     L.p64gpu_release_scratch.argtypes = []
     L.p64gpu_encoder_open.argtypes = [i32, i32, i32, i32, i32, ctypes.POINTER(vp)]
     L.p64gpu_encoder_frame.argtypes = [vp, vp, i32, i32, vp, vp, vp, vp, vp]
@@ -468,6 +471,62 @@ def decode_recon(ref, recon, coef, mb, quant_mb, coded_mask, *, width: int, heig
                                      recon.data_ptr(), coef.data_ptr(), mb.data_ptr(),
                                      quant_mb.data_ptr(), coded_mask.data_ptr(), _stream(torch)))
     return recon
+
+
+def decode_recon_packed(ref, recon, levels, nlevels: int, index, mb, quant_mb, coded_mask, *, width: int,
+                        height: int):
+    """decode_recon from the packed level layout (ABI v3,
+    p64gpu_decode_recon_packed): levels int16 [>= nlevels, 64] holds only the
+    transmitted blocks' levels in raster order, index uint32 [groups, 4] the
+    per-64-block group entries (stream.pack_levels / pack_levels_device)."""
+    torch = _torch()
+    for t, dt, name in ((ref, torch.uint8, "ref"), (recon, torch.uint8, "recon"),
+                        (levels, torch.int16, "levels"), (index, torch.int32, "index"), (mb, torch.int8, "mb"),
+                        (quant_mb, torch.uint8, "quant_mb"), (coded_mask, torch.uint8, "coded_mask")):
+        _dev_check(t, dt, name)
+    stride = picture_bytes(width, height)
+    nframes = recon.numel() // stride
+    nmb = (width // 16) * (height // 16)
+    nmb_all = nframes * nmb
+    ngr = (6 * nmb + 63) // 64
+    if nframes < 1 or ref.numel() < nframes * stride or levels.numel() < nlevels * 64 or \
+            index.numel() < nframes * ngr * 4 or mb.numel() < nmb_all * 4 or quant_mb.numel() < nmb_all or \
+            coded_mask.numel() < nmb_all:
+        raise P64GpuError("buffer sizes do not match nframes x picture geometry")
+    _check(lib().p64gpu_decode_recon_packed(width, height, nframes, stride, ref.data_ptr(), recon.data_ptr(),
+                                            levels.data_ptr(), int(nlevels), index.data_ptr(), mb.data_ptr(),
+                                            quant_mb.data_ptr(), coded_mask.data_ptr(), _stream(torch)))
+    return recon
+
+
+def pack_levels_device(coef, mb, coded_mask, width: int, height: int):
+    """The packed layout of decode_recon_packed from device arrays in the
+    dense layout (an encoder's levels and records, or the reader's): the
+    same entries p64s_pack_levels makes on the host, by torch ops (a bench /
+    test helper: the reader's host output goes through stream.pack_levels).
+    Returns (levels [n, 64] int16, n, index [groups, 4] int32)."""
+    torch = _torch()
+    nmb = (width // 16) * (height // 16)
+    mbr = mb.reshape(-1, nmb, 4)
+    nf = mbr.shape[0]
+    mt = mbr[..., 0].long()
+    tc = torch.tensor(TCOEFF_MTYPE, device=mb.device)[mt]
+    hc = torch.tensor(CBP_MTYPE, device=mb.device)[mt]
+    cbp = torch.where(hc == 1, mbr[..., 1].long() & 63, torch.full_like(mt, 63))
+    bits = (cbp[..., None] >> (5 - torch.arange(6, device=mb.device))) & 1  # [nf, nmb, 6]
+    tx = (bits * tc[..., None] * (coded_mask.reshape(nf, nmb)[..., None] != 0)).reshape(nf, 6 * nmb)
+    ngr = (6 * nmb + 63) // 64
+    pad = torch.zeros((nf, ngr * 64), dtype=torch.long, device=mb.device)
+    pad[:, :6 * nmb] = tx
+    g = pad.reshape(nf, ngr, 64)
+    cnt = g.sum(dim=2).reshape(-1)
+    start = torch.cumsum(cnt, 0) - cnt
+    w = (g.reshape(-1, 64) << torch.arange(64, device=mb.device)).sum(dim=1)  # (int64 wraps: bit 63 fine)
+    index = torch.stack([start, torch.zeros_like(start), w & 0xFFFFFFFF, (w >> 32) & 0xFFFFFFFF], dim=1)
+    index = index.to(torch.int64).to(torch.int32)
+    sel = tx.reshape(-1).nonzero().squeeze(1)
+    levels = coef.reshape(-1, 64).index_select(0, sel).contiguous()
+    return levels, int(sel.numel()), index.contiguous()
 
 
 class Encoder:

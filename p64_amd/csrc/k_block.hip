@@ -1127,6 +1127,72 @@ __global__ __launch_bounds__(64) OCC4 void k_recon_mbg(int w, int h, int64_t str
   rec_wave_compact(w, h, stride, rec, A, S, slots, lane);
 }
 
+// Decoder reconstruction from PACKED levels (p64gpu_decode_recon_packed, ABI
+// v3): the transmitted blocks' levels contiguous in raster order, and per
+// group of 64 blocks of a picture (a wave) its first transmitted block's index
+// and its transmitted-block mask, {start, 0, mask lo, mask hi}
+// (p64s_pack_levels).  The wave reads its group's entry with one scalar load
+// while its records are in flight and issues its level loads at once from
+// start + (the lane's rank among the set bits) -- the levels no longer wait
+// for the record (in k_recon_mbg a lane learns from its record whether, and
+// so where, to load); only the prediction source does.  Waves map to
+// pictures: nwpp = ceil(6 nmb / 64) per picture, the last one partly idle.
+typedef unsigned su4 __attribute__((ext_vector_type(4)));
+__global__ __launch_bounds__(64) OCC4 void k_recon_pk(int w, int h, int64_t stride, const uint8_t *refp,
+                                                          uint8_t *recp, const int16_t *levels, uint32_t nlev,
+                                                          const uint32_t *index, const p64_mb_rec *mbr,
+                                                          const uint8_t *quant_mb, const uint8_t *coded_mask,
+                                                          BlkDiv kd, unsigned nmbs, unsigned nwpp) {
+  const int lane = threadIdx.x & 63;
+  const unsigned wv = xcd_remap(blockIdx.x, gridDim.x);  // (grid = nframes x nwpp)
+  PRIO_HIGH();
+  const int nmb = (w >> 4) * (h >> 4), nfr = (int)mdiv(nmbs, kd.mn, kd.sn);
+  const unsigned fi = wv / nwpp, j = wv - fi * nwpp;  // (scalar, once per wave)
+  RecBufs B;
+  B.ref = __builtin_amdgcn_make_buffer_rsrc((void *)refp, (short)0, (int)(nfr * stride), BUF_RSRC_W3);
+  B.coef = __builtin_amdgcn_make_buffer_rsrc((void *)levels, (short)0, (int)(nlev * 128u), BUF_RSRC_W3);
+  B.mb = __builtin_amdgcn_make_buffer_rsrc((void *)mbr, (short)0, nfr * nmb * 4, BUF_RSRC_W3);
+  B.q = __builtin_amdgcn_make_buffer_rsrc((void *)quant_mb, (short)0, nfr * nmb, BUF_RSRC_W3);
+  B.mask = __builtin_amdgcn_make_buffer_rsrc((void *)coded_mask, (short)0, nfr * nmb, BUF_RSRC_W3);
+  const __amdgpu_buffer_rsrc_t rec =
+      __builtin_amdgcn_make_buffer_rsrc((void *)recp, (short)0, (int)(nfr * stride), BUF_RSRC_W3);
+  const unsigned nb = 6u * (unsigned)nmb, bl = 64u * j + (unsigned)lane;  // block within the picture
+  const bool valid = bl < nb;
+  const unsigned g = fi * nb + min(bl, nb - 1);
+  const unsigned gmb = __umulhi(g, 0xAAAAAAABu) >> 2;  // g / 6
+  RecStageA A;
+  A.p = blk_pos_mb(gmb, (int)(g - 6u * gmb), w, h, kd);
+  A.m = __builtin_amdgcn_raw_buffer_load_b32(B.mb, 4 * gmb, 0, 0);
+  A.q = __builtin_amdgcn_raw_buffer_load_b8(B.q, gmb, 0, 0);
+  A.coded = __builtin_amdgcn_raw_buffer_load_b8(B.mask, valid ? gmb : BUF_OOB, 0, 0);
+  // the group's entry by a scalar load (its wait is on the scalar counter:
+  // the record loads above stay in flight), then the level loads
+  su4 ix;
+  asm volatile("s_load_dwordx4 %0, %1, %2\n s_waitcnt lgkmcnt(0)"
+               : "=s"(ix)
+               : "s"(index), "s"(16u * wv));
+  const uint64_t msk = (uint64_t)ix.z | ((uint64_t)ix.w << 32);
+  const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(msk >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)msk, 0u));
+  const uint32_t lo = ((msk >> lane) & 1) && valid ? (ix.x + rank) * 128u : BUF_OOB;
+  uint32_t lq[8][4];
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    const auto v = __builtin_amdgcn_raw_buffer_load_b128(B.coef, lo + 16 * k, 0, 0);
+    lq[k][0] = v[0];
+    lq[k][1] = v[1];
+    lq[k][2] = v[2];
+    lq[k][3] = v[3];
+  }
+  RecStageB S = rec_stage_b<false>(B, w, h, stride, A);
+#pragma unroll
+  for (int k = 0; k < 8; k++)
+#pragma unroll
+    for (int i = 0; i < 4; i++) S.lq[k][i] = lq[k][i];
+  PRIO_LOW();
+  __shared__ uint32_t slots[RSLOT * (64 / LPB)];
+  rec_wave_compact(w, h, stride, rec, A, S, slots, lane);
+}
+
 // ---------------------------------------------------------------------------
 // inter picture, second stage of the split encoder: k_motion writes every
 // MB's ME record, then this block-layout kernel does the rest of
@@ -1221,30 +1287,40 @@ __global__ __launch_bounds__(64) OCC4 void k_inter_mbg(p64gpu_encode_args a, Blk
   PRIO_LOW();  // the loads are out
   // VAR, VAROR, MWOR at the chosen vector (me.c:229-245 == 313-329): per luma
   // lane the sums over its 8x8 quadrant by byte dot products, sum (r-c)^2 =
-  // r.r - 2 r.c + c.c (exact in u32), then the MB's four luma lanes added
-  // (lanes 6m..6m+3) and the results handed to its six lanes
+  // r.r - 2 r.c + c.c (exact in u32; c.c first: the current rows arrive
+  // before the source), then every lane adds its MB's four luma lanes
+  // (6m..6m+3) from one LDS exchange (the level staging, not in use yet)
   uint32_t rr = 0, rc = 0, cc = 0, rs = 0;
+#pragma unroll
+  for (int r = 0; r < 8; r++)
+    cc = __builtin_amdgcn_udot4(f.rows[r].y, f.rows[r].y, __builtin_amdgcn_udot4(f.rows[r].x, f.rows[r].x, cc, false),
+                                false);
 #pragma unroll
   for (int r = 0; r < 8; r++) {
     const uint32_t w0 = align4(S1.pred.d[r][1], S1.pred.d[r][0], S1.pred.sh);
     const uint32_t w1 = align4(S1.pred.d[r][2], S1.pred.d[r][1], S1.pred.sh);
-    const uint32_t c0 = f.rows[r].x, c1 = f.rows[r].y;
     rr = __builtin_amdgcn_udot4(w1, w1, __builtin_amdgcn_udot4(w0, w0, rr, false), false);
-    rc = __builtin_amdgcn_udot4(w1, c1, __builtin_amdgcn_udot4(w0, c0, rc, false), false);
-    cc = __builtin_amdgcn_udot4(c1, c1, __builtin_amdgcn_udot4(c0, c0, cc, false), false);
+    rc = __builtin_amdgcn_udot4(w1, f.rows[r].y, __builtin_amdgcn_udot4(w0, f.rows[r].x, rc, false), false);
     rs = sad4(w1, 0u, sad4(w0, 0u, rs));
   }
-  const bool luma = b < 4;
-  uint32_t e2 = luma ? rr + cc - 2 * rc : 0u;
-  rr = luma ? rr : 0u;
-  rs = luma ? rs : 0u;
-  e2 += __shfl_down(e2, 1) + __shfl_down(e2, 2) + __shfl_down(e2, 3);
-  rr += __shfl_down(rr, 1) + __shfl_down(rr, 2) + __shfl_down(rr, 3);
-  rs += __shfl_down(rs, 1) + __shfl_down(rs, 2) + __shfl_down(rs, 3);
-  const int src = l - b;  // the MB's lane 0 holds its totals (tail lanes 60..63 copy lane 59)
-  const int var = (int)(__shfl(e2, src) / 256u);
-  const uint32_t rs_mb = __shfl(rs, src);
-  const int varor = (int)(__shfl(rr, src) / 256u) - (int)(rs_mb / 256u) * (int)(rs_mb / 256u);
+  uint32_t e2 = rr + cc - 2 * rc, tr = 0, te = 0, ts = 0;
+  {
+    uint8_t *x = lds + lane * 16;
+    *reinterpret_cast<uint4 *>(x) = make_uint4(e2, rr, rs, 0u);
+    WAVE_FENCE();
+    const uint8_t *g0 = lds + (l - b) * 16;  // the MB's lane 0 (tail lanes 60..63 copy lane 59)
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      const uint4 v = *reinterpret_cast<const uint4 *>(g0 + 16 * i);
+      te += v.x;
+      tr += v.y;
+      ts += v.z;
+    }
+    WAVE_FENCE();  // (the staging is written again later)
+  }
+  const int var = (int)(te / 256u);
+  const uint32_t rs_mb = ts;
+  const int varor = (int)(tr / 256u) - (int)(rs_mb / 256u) * (int)(rs_mb / 256u);
 
   // MTYPE (p64.c:734-772): the decision, the -o override, the intra refresh
   MeOut mo_;
@@ -1539,6 +1615,15 @@ hipError_t recon_mbg(int w, int h, int nframes, int64_t stride, const uint8_t *r
   const unsigned nm = (unsigned)((int64_t)nframes * (w / 16) * (h / 16));
   hipLaunchKernelGGL(k_recon_mbg, dim3((6u * nm + 63u) / 64u), dim3(64), 0, st, w, h, stride, ref, recon,
                      coef, mb, quant_mb, coded_mask, blk_div(w, h), nm);
+  return hipGetLastError();
+}
+
+hipError_t recon_pk(int w, int h, int nframes, int64_t stride, const uint8_t *ref, uint8_t *recon,
+                    const int16_t *levels, uint32_t nlev, const uint32_t *index, const p64_mb_rec *mb,
+                    const uint8_t *quant_mb, const uint8_t *coded_mask, hipStream_t st) {
+  const unsigned nmb = (unsigned)((w / 16) * (h / 16)), nwpp = (6u * nmb + 63u) / 64u;
+  hipLaunchKernelGGL(k_recon_pk, dim3((unsigned)nframes * nwpp), dim3(64), 0, st, w, h, stride, ref, recon, levels,
+                     nlev, index, mb, quant_mb, coded_mask, blk_div(w, h), (unsigned)nframes * nmb, nwpp);
   return hipGetLastError();
 }
 

@@ -29,6 +29,9 @@ hipError_t inter_mbg(const p64gpu_encode_args &a, p64_me_rec *me, const uint32_t
 hipError_t recon_mbg(int w, int h, int nframes, int64_t stride, const uint8_t *ref, uint8_t *recon,
                      const int16_t *coef, const p64_mb_rec *mb, const uint8_t *quant_mb,
                      const uint8_t *coded_mask, hipStream_t st);
+hipError_t recon_pk(int w, int h, int nframes, int64_t stride, const uint8_t *ref, uint8_t *recon,
+                    const int16_t *levels, uint32_t nlev, const uint32_t *index, const p64_mb_rec *mb,
+                    const uint8_t *quant_mb, const uint8_t *coded_mask, hipStream_t st);
 
 // k_aux.hip -- reference block routines one thread per block; synthetic input;
 // the clock probe

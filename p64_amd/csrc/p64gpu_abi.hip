@@ -398,6 +398,30 @@ int p64gpu_decode_recon(int w, int h, int nframes, int64_t stride, const uint8_t
   return P64GPU_OK;
 }
 
+int p64gpu_decode_recon_packed(int w, int h, int nframes, int64_t stride, const uint8_t *ref, uint8_t *recon,
+                               const int16_t *levels, int64_t nlevels, const uint32_t *index,
+                               const p64_mb_rec *mb, const uint8_t *quant_mb, const uint8_t *coded_mask,
+                               void *stream) {
+  int s = check_geometry(w, h, nframes, stride);
+  if (s) return s;
+  if (!ref || !recon || !index || !mb || !quant_mb || !coded_mask || (!levels && nlevels))
+    return fail(P64GPU_E_INVALID, "NULL buffer");
+  if (nlevels < 0 || nlevels >= (((int64_t)1) << 31) / 128)
+    return fail(P64GPU_E_INVALID, "nlevels %lld: 0 .. 2^24-1 blocks per call", (long long)nlevels);
+  if (!aligned(ref, 16) || !aligned(recon, 16) || !aligned(levels, 16) || !aligned(index, 16) || !aligned(mb, 4))
+    return fail(P64GPU_E_INVALID, "ref/recon/levels/index must be 16-byte aligned, mb 4-byte aligned");
+  const size_t nmb = (size_t)(w / 16) * (h / 16), nwpp = (6 * nmb + 63) / 64;
+  const int chunk = pictures_per_launch(w, h, stride);
+  for (int f0 = 0; f0 < nframes; f0 += chunk) {
+    const int nf = nframes - f0 < chunk ? nframes - f0 : chunk;
+    const size_t m0 = (size_t)f0 * nmb;
+    HIP_TRY(p64k::recon_pk(w, h, nf, stride, ref + (size_t)f0 * stride, recon + (size_t)f0 * stride, levels,
+                           (uint32_t)nlevels, index + (size_t)f0 * nwpp * 4, mb + m0, quant_mb + m0,
+                           coded_mask + m0, (hipStream_t)stream));
+  }
+  return P64GPU_OK;
+}
+
 int p64gpu_synth_content(int content, int w, int h, uint32_t seed0, int nseeds, int frame0, int nslots,
                          int64_t stride, uint8_t *out, void *stream) {
   int s = check_geometry(w, h, 1, stride);

@@ -249,12 +249,19 @@ static int decode(const opts *o) {
   p64_mb_rec *mb = malloc(nmb * sizeof *mb);
   uint8_t *qm = malloc(nmb), *coded = malloc(nmb), *host = calloc(pic, 1);
   int16_t *coef = malloc((size_t)nmb * 384 * sizeof *coef);
+  /* the packed layout of p64gpu_decode_recon_packed: the transmitted blocks'
+   * levels only, and the per-group index (p64s_pack_levels) */
+  const size_t ngr = ((size_t)nmb * 6 + 63) / 64;
+  int16_t *levels = malloc((size_t)nmb * 384 * sizeof *levels);
+  uint32_t *index = malloc(ngr * 16);
   uint8_t *d_pic[2], *d_qm, *d_coded;
   int16_t *d_coef;
+  uint32_t *d_index;
   p64_mb_rec *d_mb;
   if ((s = p64gpu_alloc((void **)&d_pic[0], pic)) || (s = p64gpu_alloc((void **)&d_pic[1], pic)) ||
       (s = p64gpu_alloc((void **)&d_qm, nmb)) || (s = p64gpu_alloc((void **)&d_coded, nmb)) ||
       (s = p64gpu_alloc((void **)&d_coef, (size_t)nmb * 384 * sizeof *coef)) ||
+      (s = p64gpu_alloc((void **)&d_index, ngr * 16)) ||
       (s = p64gpu_alloc((void **)&d_mb, nmb * sizeof *mb)) ||
       (s = p64gpu_copy_to_device(d_pic[0], host, pic, NULL))) /* ClearFS */
     return die("device buffers", s);
@@ -297,12 +304,16 @@ static int decode(const opts *o) {
     if (!npics) offset = (info.tr - frame) % 32;
     /* recon starts as the previous picture: untransmitted MBs keep it */
     uint8_t *ref = d_pic[prev], *rec = d_pic[prev ^ 1];
+    const int64_t nlev = p64s_pack_levels(info.format, 1, mb, coded, coef, levels, index);
+    if (nlev < 0) return die("pack_levels", (int)nlev);
     if ((s = p64gpu_copy_on_device(rec, ref, pic, NULL)) ||
         (s = p64gpu_copy_to_device(d_mb, mb, nmb * sizeof *mb, NULL)) ||
         (s = p64gpu_copy_to_device(d_qm, qm, nmb, NULL)) ||
         (s = p64gpu_copy_to_device(d_coded, coded, nmb, NULL)) ||
-        (s = p64gpu_copy_to_device(d_coef, coef, (size_t)nmb * 384 * sizeof *coef, NULL)) ||
-        (s = p64gpu_decode_recon(w, h, 1, (int64_t)pic, ref, rec, d_coef, d_mb, d_qm, d_coded, NULL)) ||
+        (s = p64gpu_copy_to_device(d_coef, levels, (size_t)nlev * 64 * sizeof *levels, NULL)) ||
+        (s = p64gpu_copy_to_device(d_index, index, ngr * 16, NULL)) ||
+        (s = p64gpu_decode_recon_packed(w, h, 1, (int64_t)pic, ref, rec, d_coef, nlev, d_index, d_mb, d_qm,
+                                        d_coded, NULL)) ||
         (s = p64gpu_copy_to_host(host, rec, pic, NULL)) || (s = p64gpu_synchronize(NULL)))
       return die("decode", s);
     prev ^= 1;

@@ -351,13 +351,39 @@ def encode_sequence(frames, width: int, height: int, *, quant: int = 0, me_mode:
         enc.close()
 
 
-def decode_sequence(data: bytes, start_frame: int = 0, force_cif: bool = False) -> list[np.ndarray]:
+def pack_levels(fmt: int, mb, coded, coef):
+    """p64s_pack_levels: the packed level layout of decode_recon_packed from
+    the reader's dense output of one or more pictures (mb [n, nmb] records,
+    coded [n, nmb], coef [n, nmb, 6, 64]).  Returns (levels [k, 64] int16,
+    index [groups, 4] uint32)."""
+    _, _, ngob = geometry(fmt)
+    nmb = ngob * 33
+    mbv = np.ascontiguousarray(mb)
+    if mbv.dtype != MB_DTYPE:
+        mbv = np.ascontiguousarray(np.asarray(mb, np.int8).reshape(-1, 4)).view(MB_DTYPE).reshape(-1)
+    cd = np.ascontiguousarray(coded, dtype=np.uint8).reshape(-1)
+    cf = np.ascontiguousarray(coef, dtype=np.int16).reshape(-1)
+    n = cd.size // nmb
+    if mbv.size != n * nmb or cf.size != n * nmb * 384:
+        raise P64GpuError("pack_levels: arrays do not match the picture format")
+    levels = np.empty((n * nmb * 6, 64), np.int16)
+    index = np.empty((n * ((6 * nmb + 63) // 64), 4), np.uint32)
+    k = int(lib().p64s_pack_levels(fmt, n, mbv.ctypes.data, cd.ctypes.data, cf.ctypes.data,
+                                   levels.ctypes.data, index.ctypes.data))
+    _check(k if k < 0 else 0)
+    return levels[:k], index
+
+
+def decode_sequence(data: bytes, start_frame: int = 0, force_cif: bool = False,
+                    packed: bool = True) -> list[np.ndarray]:
     """p64DecodeSequence (p64.c:1022): host parse + GPU reconstruction; returns
     the output frames (Y|U|V bytes) in the order the reference writes them.
-    force_cif: the -c flag (CIF geometry whatever the stream's PTYPE says)."""
+    force_cif: the -c flag (CIF geometry whatever the stream's PTYPE says).
+    packed: the reader's levels packed (pack_levels) for decode_recon_packed
+    (ABI v3, the default); else the dense layout through decode_recon."""
     import torch
 
-    from . import decode_recon
+    from . import decode_recon, decode_recon_packed
     r = Reader(data, force_cif=force_cif)
     w, h, nmb = r.width, r.height, r.nmb
     pic = w * h * 3 // 2
@@ -368,8 +394,14 @@ def decode_sequence(data: bytes, start_frame: int = 0, force_cif: bool = False) 
         ref, rec = bufs[prev], bufs[prev ^ 1]
         rec.copy_(ref)  # MBs absent from the stream keep the previous picture
         dev = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()  # noqa: E731
-        decode_recon(ref, rec, dev(p.coef), dev(p.mb.view(np.int8)), dev(p.quant_mb),
-                     dev(p.coded), width=w, height=h)
+        if packed:
+            lv, ix = pack_levels(r.fmt, p.mb, p.coded, p.coef)
+            lvd = dev(lv) if len(lv) else torch.zeros((1, 64), dtype=torch.int16, device="cuda")
+            decode_recon_packed(ref, rec, lvd, len(lv), dev(ix.view(np.int32)), dev(p.mb.view(np.int8)),
+                                dev(p.quant_mb), dev(p.coded), width=w, height=h)
+        else:
+            decode_recon(ref, rec, dev(p.coef), dev(p.mb.view(np.int8)), dev(p.quant_mb),
+                         dev(p.coded), width=w, height=h)
         pics.append(rec.cpu().numpy())
         trs.append(p.tr)
         prev ^= 1

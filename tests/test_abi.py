@@ -29,7 +29,8 @@ def test_header_declares_expected_entry_points():
               "p64gpu_encoder_close", "p64gpu_synth_frames", "p64_synth_frame",
               "p64gpu_copy_on_device", "p64s_write_picture", "p64s_write_end",
               "p64s_read_picture", "p64s_reader_open", "p64gpu_encode_mb_list",
-              "p64s_write_mb", "p64seq_open", "p64seq_encode", "p64seq_finish"):
+              "p64s_write_mb", "p64seq_open", "p64seq_encode", "p64seq_finish",
+              "p64gpu_decode_recon_packed", "p64s_pack_levels", "p64s_write_bits"):
         assert n in names
 
 
@@ -43,7 +44,7 @@ def test_library_exports_every_declared_symbol(p64):
 
 def test_abi_version_and_strings(p64):
     L = p64.lib()
-    assert L.p64gpu_abi_version() == 2 == p64.ABI_VERSION
+    assert L.p64gpu_abi_version() == 3 == p64.ABI_VERSION
     assert L.p64gpu_strerror(0) == b"ok"
     assert L.p64gpu_strerror(-1) == b"invalid argument"
 

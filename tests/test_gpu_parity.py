@@ -878,11 +878,19 @@ def test_bench_scale_properties(p64, oracle_mod, torch_dev, content):
     mask = torch.ones_like(qmb)
     prev = torch.zeros(S * pic, dtype=torch.uint8, device="cuda")
     sel = torch.tensor([32 >> b for b in range(6)], dtype=torch.uint8, device="cuda")
+    prevp = prev.clone()
     for t in range(nfr):
         d = torch.zeros_like(prev)
         p64.decode_recon(prev, d, outs[t][0], outs[t][1], qmb, mask, width=w, height=h)
         assert torch.equal(d, recs[t]), f"decoder recon != encoder recon at picture {t}"
         prev = d
+        # the packed layout (ABI v3), built on the device from the same levels
+        lv, n, ix = p64.pack_levels_device(outs[t][0], outs[t][1], mask, w, h)
+        dp = torch.zeros_like(prevp)
+        p64.decode_recon_packed(prevp, dp, lv if n else torch.zeros((1, 64), dtype=torch.int16, device="cuda"),
+                                n, ix, outs[t][1], qmb, mask, width=w, height=h)
+        assert torch.equal(dp, recs[t]), f"packed decoder recon != encoder recon at picture {t}"
+        prevp = dp
         coef = outs[t][0].view(S, nmb, 6, 64)
         stored = (outs[t][3][..., None] & sel) != 0  # [S, nmb, 6]: the nonzero-block mask
         lv = torch.where(stored[..., None], coef, torch.zeros_like(coef))
@@ -959,7 +967,8 @@ def _edge_level_blocks(rng, n):
     return out
 
 
-def test_decoder_extreme_levels_every_q_vs_oracle(p64, oracle_mod, torch_dev):
+@pytest.mark.parametrize("packed", [False, True])
+def test_decoder_extreme_levels_every_q_vs_oracle(p64, oracle_mod, torch_dev, packed):
     """k_recon_mbg's packed dequantiser (exact for |level| <= 528) and v_dot2
     IDCT column pass at their edges: |level| = 127 in every position with the
     IDCT's worst sign patterns, every q = 1..31, intra (DC 1..254) and inter
@@ -967,7 +976,10 @@ def test_decoder_extreme_levels_every_q_vs_oracle(p64, oracle_mod, torch_dev):
     (p64.c:1179-1237 + 971-1013).  Rounds 2-3 leave about a third of the MBs
     out of the coded mask (MBs the MBA addressing skips, p64.c:1163-1167,
     1185-1186): their pixels must stay untouched while the wave-wide row
-    stores write their neighbours."""
+    stores write their neighbours.  packed: the same through
+    p64gpu_decode_recon_packed (ABI v3) with the levels packed by
+    p64s_pack_levels (the transmitted blocks only, per-64-block index)."""
+    from p64_amd import stream
     torch = torch_dev
     w, h = 176, 144
     mbw, nmb, pic = w // 16, 99, w * h * 3 // 2
@@ -996,9 +1008,15 @@ def test_decoder_extreme_levels_every_q_vs_oracle(p64, oracle_mod, torch_dev):
                                      int(mvx[k]), int(mvy[k]), int(q[k]), coef[k])
         mb = np.stack([mt, cbp, mvx, mvy], 1).astype(np.int8)
         d = dev(torch, recon0)
-        p64.decode_recon(dev(torch, ref), d, dev(torch, coef), dev(torch, mb),
-                         dev(torch, q.astype(np.uint8)), dev(torch, coded),
-                         width=w, height=h)
+        if packed:
+            lv, ix = stream.pack_levels(stream.QCIF, mb, coded, coef)
+            p64.decode_recon_packed(dev(torch, ref), d, dev(torch, lv), len(lv), dev(torch, ix.view(np.int32)),
+                                    dev(torch, mb), dev(torch, q.astype(np.uint8)), dev(torch, coded),
+                                    width=w, height=h)
+        else:
+            p64.decode_recon(dev(torch, ref), d, dev(torch, coef), dev(torch, mb),
+                             dev(torch, q.astype(np.uint8)), dev(torch, coded),
+                             width=w, height=h)
         np.testing.assert_array_equal(host(d), exp, err_msg=f"round {rnd}")
 
 

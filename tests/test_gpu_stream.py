@@ -117,10 +117,14 @@ def test_cli_verbose_loud_parity_flags(p64, torch_dev, tmp_path):
     assert hashlib.sha256((tmp_path / "o.p64").read_bytes()).hexdigest() == str(z["stream_sha256"])
 
 
-def test_python_decode_short_p64_md5(p64, torch_dev):
+@pytest.mark.parametrize("packed", [True, False])
+def test_python_decode_short_p64_md5(p64, torch_dev, packed):
+    """short.p64 through the Python reader + GPU reconstruction, with the
+    levels packed (p64gpu_decode_recon_packed, ABI v3; the CLI's path too) and
+    dense (p64gpu_decode_recon): the reference's 21 plane MD5s."""
     from p64_amd import stream
     exp = json.load(open(os.path.join(GOLDEN, "decode.json")))
-    frames = stream.decode_sequence(open(os.path.join(GOLDEN, "short.p64"), "rb").read())
+    frames = stream.decode_sequence(open(os.path.join(GOLDEN, "short.p64"), "rb").read(), packed=packed)
     assert len(frames) == 7
     w, h = 352, 240
     for i, f in enumerate(frames):

@@ -339,3 +339,48 @@ def test_force_cif_refused_after_first_picture(p64, st):
     info = st._Info()
     assert p64.lib().p64s_reader_info(r2._h, ctypes.byref(info)) == 0
     assert (info.width, info.height) == (352, 288)
+
+
+def test_pack_levels_matches_restatement(p64):
+    """p64s_pack_levels (the packed layout of p64gpu_decode_recon_packed) on
+    the reader's output of short.p64 and on a golden sequence's records:
+    exactly the blocks DecompressMDU reads (p64.c:1200-1217: MB present,
+    MTYPE with coefficients, CBP bit) in raster order, and per 64-block
+    group its first block's index and mask."""
+    import numpy as np
+    from p64_amd import stream
+    from test_oracle_golden import load
+    TC = np.array(p64.TCOEFF_MTYPE)
+    CB = np.array(p64.CBP_MTYPE)
+
+    def restate(mb, coded, coef, nmb):
+        n = coded.size // nmb
+        mt = mb["mtype"].astype(int).reshape(n, nmb)
+        cbp = np.where(CB[mt] == 1, mb["cbp"].astype(int).reshape(n, nmb) & 63, 63)
+        bits = (cbp[..., None] >> (5 - np.arange(6))) & 1
+        tx = (bits * TC[mt][..., None] * (coded.reshape(n, nmb)[..., None] != 0)).reshape(n, 6 * nmb)
+        ngr = (6 * nmb + 63) // 64
+        pad = np.zeros((n, ngr * 64), np.int64)
+        pad[:, :6 * nmb] = tx
+        g = pad.reshape(-1, 64)
+        cnt = g.sum(1)
+        m = (g.astype(np.uint64) << np.arange(64, dtype=np.uint64)).sum(1, dtype=np.uint64)
+        return coef.reshape(n, 6 * nmb, 64)[tx == 1], np.cumsum(cnt) - cnt, m
+
+    r = stream.Reader(open(os.path.join(GOLDEN, "short.p64"), "rb").read())
+    pics = list(r)
+    cases = [(r.fmt, np.stack([p.mb for p in pics]), np.stack([p.coded for p in pics]),
+              np.stack([p.coef for p in pics]))]
+    z = load("seq_cif_full31.npz")
+    mbz = z["mb"].astype(np.int8).reshape(-1, 4).view(p64.MB_DTYPE).reshape(-1)
+    coded = np.ones(mbz.size, np.uint8)
+    coded[::7] = 0
+    cases.append((stream.CIF, mbz, coded, z["coef"].astype(np.int16)))
+    for fmt, mb, cd, coef in cases:
+        nmb = stream.geometry(fmt)[2] * 33
+        lv, ix = stream.pack_levels(fmt, mb, cd, coef)
+        elv, start, m = restate(np.asarray(mb).reshape(-1), cd.reshape(-1), coef, nmb)
+        np.testing.assert_array_equal(lv, elv)
+        np.testing.assert_array_equal(ix[:, 0], start)
+        assert not ix[:, 1].any()
+        np.testing.assert_array_equal(ix[:, 2].astype(np.uint64) | (ix[:, 3].astype(np.uint64) << np.uint64(32)), m)

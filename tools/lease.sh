@@ -45,7 +45,7 @@ for st in "$@"; do
         > $O/bench_prof$sfx.json 2> $O/bench_prof$sfx.err) || { tail -20 $O/bench_prof$sfx.err; exit 1; }
       find $O/prof$sfx -name "*kernel_stats.csv" -exec cp {} $O/kernel_stats$sfx.csv \;
       find $O/prof$sfx -name "*kernel_trace.csv" -exec cp {} $O/kernel_trace$sfx.csv \;
-      for k in "" k_intra_mbg k_recon_mbg; do
+      for k in "" k_intra_mbg k_recon_mbg k_recon_pk; do
         python3 tools/timed_region.py $O/kernel_trace$sfx.csv 20 --json $O/timed_region$sfx.json --key $KEY $k \
           >> $O/timed_region$sfx.txt
       done
