@@ -285,7 +285,8 @@ class CodedFeed:
         self.mx = [torch.zeros(1, dtype=torch.int64, device="cuda") for _ in range(2)]
         self.bits = [None, None]
         self.ev = [torch.cuda.Event(), torch.cuda.Event()]
-        self.side = torch.cuda.Stream()
+        # (P64_FEED_SIDE=0: gathers on the encode stream itself -- diagnostic)
+        self.side = torch.cuda.Stream() if os.environ.get("P64_FEED_SIDE", "1") != "0" else torch.cuda.current_stream()
         self.pending = None
         # rank 0: (rank, local row) of each kept global sequence
         self.keep = {g: (g // S, g % S) for g in keep if g < world * S}
@@ -1187,6 +1188,12 @@ def main(argv=None):
         cpu["comparable_note"] = ("the CPU leg includes entropy coding; with_vlc is the GPU rate "
                                   "with entropy coding (value stops at the levels)")
     line["cpu_baseline"] = cpu
+    import p64_amd as _p
+    if hasattr(_p.lib(), "p64gpu_vlc_check_errors_"):  # (a bounds-checked coder build, P64GPU_LIB)
+        import ctypes
+        e = ctypes.c_uint32(0)
+        _p.lib().p64gpu_vlc_check_errors_(ctypes.byref(e))
+        line["vlc_check_errors"] = int(e.value)
     print(json.dumps(line), flush=True)
 
 

@@ -343,14 +343,19 @@ struct MeOut {
 // xv/1.1 is 11 sad > 10 sad0 unless the two are equal (the double quotient's
 // error, < 2e-11, cannot cross a gap of 1/11 otherwise), and on equality the
 // rounded quotient decides, computed as written.
+// the inter-without-MC test of the decision (p64.c:745-753): from the two
+// SADs alone, so a caller can act on it before VAR / VAROR are known
+__device__ __forceinline__ bool decide_inter(int sad, int sad0) {
+  bool inter = sad0 < 256 || (sad0 < 768 && 2 * sad > sad0);
+  if (!inter) {
+    const int t = 11 * sad - 10 * sad0;
+    inter = t != 0 ? t > 0 : (double)sad / 256 > ((double)sad0 / 256) / 1.1;
+  }
+  return inter;
+}
 __device__ __forceinline__ int decide_mtype(const MeOut &m) {
   if (m.var < 64 || m.varor > m.var) {
-    bool inter = m.sad0 < 256 || (m.sad0 < 768 && 2 * m.sad > m.sad0);
-    if (!inter) {
-      const int t = 11 * m.sad - 10 * m.sad0;
-      inter = t != 0 ? t > 0 : (double)m.sad / 256 > ((double)m.sad0 / 256) / 1.1;
-    }
-    if (inter) return 2;
+    if (decide_inter(m.sad, m.sad0)) return 2;
     return m.var < 6 ? 5 : 8;  // VAR < D_FILTERTHRESHOLD (6.0)
   }
   return 0;

@@ -1284,6 +1284,22 @@ __global__ __launch_bounds__(64) OCC4 void k_inter_mbg(p64gpu_encode_args a, Blk
   A1.q = 0;
   A1.coded = 1;
   const RecStageB S1 = rec_stage_b<false>(B, w, h, stride, A1);
+  // and the zero-vector source where the MB may turn out a non-MC inter type
+  // (2, 3) with a vector other than (0,0): the decision's inter test needs
+  // only the two SADs (decide_inter), the override is known too -- so these
+  // loads go out at the same level as the ones above instead of after the
+  // statistics (29% of the waves on SURVEY.md 8(d)'s content have such an MB)
+  const bool cand0 = (mvx | mvy) != 0 && li <= 131 && (ov >= 0 ? ov == 2 || ov == 3 : decide_inter(m.sad, m.sad0));
+  RecStageB S0;
+  const bool any0 = uni(__any(cand0));
+  if (any0) {
+    RecStageA A0;
+    A0.p = pos;
+    A0.m = 2u;
+    A0.q = 0;
+    A0.coded = cand0 ? 1 : 0;  // (others: out of range, no traffic)
+    S0 = rec_stage_b<false>(B, w, h, stride, A0);
+  }
   PRIO_LOW();  // the loads are out
   // VAR, VAROR, MWOR at the chosen vector (me.c:229-245 == 313-329): per luma
   // lane the sums over its 8x8 quadrant by byte dot products, sum (r-c)^2 =
@@ -1339,17 +1355,11 @@ __global__ __launch_bounds__(64) OCC4 void k_inter_mbg(p64gpu_encode_args a, Blk
   // is not (0,0); intra none
   uint2 prow[8];
   {
+    // (need0 implies cand0: a non-MC inter type comes from the inter test or
+    // the override, and a refreshed MB is intra)
     const bool need0 = !mt_intra(mt) && !mt_mf(mt) && (mvx | mvy) != 0;
     PredSrc P = S1.pred;
-    if (uni(__any(need0))) {
-      RecStageA A0;
-      A0.p = pos;
-      A0.m = 2u;
-      A0.q = 0;
-      A0.coded = need0 ? 1 : 0;  // (others: out of range, no traffic)
-      const RecStageB S0 = rec_stage_b<false>(B, w, h, stride, A0);
-      if (need0) P = S0.pred;
-    }
+    if (any0 && need0) P = S0.pred;
     pred_rows(P, mt_filter(mt), prow);
     if (mt_intra(mt)) {
 #pragma unroll

@@ -9,6 +9,7 @@
 #   prof[=args]              rocprofv3 --kernel-trace --stats of the bench (--no-cpu) + timed region
 #   pmc=content              tools/pmc_bench.sh passes for that content
 #   probe[=args]             tools/vlc_fault_probe.py with the bounds-checked coder
+#   sadcount=content         executed v_sad_u8 work of k_motion (abtest/lib_sadcount.so, tools/sad_count.py)
 #   py=script.py[,args]      any tracked python tool, e.g. py=tools/stream_time.py
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -56,6 +57,10 @@ for st in "$@"; do
       P64GPU_LIB=$R/abtest/lib_vlccheck.so timeout -k 10 300 python3 -u tools/vlc_fault_probe.py $(echo $arg | tr ',' ' ') \
         > $O/probe$sfx.log 2>&1 || { cat $O/probe$sfx.log; exit 1; }
       cat $O/probe$sfx.log | tee -a $O/summary.txt ;;
+    sadcount)
+      P64GPU_LIB=$R/abtest/lib_sadcount.so timeout -k 10 300 python3 -u tools/sad_count_run.py --content $arg \
+        > $O/sad_$arg.json 2> $O/sad_$arg.err || { tail -20 $O/sad_$arg.err; exit 1; }
+      cut -c1-300 $O/sad_$arg.json | tee -a $O/summary.txt ;;
     py)
       scr=${arg%%,*}
       rest=""
