@@ -1017,10 +1017,18 @@ def main(argv=None):
                 step_graphs[t] = gr
             torch.cuda.synchronize()
 
+            dbg = os.environ.get("P64_FEED_SYNC", "0") != "0"  # (diagnostic: localise a fault)
+
             def timed_launch(t):
                 torch.cuda.current_stream().wait_stream(feed.side)
                 step_graphs[t].replay()
+                if dbg:
+                    torch.cuda.synchronize()
+                    print(f"feed step {t}: replay ok", file=sys.stderr, flush=True)
                 feed.code_host(t)
+                if dbg:
+                    torch.cuda.synchronize()
+                    print(f"feed step {t}: gather ok", file=sys.stderr, flush=True)
             timed_post = None
         # the checked sequences (VERIFY_SEQS: one of each synth seed class) after
         # the warmup, checked against the oracle after the timed region
