@@ -346,6 +346,10 @@ class CodedFeed:
         ({global sequence: bytes}, closed like p64seq_finish) and bit counts."""
         self.torch.cuda.synchronize()
         writers = {g: self.p64s.Writer(fmt) for g in self.keep}
+        if os.environ.get("P64_FEED_SYNC", "0") != "0":  # (diagnostic)
+            for t, per in zip(self.steps, self.kept):
+                print(f"kept step {t}: " + " ".join(f"{g}:{int(per[g][1].item()) & 0xFFFFFFFF}" for g in per),
+                      file=sys.stderr, flush=True)
         for per in self.kept:
             pieces = {g: per[g][0].cpu().numpy().tobytes() for g in writers}
             bits = {g: int(per[g][1].item()) & 0xFFFFFFFF for g in writers}

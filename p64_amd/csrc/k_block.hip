@@ -1042,7 +1042,9 @@ __constant__ InterIdctLim c_idct_lim = make_inter_idct_lim();
 #define INTER_DIRECT_MIN 32  // coded blocks in a wave from which each lane runs its own IQ/IDCT
 #endif
 
-// the decoder's reconstruction through idct_coded_blocks
+// the decoder's reconstruction through idct_coded_blocks (DIRECT: or, in a
+// wave of many small-level inter blocks, one block per lane in registers)
+template <bool DIRECT = false>
 __device__ __forceinline__ void rec_wave_compact(int w, int h, int64_t stride, __amdgpu_buffer_rsrc_t rec,
                                                  const RecStageA &A, const RecStageB &S, uint32_t *slots,
                                                  int lane) {
@@ -1066,7 +1068,23 @@ __device__ __forceinline__ void rec_wave_compact(int w, int h, int64_t stride, _
     np[c][2] = pair(40 + c, 24 + c);
     np[c][3] = pair(16 + c, 48 + c);
   }
-  idct_coded_blocks(S.ck, np, A.q, !S.inter, prow, slots, lane);
+  // a wave with many coded blocks (SURVEY.md 8(d)'s stream: ~50 of 64) runs
+  // one block per lane in registers when every coded block is an inter one
+  // whose levels keep the packed column pass exact (sum l^2 <= the limit
+  // squared bounds max |l|), as k_inter_mbg does; else the LDS pass
+  int ss = 0;
+#pragma unroll
+  for (int c = 0; c < (DIRECT ? 8 : 0); c++)
+#pragma unroll
+    for (int j = 0; j < 4; j++)
+      ss = __builtin_amdgcn_sdot2(__builtin_bit_cast(s16x2, np[c][j]), __builtin_bit_cast(s16x2, np[c][j]), ss, false);
+  const int nck = __popcll(__ballot(S.ck));
+  const bool lane_ok = !S.ck || (S.inter && ss <= c_idct_lim.l2[A.q & 31]);
+  if (DIRECT && nck >= INTER_DIRECT_MIN && uni(__all(lane_ok))) {
+    if (S.ck) iq_idct_inter_rec(np, A.q, prow);
+  } else {
+    idct_coded_blocks(S.ck, np, A.q, !S.inter, prow, slots, lane);
+  }
   {  // every block of a coded MB, wave-wide: the reconstruction (coded blocks,
      // read back from the pass) or the prediction (uncoded blocks)
     const uint32_t uo = A.coded ? ro : BUF_OOB;
@@ -1190,7 +1208,7 @@ __global__ __launch_bounds__(64) OCC4 void k_recon_pk(int w, int h, int64_t stri
     for (int i = 0; i < 4; i++) S.lq[k][i] = lq[k][i];
   PRIO_LOW();
   __shared__ uint32_t slots[RSLOT * (64 / LPB)];
-  rec_wave_compact(w, h, stride, rec, A, S, slots, lane);
+  rec_wave_compact<true>(w, h, stride, rec, A, S, slots, lane);
 }
 
 // ---------------------------------------------------------------------------

@@ -38,11 +38,13 @@ SIMDS = 1024
 XCDS = 8
 WORKLOADS = {  # pmc_bench.sh tag -> {kernel: bench.py pmc key}
     "synth": {"k_motion<2>": "352x288_full31_q8_S256_me", "k_inter_mbg<false, false, true, false>": "352x288_full31_q8_S256_inter",
-              "k_intra_mbg<false, false, true, false>": "352x288_intra_q8_S256", "k_recon_mbg": "352x288_decode_q8_S256"},
+              "k_intra_mbg<false, false, true, false>": "352x288_intra_q8_S256", "k_recon_pk": "352x288_decode_q8_S256",
+              "k_recon_mbg": "352x288_decode_q8_S256_dense"},
     "survey": {"k_motion<2>": "352x288_full31_q8_S256_survey_me",
                "k_inter_mbg<false, false, true, false>": "352x288_full31_q8_S256_survey_inter",
                "k_intra_mbg<false, false, true, false>": "352x288_intra_q8_S256_survey",
-               "k_recon_mbg": "352x288_decode_q8_S256_survey"},
+               "k_recon_pk": "352x288_decode_q8_S256_survey",
+               "k_recon_mbg": "352x288_decode_q8_S256_survey_dense"},
     "noise": {"k_motion<2>": "352x288_full31_q8_S256_noise_me",
               "k_inter_mbg<false, false, true, false>": "352x288_full31_q8_S256_noise_inter"},
     "pan15": {"k_motion<2>": "352x288_full31_q8_S256_pan15_me",
@@ -51,7 +53,8 @@ WORKLOADS = {  # pmc_bench.sh tag -> {kernel: bench.py pmc key}
              "k_inter_mbg<false, false, true, false>": "352x288_full31_q8_S256_flat_inter"},
 }
 ASM_LABEL = {"k_encode<2>": "k_encodeILi2E", "k_intra_mbg<false, false, true, false>": "k_intra_mbgILb0ELb0ELb1ELb0E",
-             "k_recon_blk": "k_recon_blk", "k_recon_mbg": "k_recon_mbg", "k_motion<2>": "k_motionILi2E",
+             "k_recon_blk": "k_recon_blk", "k_recon_mbg": "k_recon_mbg", "k_recon_pk": "k_recon_pk",
+             "k_motion<2>": "k_motionILi2E",
              "k_inter_mbg<false, false, true, false>": "k_inter_mbgILb0ELb0ELb1ELb0E"}
 
 
