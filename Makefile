@@ -74,3 +74,13 @@ abtest/lib_vlccheck.so: p64_amd/csrc/p64vlc.hip $(GPU_OBJS) p64_amd/csrc/synth.o
 	$(HIPCC) $(HIPFLAGS) -DP64_VLC_CHECK -c $< -o abtest/p64vlc_check.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $(GPU_OBJS) p64_amd/csrc/synth.o p64_amd/csrc/p64stream.o \
 	  p64_amd/csrc/p64seq.o p64_amd/csrc/p64prog.o abtest/p64vlc_check.o
+
+# the same checked build with the round-5 status memset (hipMemsetAsync) instead
+# of the zeroing kernel: the A/B of tools/vlc_fault_probe.py stage E
+vlcmemset: abtest/lib_vlcmemset.so
+abtest/lib_vlcmemset.so: p64_amd/csrc/p64vlc.hip $(GPU_OBJS) p64_amd/csrc/synth.o p64_amd/csrc/p64stream.o \
+                         p64_amd/csrc/p64seq.o p64_amd/csrc/p64prog.o
+	mkdir -p abtest
+	$(HIPCC) $(HIPFLAGS) -DP64_VLC_CHECK -DVLC_STATUS_MEMSET -c $< -o abtest/p64vlc_memset.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $(GPU_OBJS) p64_amd/csrc/synth.o p64_amd/csrc/p64stream.o \
+	  p64_amd/csrc/p64seq.o p64_amd/csrc/p64prog.o abtest/p64vlc_memset.o

@@ -672,7 +672,7 @@ __device__ __forceinline__ void mbg_store_rows(const p64gpu_encode_args &a, cons
 // ballots, leave lanes 60..63 idle: 6.25% more waves.)
 template <bool QMB, bool CLAMP, bool POW2 = false, bool BITS = false>
 __global__ __launch_bounds__(64 * MBG_WAVES) void k_intra_mbg(p64gpu_encode_args a, BlkDiv kd, unsigned nmbs,
-                                                                 VlcLenTab vt) {
+                                                                 const uint32_t *vt) {
   __shared__ __align__(16) uint8_t lvl[MBG_WAVES * LVL_WAVE];
   __shared__ uint32_t vlen[BITS ? MBG_WAVES * VLC_LEN_WORDS : 1];
   const int lane = threadIdx.x & 63;
@@ -1257,7 +1257,7 @@ __device__ __forceinline__ void pred_rows(const PredSrc &P, bool filter, uint2 p
 // POW2: a uniform q whose D = 16q is a power of two (qlevel_pk2)
 template <bool QMB, bool OVR, bool POW2 = false, bool BITS = false>
 __global__ __launch_bounds__(64) OCC4 void k_inter_mbg(p64gpu_encode_args a, BlkDiv kd, unsigned nmbs,
-                                                             p64_me_rec *me, VlcLenTab vt) {
+                                                             p64_me_rec *me, const uint32_t *vt) {
   __shared__ __align__(16) uint8_t lds[LVL_WAVE];
   __shared__ uint32_t vlen[BITS ? VLC_LEN_WORDS : 1];
   const int lane = threadIdx.x;
@@ -1572,7 +1572,7 @@ static unsigned mbg_workgroups(unsigned nmbs, unsigned per = MBG_WAVES) {
 
 // the instance of k_intra_mbg for the call's options: <QMB, CLAMP, POW2, BITS>
 template <bool BITS>
-static void intra_launch(const p64gpu_encode_args &a, const VlcLenTab &vt, dim3 grid, dim3 block, BlkDiv kd,
+static void intra_launch(const p64gpu_encode_args &a, const uint32_t *vt, dim3 grid, dim3 block, BlkDiv kd,
                          unsigned nm, hipStream_t st) {
   const bool pow2 = !a.quant_mb && (a.quant & (a.quant - 1)) == 0 && make_qint_tab().ac[a.quant].m == 1;
   if (a.quant_mb)
@@ -1592,18 +1592,15 @@ hipError_t intra_mbg(const p64gpu_encode_args &a, const uint32_t *vlc_len, hipSt
   const unsigned waves = (6u * nm + 63u) / 64u;  // 64 blocks a wave
   const dim3 grid((waves + MBG_WAVES - 1) / MBG_WAVES), block(64 * MBG_WAVES);
   const BlkDiv kd = blk_div(a.width, a.height);
-  VlcLenTab vt{};
-  if (a.vlc_bits) {
-    for (int i = 0; i < VLC_LEN_WORDS; i++) vt.w[i] = vlc_len[i];
-    intra_launch<true>(a, vt, grid, block, kd, nm, st);
-  } else {
-    intra_launch<false>(a, vt, grid, block, kd, nm, st);
-  }
+  if (a.vlc_bits)  // vlc_len: the count's table in device memory (p64gpu_vlc_len_dev_)
+    intra_launch<true>(a, vlc_len, grid, block, kd, nm, st);
+  else
+    intra_launch<false>(a, nullptr, grid, block, kd, nm, st);
   return hipGetLastError();
 }
 
 template <bool BITS>
-static void inter_launch(const p64gpu_encode_args &a, p64_me_rec *me, const VlcLenTab &vt, dim3 grid,
+static void inter_launch(const p64gpu_encode_args &a, p64_me_rec *me, const uint32_t *vt, dim3 grid,
                          dim3 block, BlkDiv kd, unsigned nm, hipStream_t st) {
   const bool ovr = a.mtype_override != nullptr;
   // a uniform q with D = 16q a power of two: the packed quantiser (multiplier 1)
@@ -1627,13 +1624,10 @@ hipError_t inter_mbg(const p64gpu_encode_args &a, p64_me_rec *me, const uint32_t
   const unsigned nm = (unsigned)((int64_t)a.nframes * (a.width / 16) * (a.height / 16));
   const dim3 grid(mbg_workgroups(nm, 1)), block(64);
   const BlkDiv kd = blk_div(a.width, a.height);
-  VlcLenTab vt{};
-  if (a.vlc_bits) {
-    for (int i = 0; i < VLC_LEN_WORDS; i++) vt.w[i] = vlc_len[i];
-    inter_launch<true>(a, me, vt, grid, block, kd, nm, st);
-  } else {
-    inter_launch<false>(a, me, vt, grid, block, kd, nm, st);
-  }
+  if (a.vlc_bits)
+    inter_launch<true>(a, me, vlc_len, grid, block, kd, nm, st);
+  else
+    inter_launch<false>(a, me, nullptr, grid, block, kd, nm, st);
   return hipGetLastError();
 }
 

@@ -21,6 +21,7 @@
 #include "vlc_count.h"
 
 extern "C" int p64gpu_vlc_len_table_(uint32_t *out);
+extern "C" const uint32_t *p64gpu_vlc_len_dev_(void *stream);
 extern "C" int p64gpu_vlc_block_bits_(int width, int height, int nframes, const p64_mb_rec *mb,
                                       const int16_t *coef, uint16_t *blk_bits, void *stream);
 
@@ -201,11 +202,9 @@ int encode_launch(const p64gpu_encode_args *a, const int32_t *mb_list, int count
   if (a->flags & ~P64GPU_FLAG_ME_GIVEN) return fail(P64GPU_E_INVALID, "flags 0x%x: unknown bits", a->flags);
   if (a->vlc_bits && (mb_list || !aligned(a->vlc_bits, 16)))
     return fail(P64GPU_E_INVALID, "vlc_bits: 16-byte aligned, and not with an MB list");
-  uint32_t vlc_len[p64k::VLC_LEN_WORDS];
-  if (a->vlc_bits) {
-    const int s2 = p64gpu_vlc_len_table_(vlc_len);
-    if (s2) return s2;
-  }
+  const uint32_t *vlc_len = nullptr;  // the count's code lengths, device copy (p64vlc.hip)
+  if (a->vlc_bits && !(vlc_len = p64gpu_vlc_len_dev_(stream)))
+    return fail(P64GPU_E_HIP, "vlc_bits: code-length table upload: %s", p64gpu_last_error());
   const bool me_given = (a->flags & P64GPU_FLAG_ME_GIVEN) != 0;
   if (me_given && (a->intra || !a->me || mb_list))
     return fail(P64GPU_E_INVALID, "P64GPU_FLAG_ME_GIVEN needs an inter picture batch with args->me");

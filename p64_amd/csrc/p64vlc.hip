@@ -13,6 +13,7 @@
 
 #include <algorithm>
 #include <cstdint>
+#include <mutex>
 
 #include "../../include/p64gpu.h"
 #include "../../include/p64stream.h"
@@ -356,8 +357,24 @@ __device__ __forceinline__ uint64_t st_wait(const uint64_t *p) {  // until nonze
     __builtin_amdgcn_s_sleep(1);
   }
 }
+// the look-back's status words of a launch, zeroed (k_vlc_blk's precondition)
+__global__ __launch_bounds__(256) void k_vlc_zero(uint4 *p, unsigned n) {
+  const unsigned i = blockIdx.x * 256u + threadIdx.x;
+  if (i < n) p[i] = make_uint4(0u, 0u, 0u, 0u);
+}
+
+// the code tables live in device memory (d_tabs: uploaded once per device,
+// vlc_tables_on_device), not in the kernel arguments: 2.6 KB of by-value
+// tables made every launch's argument block that large (round 6)
+struct DevTabs {
+  VlcTables t;
+  p64k::VlcLenTab l;
+};
+__device__ DevTabs d_tabs;
 template <int MODE>
-__global__ __launch_bounds__(64 * VLC_WAVES) void k_vlc_blk(VlcArgs a, VlcTables Tg, p64k::VlcLenTab Lg) {
+__global__ __launch_bounds__(64 * VLC_WAVES) void k_vlc_blk(VlcArgs a) {
+  const VlcTables &Tg = d_tabs.t;
+  const p64k::VlcLenTab &Lg = d_tabs.l;
   constexpr bool EMIT = MODE != VLC_COUNT, COUNT = MODE != VLC_GIVEN;
   __shared__ VlcTables T;  // per-lane table lookups from LDS, loaded once per workgroup
   __shared__ uint32_t vlen[COUNT ? p64k::VLC_LEN_WORDS : 1];  // the count's code lengths (vlc_count.h)
@@ -664,6 +681,41 @@ thread_local bool g_tab_ok = false;
 thread_local p64k::VlcLenTab g_len;  // the count's code lengths (p64gpu_vlc_len_table_)
 thread_local bool g_len_ok = false;
 
+// d_tabs on the current device: uploaded by the first call on each device
+// from a pinned host copy (built once from the host writer's tables) and
+// synchronised, so every later launch -- on any stream, captured or not --
+// finds it in place.  A first call made while its stream is capturing
+// records the upload as a copy node of the graph instead (the pinned copy
+// outlives every graph) and leaves the device marked not yet uploaded.
+std::mutex g_tabs_mu;
+DevTabs *g_tabs_host = nullptr;
+uint64_t g_tabs_done = 0;  // bit d: device d has d_tabs
+int vlc_tables_on_device(hipStream_t st) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev > 63) return p64gpu_fail_(P64GPU_E_HIP, "vlc: device");
+  std::lock_guard<std::mutex> lk(g_tabs_mu);
+  if (g_tabs_done >> dev & 1) return P64GPU_OK;
+  if (!g_tabs_host) {
+    DevTabs *h = nullptr;
+    if (hipHostMalloc((void **)&h, sizeof(DevTabs), 0) != hipSuccess)
+      return p64gpu_fail_(P64GPU_E_NOMEM, "vlc: pinned table copy");
+    const int s = p64gpu_vlc_len_table_(h->l.w);  // (fills g_tab)
+    if (s) return s;
+    h->t = g_tab;
+    g_tabs_host = h;
+  }
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(st, &cs) != hipSuccess) return p64gpu_fail_(P64GPU_E_HIP, "vlc: capture status");
+  if (hipMemcpyToSymbolAsync(HIP_SYMBOL(d_tabs), g_tabs_host, sizeof(DevTabs), 0, hipMemcpyHostToDevice, st) !=
+      hipSuccess)
+    return p64gpu_fail_(P64GPU_E_HIP, "vlc: table upload");
+  if (cs == hipStreamCaptureStatusNone) {
+    if (hipStreamSynchronize(st) != hipSuccess) return p64gpu_fail_(P64GPU_E_HIP, "vlc: table upload sync");
+    g_tabs_done |= 1ull << dev;
+  }
+  return P64GPU_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -715,6 +767,10 @@ int p64gpu_vlc_pictures(const p64gpu_vlc_args *x, void *stream) {
     if (s) return s;
     g_len_ok = true;
   }
+  {
+    const int s = vlc_tables_on_device((hipStream_t)stream);
+    if (s) return s;
+  }
   int ngob = 0;
   p64s_geometry(fmt, nullptr, nullptr, &ngob);
   const int nmb = ngob * 33;
@@ -748,19 +804,39 @@ int p64gpu_vlc_pictures(const p64gpu_vlc_args *x, void *stream) {
     a.status = scr;  // [nc][nwg][2] uint64: the look-back word and the tail
     const int nwg = (nmb + VLC_WAVES * VLC_MBS - 1) / (VLC_WAVES * VLC_MBS);  // workgroups per picture
     const dim3 grid((unsigned)nwg, (unsigned)nc);
-    hipError_t me = hipMemsetAsync(scr, 0, (size_t)nc * nwg * 16, st);
+    // the status words zeroed by a kernel, not hipMemsetAsync: captured in a
+    // HIP graph, the memset node was seen not to complete before this
+    // launch's look-back on some replays (stale status words: wrong starts,
+    // invalid flags, and stores from a garbage start -- the illegal-address
+    // faults of round 5's variant and of round 6's per-step fed graphs;
+    // DESIGN.md 9c); kernel-to-kernel order within a stream always holds
+    const unsigned nz = (unsigned)nc * (unsigned)nwg;  // uint4 per workgroup
+#ifdef VLC_STATUS_MEMSET  // (the round-5 form, kept for the A/B of tools/vlc_fault_probe.py stage E)
+    hipError_t me = hipMemsetAsync(scr, 0, (size_t)nz * 16, st);
     if (me != hipSuccess) return p64gpu_fail_(P64GPU_E_HIP, hipGetErrorString(me));
+#else
+    hipLaunchKernelGGL(k_vlc_zero, dim3((nz + 255) / 256), dim3(256), 0, st, reinterpret_cast<uint4 *>(scr), nz);
+#endif
     if (x->blk_bits) {  // the blocks' bits from the encoder: no count
       a.blk_bits = x->blk_bits + m0 * 8;
-      hipLaunchKernelGGL(k_vlc_blk<VLC_GIVEN>, grid, dim3(64 * VLC_WAVES), 0, st, a, g_tab, g_len);
+      hipLaunchKernelGGL(k_vlc_blk<VLC_GIVEN>, grid, dim3(64 * VLC_WAVES), 0, st, a);
     } else {
       a.blk_bits = nullptr;
-      hipLaunchKernelGGL(k_vlc_blk<VLC_ONE>, grid, dim3(64 * VLC_WAVES), 0, st, a, g_tab, g_len);
+      hipLaunchKernelGGL(k_vlc_blk<VLC_ONE>, grid, dim3(64 * VLC_WAVES), 0, st, a);
     }
   }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return p64gpu_fail_(P64GPU_E_HIP, hipGetErrorString(e));
   return P64GPU_OK;
+}
+
+// (library-internal) the count's code-length table in device memory (for the
+// BITS instances of the block-layout encoders), uploaded if needed
+const uint32_t *p64gpu_vlc_len_dev_(void *stream) {
+  if (vlc_tables_on_device((hipStream_t)stream)) return nullptr;
+  void *p = nullptr;
+  if (hipGetSymbolAddress(&p, HIP_SYMBOL(d_tabs)) != hipSuccess) return nullptr;
+  return reinterpret_cast<const DevTabs *>(p)->l.w;
 }
 
 // (library-internal) the code-length table of the block bit counts
@@ -793,8 +869,7 @@ int p64gpu_vlc_block_bits_(int width, int height, int nframes, const p64_mb_rec 
                            uint16_t *blk_bits, void *stream) {
   const int fmt = p64s_format_of(width, height);
   if (fmt < 0) return fmt;
-  p64k::VlcLenTab lt;
-  int s = p64gpu_vlc_len_table_(lt.w);
+  int s = vlc_tables_on_device((hipStream_t)stream);
   if (s) return s;
   int ngob = 0;
   p64s_geometry(fmt, nullptr, nullptr, &ngob);
@@ -814,7 +889,7 @@ int p64gpu_vlc_block_bits_(int width, int height, int nframes, const p64_mb_rec 
     a.coef = coef + m0 * 384;
     a.blk_bits = blk_bits + m0 * 8;
     const dim3 grid((unsigned)((nmb + VLC_WAVES * VLC_MBS - 1) / (VLC_WAVES * VLC_MBS)), (unsigned)nc);
-    hipLaunchKernelGGL(k_vlc_blk<VLC_COUNT>, grid, dim3(64 * VLC_WAVES), 0, (hipStream_t)stream, a, g_tab, lt);
+    hipLaunchKernelGGL(k_vlc_blk<VLC_COUNT>, grid, dim3(64 * VLC_WAVES), 0, (hipStream_t)stream, a);
   }
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? P64GPU_OK : p64gpu_fail_(P64GPU_E_HIP, hipGetErrorString(e));

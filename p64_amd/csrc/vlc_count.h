@@ -71,5 +71,11 @@ __device__ __forceinline__ void load_vlc_len(const VlcLenTab &vt, uint32_t *dst,
   dst[lane] = vt.w[lane];
   if (lane < VLC_LEN_WORDS - 64) dst[lane + 64] = vt.w[lane + 64];
 }
+// the same from the device copy (p64gpu_vlc_len_dev_: the table is not a
+// kernel argument)
+__device__ __forceinline__ void load_vlc_len(const uint32_t *vt, uint32_t *dst, int lane) {
+  dst[lane] = vt[lane];
+  if (lane < VLC_LEN_WORDS - 64) dst[lane + 64] = vt[lane + 64];
+}
 
 }  // namespace p64k
