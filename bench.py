@@ -1022,6 +1022,25 @@ def main(argv=None):
             torch.cuda.synchronize()
 
             dbg = os.environ.get("P64_FEED_SYNC", "0") != "0"  # (diagnostic: localise a fault)
+            # the scatter of step t+1's pictures is issued during step t on a
+            # stream of its own (slots differ between consecutive steps); the
+            # first timed step scatters in place, so the region holds exactly
+            # K scatters
+            pf = torch.cuda.Stream()
+            pf_ev = {}
+            t_last = args.warmup + args.steps
+
+            def timed_pre(t):
+                if t not in pf_ev:
+                    pre(t)
+                else:
+                    torch.cuda.current_stream().wait_event(pf_ev.pop(t))
+                if t + 1 <= t_last:
+                    with torch.cuda.stream(pf):
+                        pre(t + 1)
+                        e = torch.cuda.Event()
+                        e.record(pf)
+                    pf_ev[t + 1] = e
 
             def timed_launch(t):
                 torch.cuda.current_stream().wait_stream(feed.side)
@@ -1042,7 +1061,8 @@ def main(argv=None):
             snap[vt] = snapshot(out_of(vt), me, rec[vt % 2], seqs, pic)
         t_first = 1 + args.warmup
         elapsed, kavg, clk = timed_region(torch, dist, world, args.steps, t_first, timed_launch,
-                                          pre if root else None, timed_post,
+                                          (timed_pre if feed is not None and not args.eager else pre)
+                                          if root else None, timed_post,
                                           graph=not args.eager, spinup_ms=args.spinup_ms,
                                           spin={"init": spin_init, "reset": spin_reset,
                                                 "launch": spin_launch,
