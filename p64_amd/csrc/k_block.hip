@@ -1208,7 +1208,7 @@ __global__ __launch_bounds__(64) OCC4 void k_recon_pk(int w, int h, int64_t stri
     for (int i = 0; i < 4; i++) S.lq[k][i] = lq[k][i];
   PRIO_LOW();
   __shared__ uint32_t slots[RSLOT * (64 / LPB)];
-  rec_wave_compact<true>(w, h, stride, rec, A, S, slots, lane);
+  rec_wave_compact<false>(w, h, stride, rec, A, S, slots, lane);  // (DIRECT: 119 VGPRs, 4 waves: 39.6 vs 36.1 us, r06f)
 }
 
 // ---------------------------------------------------------------------------
