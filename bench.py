@@ -675,7 +675,7 @@ def load_pmc(path, workload_key):
 
 
 def timing_note(args, root=False):
-    if root and args.gather == "coded" and not args.eager:
+    if root and args.gather == "coded" and not args.eager and os.environ.get("P64_FEED_GRAPHS", "0") != "0":
         return "HIP events around each step's graph replay (encode + entropy coder)"
     if args.eager or root:
         return "HIP events around each launch (kernel + launch gap)"
@@ -1003,7 +1003,8 @@ def main(argv=None):
         for t in range(1 + args.warmup):  # intra picture + warmup, untimed
             step(t)
         timed_launch, timed_post = launch, (post if root else None)
-        if feed is not None and not args.eager:
+        feed_graphs = feed is not None and not args.eager and os.environ.get("P64_FEED_GRAPHS", "0") != "0"
+        if feed_graphs:
             # --feed root, coded: each timed step's device work (encode + coder
             # + the phase bookkeeping) captured as its own HIP graph before the
             # region and replayed in the step, so the host issues four calls a
@@ -1037,6 +1038,19 @@ def main(argv=None):
             torch.cuda.synchronize()
 
             dbg = os.environ.get("P64_FEED_SYNC", "0") != "0"  # (diagnostic: localise a fault)
+
+            def timed_launch(t):
+                torch.cuda.current_stream().wait_stream(feed.side)
+                step_graphs[t].replay()
+                if dbg:
+                    torch.cuda.synchronize()
+                    print(f"feed step {t}: replay ok", file=sys.stderr, flush=True)
+                feed.code_host(t)
+                if dbg:
+                    torch.cuda.synchronize()
+                    print(f"feed step {t}: gather ok", file=sys.stderr, flush=True)
+            timed_post = None
+        if feed is not None:
             # the scatter of step t+1's pictures is issued during step t on a
             # stream of its own (slots differ between consecutive steps); the
             # first timed step scatters in place, so the region holds exactly
@@ -1056,18 +1070,6 @@ def main(argv=None):
                         e = torch.cuda.Event()
                         e.record(pf)
                     pf_ev[t + 1] = e
-
-            def timed_launch(t):
-                torch.cuda.current_stream().wait_stream(feed.side)
-                step_graphs[t].replay()
-                if dbg:
-                    torch.cuda.synchronize()
-                    print(f"feed step {t}: replay ok", file=sys.stderr, flush=True)
-                feed.code_host(t)
-                if dbg:
-                    torch.cuda.synchronize()
-                    print(f"feed step {t}: gather ok", file=sys.stderr, flush=True)
-            timed_post = None
         # the checked sequences (VERIFY_SEQS: one of each synth seed class) after
         # the warmup, checked against the oracle after the timed region
         seqs = [i for i in VERIFY_SEQS if i < S]
@@ -1076,7 +1078,7 @@ def main(argv=None):
             snap[vt] = snapshot(out_of(vt), me, rec[vt % 2], seqs, pic)
         t_first = 1 + args.warmup
         elapsed, kavg, clk = timed_region(torch, dist, world, args.steps, t_first, timed_launch,
-                                          (timed_pre if feed is not None and not args.eager else pre)
+                                          (timed_pre if feed is not None else pre)
                                           if root else None, timed_post,
                                           graph=not args.eager, spinup_ms=args.spinup_ms,
                                           spin={"init": spin_init, "reset": spin_reset,
@@ -1177,7 +1179,7 @@ def main(argv=None):
                                        + ("the entropy-coded pictures (GPU VLC on each rank in the step)"
                                           if args.gather == "coded" else "levels + records")
                                        + ("; roofline times each step's device work: encode + coder, one "
-                                          "graph replay per step" if feed is not None and not args.eager
+                                          "graph replay per step" if feed_graphs
                                           else "; roofline times the encode launch alone") + ")")},
             "roofline": roofline(mbs_launch * BYTES_PER_MB_FIXED + lvl_bytes, kavg, kernel, pmc,
                                  algorithmic_bytes_per_mb=round(BYTES_PER_MB_FIXED + lvl_bytes / mbs_launch, 1),
