@@ -281,8 +281,7 @@ class CodedFeed:
         self.gq = torch.full((S, nmb // 33), quant, dtype=torch.uint8, device="cuda")
         self.trs = [torch.full((S,), t, dtype=torch.int32, device="cuda") for t in range(32)]
         self.seq_bits = torch.zeros(S, dtype=torch.int64, device="cuda")  # bits so far per sequence
-        self.phase = torch.zeros(S, dtype=torch.uint8, device="cuda")
-        self.mx = [torch.zeros(1, dtype=torch.int64, device="cuda") for _ in range(2)]
+        self.mx = [torch.zeros(1, dtype=torch.int32, device="cuda") for _ in range(2)]  # the longest picture
         self.bits = [None, None]
         self.ev = [torch.cuda.Event(), torch.cuda.Event()]
         # (P64_FEED_SIDE=0: gathers on the encode stream itself -- diagnostic)
@@ -302,19 +301,16 @@ class CodedFeed:
 
     def code_gpu(self, t, o):
         """The device work of step t's coding on the current stream (no host
-        synchronisation, capturable in a HIP graph): the pictures' bit phases,
-        the coder, the running bit counts, the longest picture.  The caller
-        has made the stream wait for the side stream first."""
-        torch = self.torch
+        synchronisation, capturable in a HIP graph): the coder, which takes
+        each picture's bit phase from its sequence's running bit count,
+        advances it and keeps the step's longest picture (p64gpu_vlc_args
+        seq_bits / max_bits, ABI v3: two launches, no bookkeeping kernels).
+        The caller has made the stream wait for the side stream first."""
         k = t % 2
-        ph = (self.seq_bits & 7).to(torch.uint8)
-        self.phase.copy_(ph)
         _, bits = self.p64s.vlc_pictures(o.mb, o.coef, self.gq, self.trs[t % 32], width=self.w, height=self.h,
-                                         phase=self.phase, buffers=self.bufs[k], host_bits=False,
-                                         blk_bits=o.vlc_bits)
-        self.seq_bits.add_(bits.to(torch.int64) - self.phase.to(torch.int64))
+                                         buffers=self.bufs[k], host_bits=False, blk_bits=o.vlc_bits,
+                                         seq_bits=self.seq_bits, max_bits=self.mx[k])
         self.bits[k] = bits
-        torch.amax(bits.to(torch.int64), dim=0, keepdim=True, out=self.mx[k])
 
     def code_host(self, t):
         """After step t's device work is issued: its event, and the gather of

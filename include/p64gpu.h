@@ -57,7 +57,8 @@
  * ABI version 3 (round 6): p64gpu_decode_recon_packed (packed levels +
  * per-group index, p64s_pack_levels in p64stream.h); p64gpu_vlc_pictures
  * accepts any device-addressable pointer (pinned host memory included) and
- * refuses pageable host memory.
+ * refuses pageable host memory; p64gpu_vlc_args.seq_bits / .max_bits
+ * (appended).
  */
 #ifndef P64GPU_H
 #define P64GPU_H
@@ -290,6 +291,15 @@ typedef struct {
                                encoder (p64gpu_encode_args.vlc_bits, same
                                records and levels), 16-byte aligned, read
                                only: the blocks are not counted again        */
+  int64_t *seq_bits;        /* (ABI v3) NULL, or [nframes] 8-byte aligned: the
+                               running bit count of each picture's sequence;
+                               the picture starts at phase seq_bits[i] & 7
+                               (`phase` is then not read) and seq_bits[i]
+                               advances by the picture's bits (not for an
+                               invalid picture) -- a sequence's pictures coded
+                               call after call without a host round trip    */
+  uint32_t *max_bits;       /* (ABI v3) NULL, or [1]: set to the largest
+                               bits[i] of the call's valid pictures         */
 } p64gpu_vlc_args;
 int64_t p64gpu_vlc_max_bytes(int width, int height);
 int p64gpu_vlc_pictures(const p64gpu_vlc_args *args, void *stream);

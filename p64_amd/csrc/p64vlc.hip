@@ -56,6 +56,8 @@ struct VlcArgs {
   uint32_t *bits;     // [nframes]
   uint32_t *status;   // [nframes][workgroups][2] uint64 (look-back word, tail), zeroed before the launch
   uint16_t *blk_bits; // [nframes][nmb][8], raster order: [1 + b] block b's bits
+  int64_t *seq_bits;  // NULL or [nframes]: the sequences' running bit counts (phase = & 7; updated)
+  uint32_t *max_bits; // NULL or [1]: the longest valid picture's bits (zeroed by k_vlc_zero)
 };
 
 __device__ __forceinline__ bool mt_quant(int m) { return m == 1 || m == 3 || m == 6 || m == 9; }
@@ -358,9 +360,10 @@ __device__ __forceinline__ uint64_t st_wait(const uint64_t *p) {  // until nonze
   }
 }
 // the look-back's status words of a launch, zeroed (k_vlc_blk's precondition)
-__global__ __launch_bounds__(256) void k_vlc_zero(uint4 *p, unsigned n) {
+__global__ __launch_bounds__(256) void k_vlc_zero(uint4 *p, unsigned n, uint32_t *max_bits) {
   const unsigned i = blockIdx.x * 256u + threadIdx.x;
   if (i < n) p[i] = make_uint4(0u, 0u, 0u, 0u);
+  if (max_bits && i == 0) *max_bits = 0u;
 }
 
 // the code tables live in device memory (d_tabs: uploaded once per device,
@@ -547,7 +550,7 @@ __global__ __launch_bounds__(64 * VLC_WAVES) void k_vlc_blk(VlcArgs a) {
     int64_t first = 0;
     bool bad_all = wbad;
     if (G == 0) {
-      first = a.phase ? a.phase[fi] : 0;
+      first = a.seq_bits ? (a.seq_bits[fi] & 7) : (a.phase ? a.phase[fi] : 0);
     } else {
       for (int v = G - 1;;) {
         const uint64_t inc = __ballot((s >> 62) == 2), zero = __ballot(s == 0);
@@ -568,7 +571,14 @@ __global__ __launch_bounds__(64 * VLC_WAVES) void k_vlc_blk(VlcArgs a) {
     const int64_t endb = first + wt;
     if (lane == 0 && VLC_OK(fi < a.nframes && G < ng, 4)) {
       st_store(stw + 2 * G, ST_INCL | (bad_all ? ST_BAD : 0) | (uint64_t)(uint32_t)endb);
-      if (G == ng - 1 && VLC_OK(fi < a.nframes, 5)) a.bits[fi] = (bad_all || endb + 64 > a.out_words * 32) ? 0xFFFFFFFFu : (uint32_t)endb;
+      if (G == ng - 1 && VLC_OK(fi < a.nframes, 5)) {
+        const bool ok = !bad_all && endb + 64 <= a.out_words * 32;
+        a.bits[fi] = ok ? (uint32_t)endb : 0xFFFFFFFFu;
+        // the sequence continues after this picture: its bits less the phase
+        // (WG 0 read seq_bits before publishing its end, which this one saw)
+        if (a.seq_bits && ok) a.seq_bits[fi] = (a.seq_bits[fi] & ~(int64_t)7) + endb;
+        if (a.max_bits && ok) atomicMax(a.max_bits, (uint32_t)endb);
+      }
       s_first = first;
     }
   }
@@ -751,7 +761,7 @@ int p64gpu_vlc_pictures(const p64gpu_vlc_args *x, void *stream) {
       ((uintptr_t)x->out & 3))
     return p64gpu_fail_(P64GPU_E_INVALID, "vlc: out_stride below p64gpu_vlc_max_bytes or not 4-aligned");
   if (((uintptr_t)x->scratch & 7) || ((uintptr_t)x->coef & 15) || ((uintptr_t)x->mb & 3) ||
-      ((uintptr_t)x->blk_bits & 15))
+      ((uintptr_t)x->blk_bits & 15) || ((uintptr_t)x->seq_bits & 7) || ((uintptr_t)x->max_bits & 3))
     return p64gpu_fail_(P64GPU_E_INVALID,
                         "vlc: scratch must be 8-byte, coef and blk_bits 16-byte, mb 4-byte aligned");
   p64gpu_vlc_args y = *x;  // the pointers as the device addresses them
@@ -759,7 +769,7 @@ int p64gpu_vlc_pictures(const p64gpu_vlc_args *x, void *stream) {
   if (x->f && !(y.f = device_addressable(x->f)))                                                            \
     return p64gpu_fail_(P64GPU_E_INVALID, "vlc: " #f " is not device-addressable memory (pageable host memory?)");
   VLC_ADDR(mb) VLC_ADDR(coef) VLC_ADDR(gquant) VLC_ADDR(mquant) VLC_ADDR(tr) VLC_ADDR(phase) VLC_ADDR(out)
-  VLC_ADDR(bits) VLC_ADDR(scratch) VLC_ADDR(blk_bits)
+  VLC_ADDR(bits) VLC_ADDR(scratch) VLC_ADDR(blk_bits) VLC_ADDR(seq_bits) VLC_ADDR(max_bits)
 #undef VLC_ADDR
   x = &y;
   if (!g_len_ok) {  // (fills g_tab too)
@@ -799,6 +809,8 @@ int p64gpu_vlc_pictures(const p64gpu_vlc_args *x, void *stream) {
     a.out = reinterpret_cast<uint32_t *>(x->out) + (size_t)f0 * out_words;
     a.out_words = out_words;
     a.bits = x->bits + f0;
+    a.seq_bits = x->seq_bits ? x->seq_bits + f0 : nullptr;
+    a.max_bits = x->max_bits;
     // this chunk's [6][nc][nmb] words of the scratch
     uint32_t *scr = x->scratch + 6 * m0;
     a.status = scr;  // [nc][nwg][2] uint64: the look-back word and the tail
@@ -813,9 +825,11 @@ int p64gpu_vlc_pictures(const p64gpu_vlc_args *x, void *stream) {
     const unsigned nz = (unsigned)nc * (unsigned)nwg;  // uint4 per workgroup
 #ifdef VLC_STATUS_MEMSET  // (the round-5 form, kept for the A/B of tools/vlc_fault_probe.py stage E)
     hipError_t me = hipMemsetAsync(scr, 0, (size_t)nz * 16, st);
+    if (me == hipSuccess && f0 == 0 && x->max_bits) me = hipMemsetAsync(x->max_bits, 0, 4, st);
     if (me != hipSuccess) return p64gpu_fail_(P64GPU_E_HIP, hipGetErrorString(me));
 #else
-    hipLaunchKernelGGL(k_vlc_zero, dim3((nz + 255) / 256), dim3(256), 0, st, reinterpret_cast<uint4 *>(scr), nz);
+    hipLaunchKernelGGL(k_vlc_zero, dim3((nz + 255) / 256), dim3(256), 0, st, reinterpret_cast<uint4 *>(scr), nz,
+                       f0 == 0 ? x->max_bits : nullptr);
 #endif
     if (x->blk_bits) {  // the blocks' bits from the encoder: no count
       a.blk_bits = x->blk_bits + m0 * 8;

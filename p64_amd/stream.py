@@ -417,7 +417,8 @@ class VlcArgs(ctypes.Structure):
                 ("flags", ctypes.c_int), ("mb", ctypes.c_void_p), ("coef", ctypes.c_void_p),
                 ("gquant", ctypes.c_void_p), ("mquant", ctypes.c_void_p), ("tr", ctypes.c_void_p),
                 ("phase", ctypes.c_void_p), ("out", ctypes.c_void_p), ("out_stride", ctypes.c_int64),
-                ("bits", ctypes.c_void_p), ("scratch", ctypes.c_void_p), ("blk_bits", ctypes.c_void_p)]
+                ("bits", ctypes.c_void_p), ("scratch", ctypes.c_void_p), ("blk_bits", ctypes.c_void_p),
+                ("seq_bits", ctypes.c_void_p), ("max_bits", ctypes.c_void_p)]
 
 
 def vlc_buffers(n: int, width: int, height: int):
@@ -433,13 +434,17 @@ def vlc_buffers(n: int, width: int, height: int):
 
 
 def vlc_pictures(mb, coef, gquant, tr, *, width: int, height: int, phase=None, mquant=None,
-                 buffers=None, host_bits: bool = True, blk_bits=None):
+                 buffers=None, host_bits: bool = True, blk_bits=None, seq_bits=None, max_bits=None):
     """H.261 bits of a batch of pictures on the GPU.  All inputs are CUDA(HIP)
     tensors: mb [n, nmb, 4] int8, coef [n, nmb, 6, 64] int16, gquant [n, ngob]
     uint8, tr [n] int32, phase [n] uint8 or None, mquant [n, nmb] uint8 or None.
     buffers: (out, bits, scratch) from vlc_buffers, reused across calls.
     blk_bits: int16 [n, nmb, 8] from the encoder (FrameBatchOut.vlc_bits of the
     same records and levels): the coder skips its count pass.
+    seq_bits: int64 [n], the sequences' running bit counts: each picture
+    starts at phase seq_bits & 7 (phase is not read) and seq_bits advances by
+    its bits, on the device.  max_bits: int32 [1], set to the longest
+    picture's bit count.
     Returns (out [n, stride] uint8 tensor, bits [n] list of ints) -- or, with
     host_bits=False, the device bits tensor (no synchronisation)."""
     import torch
@@ -464,7 +469,9 @@ def vlc_pictures(mb, coef, gquant, tr, *, width: int, height: int, phase=None, m
                 mquant=mquant.data_ptr() if mquant is not None else None, tr=tr.data_ptr(),
                 phase=phase.data_ptr() if phase is not None else None, out=out.data_ptr(),
                 out_stride=stride, bits=bits.data_ptr(), scratch=scratch.data_ptr(),
-                blk_bits=blk_bits.data_ptr() if blk_bits is not None else None)
+                blk_bits=blk_bits.data_ptr() if blk_bits is not None else None,
+                seq_bits=seq_bits.data_ptr() if seq_bits is not None else None,
+                max_bits=max_bits.data_ptr() if max_bits is not None else None)
     _check(L.p64gpu_vlc_pictures(ctypes.byref(a), _stream(torch)))
     if not host_bits:
         return out, bits[:n]

@@ -130,7 +130,7 @@ def test_vlc_args_layout_matches_ctypes(p64, tmp_path):
 int main(void) {
   printf("sizeof_args %zu\n", sizeof(p64gpu_vlc_args));
   O(width); O(height); O(nframes); O(flags); O(mb); O(coef); O(gquant); O(mquant); O(tr);
-  O(phase); O(out); O(out_stride); O(bits); O(scratch); O(blk_bits);
+  O(phase); O(out); O(out_stride); O(bits); O(scratch); O(blk_bits); O(seq_bits); O(max_bits);
   return 0;
 }''')
     exe = tmp_path / "vlayout"

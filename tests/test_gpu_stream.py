@@ -572,3 +572,38 @@ def test_gpu_vlc_bits_in_pinned_host_memory(p64, torch_dev):
         assert not pageable.any()
     finally:
         hip.hipHostFree(hp)
+
+
+@pytest.mark.parametrize("name", ["qcif_tss", "cif_full31", "qcif_q1"])
+def test_gpu_vlc_seq_bits_continue_the_stream(p64, torch_dev, name):
+    """p64gpu_vlc_args.seq_bits (ABI v3): each picture starts at its
+    sequence's running bit count & 7 and the count advances on the device,
+    call after call, with no host round trip; max_bits gets the longest
+    picture.  Two copies of the fixture's sequence side by side (one starting
+    5 bits into its stream), reassembled == the reference's .p64."""
+    from p64_amd import stream
+    torch = torch_dev
+    z = load(f"seq_{name}.npz")
+    w, h, n = int(z["width"]), int(z["height"]), int(z["nframes"])
+    fmt = stream.format_of(w, h)
+    mb, coef, gq, uq = fixture_records(z, fmt)
+    d = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()  # noqa: E731
+    seq = torch.tensor([0, 5], dtype=torch.int64, device="cuda")
+    mx = torch.zeros(1, dtype=torch.int32, device="cuda")
+    bufs = stream.vlc_buffers(2, w, h)
+    asm = [stream.BitAssembler(), stream.BitAssembler()]
+    asm[1].append(b"\xa8", 5)  # (5 bits of something before the second copy's stream)
+    for t in range(n):
+        two = lambda a: np.stack([a[t], a[t]])  # noqa: E731
+        out, bits = stream.vlc_pictures(d(two(mb)), d(two(coef)), d(two(gq)), d(np.array([t % 32] * 2, np.int32)),
+                                        width=w, height=h, mquant=d(two(uq)), buffers=bufs, seq_bits=seq,
+                                        max_bits=mx)
+        assert int(mx.item()) == max(bits)
+        o = out.cpu().numpy()
+        for i in range(2):
+            asm[i].append(o[i].tobytes(), bits[i])
+        assert seq.cpu().tolist() == [asm[0].nbits, asm[1].nbits]
+    data = asm[0].end(fmt, n % 32)
+    assert hashlib.sha256(data).hexdigest() == str(z["stream_sha256"])
+    data1 = asm[1].end(fmt, n % 32)
+    assert len(data1) == len(data) + 1 or len(data1) == len(data)  # (shifted by 5 bits)
