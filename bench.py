@@ -1000,6 +1000,29 @@ def main(argv=None):
             step(t)
         timed_launch, timed_post = launch, (post if root else None)
         feed_graphs = feed is not None and not args.eager and os.environ.get("P64_FEED_GRAPHS", "0") != "0"
+        if feed is not None and not feed_graphs:
+            # eager fed steps with every launch's arguments checked and packed
+            # before the region (p64_amd.prepare_encode / stream.prepare_vlc):
+            # the host issues the step without the wrappers' per-call checks
+            prep = {}
+            for t in range(1 + args.warmup, 1 + args.warmup + args.steps):
+                o = out_of(t)
+                enc = p64_amd.prepare_encode(frames[slot(t)].reshape(-1), rec[(t + 1) % 2], rec[t % 2], li,
+                                             width=w, height=h, intra=False, quant=args.quant, me_mode=mode,
+                                             search_limit=args.search_limit, out=o)
+                vlc, vbits = p64s.prepare_vlc(o.mb, o.coef, feed.gq, feed.trs[t % 32], width=w, height=h,
+                                              buffers=feed.bufs[t % 2], blk_bits=o.vlc_bits,
+                                              seq_bits=feed.seq_bits, max_bits=feed.mx[t % 2])
+                prep[t] = (enc, vlc, vbits)
+
+            def timed_launch(t):
+                prep[t][0]()
+
+            def timed_post(t):
+                torch.cuda.current_stream().wait_stream(feed.side)
+                prep[t][1]()
+                feed.bits[t % 2] = prep[t][2]
+                feed.code_host(t)
         if feed_graphs:
             # --feed root, coded: each timed step's device work (encode + coder
             # + the phase bookkeeping) captured as its own HIP graph before the

@@ -454,6 +454,43 @@ def encode_frames(cur, ref, recon, last_intra, *, width: int, height: int, intra
     return out
 
 
+def prepare_encode(cur, ref, recon, last_intra, *, width: int, height: int, intra: bool, quant: int = 8,
+                   me_mode: int = ME_TSS, search_limit: int = 15, out: FrameBatchOut, stream=None):
+    """encode_frames' launch with its arguments checked and packed once: the
+    returned function issues it again with the same buffers (no per-call
+    Python checks -- for host loops that relaunch the same step shapes, e.g.
+    bench.py's fed path).  The tensors must outlive the returned function."""
+    torch = _torch()
+    stride = picture_bytes(width, height)
+    nframes = cur.numel() // stride
+    for t, dt, name in ((cur, torch.uint8, "cur"), (recon, torch.uint8, "recon"),
+                        (last_intra, torch.uint8, "last_intra"), (out.coef, torch.int16, "out.coef"),
+                        (out.mb, torch.int8, "out.mb")):
+        _dev_check(t, dt, name)
+    nmb_all = nframes * (width // 16) * (height // 16)
+    if nframes < 1 or recon.numel() < nframes * stride or last_intra.numel() < nmb_all or \
+            (not intra and (ref is None or ref.numel() < nframes * stride)) or \
+            out.coef.numel() < nmb_all * 384 or out.mb.numel() < nmb_all * 4:
+        raise P64GpuError("prepare_encode: buffer sizes do not match nframes x picture geometry")
+    if out.me is None and not intra:
+        raise P64GpuError("prepare_encode: inter batches need out.me")
+    a = EncodeArgs(width=width, height=height, nframes=nframes, intra=int(bool(intra)), quant=quant,
+                   me_mode=me_mode, search_limit=search_limit, flags=0, frame_stride=stride,
+                   cur=cur.data_ptr(), ref=(ref.data_ptr() if ref is not None else None), recon=recon.data_ptr(),
+                   last_intra=last_intra.data_ptr(), quant_mb=None, mtype_override=None,
+                   coef=out.coef.data_ptr(), mb=out.mb.data_ptr(),
+                   me=(out.me.data_ptr() if out.me is not None else None),
+                   nzmask=(out.nz.data_ptr() if out.nz is not None else None),
+                   vlc_bits=(out.vlc_bits.data_ptr() if out.vlc_bits is not None else None))
+    st = ctypes.c_void_p((stream or torch.cuda.current_stream()).cuda_stream)
+    L, ref_a = lib(), ctypes.byref(a)
+
+    def launch():
+        _check(L.p64gpu_encode_frames(ref_a, st))
+    launch.args = a  # (kept alive with the function)
+    return launch
+
+
 def decode_recon(ref, recon, coef, mb, quant_mb, coded_mask, *, width: int, height: int):
     """Decoder reconstruction (p64.c:1179-1237 + 971-1013) of coded MBs into recon."""
     torch = _torch()

@@ -481,6 +481,37 @@ def vlc_pictures(mb, coef, gquant, tr, *, width: int, height: int, phase=None, m
     return out, b
 
 
+def prepare_vlc(mb, coef, gquant, tr, *, width: int, height: int, buffers, blk_bits=None, seq_bits=None,
+                max_bits=None, mquant=None, phase=None, stream=None):
+    """vlc_pictures' launch checked and packed once (host_bits=False): the
+    returned function issues it again with the same buffers, without the
+    per-call Python checks (bench.py's fed path).  The tensors must outlive
+    it.  Returns (launch, bits tensor)."""
+    import torch
+
+    from . import _stream, _torch
+    _torch()
+    n = int(tr.numel())
+    _, _, ngob = geometry(format_of(width, height))
+    nmb = ngob * 33
+    out, bits, scratch = buffers
+    if mb.numel() != n * nmb * 4 or coef.numel() != n * nmb * 384 or gquant.numel() != n * ngob or \
+            out.shape[0] < n or bits.numel() < n or scratch.numel() < 6 * n * nmb:
+        raise P64GpuError("prepare_vlc: buffer sizes do not match the picture format")
+    p = lambda t: t.data_ptr() if t is not None else None  # noqa: E731
+    a = VlcArgs(width=width, height=height, nframes=n, flags=0, mb=mb.data_ptr(), coef=coef.data_ptr(),
+                gquant=gquant.data_ptr(), mquant=p(mquant), tr=tr.data_ptr(), phase=p(phase), out=out.data_ptr(),
+                out_stride=int(out.shape[1]), bits=bits.data_ptr(), scratch=scratch.data_ptr(),
+                blk_bits=p(blk_bits), seq_bits=p(seq_bits), max_bits=p(max_bits))
+    st = ctypes.c_void_p((stream or torch.cuda.current_stream()).cuda_stream) if stream is not None else _stream(torch)
+    L, ref_a = lib(), ctypes.byref(a)
+
+    def launch():
+        _check(L.p64gpu_vlc_pictures(ref_a, st))
+    launch.args = a
+    return launch, bits[:n]
+
+
 class BitAssembler:
     """Concatenates pictures coded at a bit phase (vlc_pictures) into one
     stream, and closes it like p64s_write_end (trailer header + ones)."""
