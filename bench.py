@@ -283,21 +283,72 @@ class CodedFeed:
         self.seq_bits = torch.zeros(S, dtype=torch.int64, device="cuda")  # bits so far per sequence
         self.mx = [torch.zeros(1, dtype=torch.int32, device="cuda") for _ in range(2)]  # the longest picture
         self.bits = [None, None]
-        self.ev = [torch.cuda.Event(), torch.cuda.Event()]
+        self.ev = [torch.cuda.Event(), torch.cuda.Event()]  # step t's coder done (t % 2)
+        self.enc_ev = [torch.cuda.Event(), torch.cuda.Event()]  # step t's encode done (forked coder)
         # (P64_FEED_SIDE=0: gathers on the encode stream itself -- diagnostic)
         self.side = torch.cuda.Stream() if os.environ.get("P64_FEED_SIDE", "1") != "0" else torch.cuda.current_stream()
+        # the coder on the side stream, beside the next step's encode (the
+        # encode's outputs alternate between two sets, see before_encode)
+        self.fork = os.environ.get("P64_FEED_FORK", "1") != "0" and self.side != torch.cuda.current_stream()
         self.pending = None
         # rank 0: (rank, local row) of each kept global sequence
         self.keep = {g: (g // S, g % S) for g in keep if g < world * S}
+        rows = {}
+        for g, (r, i) in sorted(self.keep.items()):
+            rows.setdefault(r, ([], []))
+            rows[r][0].append(g)
+            rows[r][1].append(i)
+        self.keep_rows = {r: (gs, torch.tensor(ix, dtype=torch.int64, device="cuda")) for r, (gs, ix) in rows.items()}
         self.kept = []  # per coded step: {global sequence: (piece tensor, bits tensor)}
         self.steps = []
 
-    def code(self, t, o):
+    def before_encode(self, t):
+        """Forked coder: step t's encode overwrites the output set step t-2's
+        coder reads (the sets alternate), so the encode stream waits for that
+        coder's event first (it ended during step t-1's encode)."""
+        if self.fork:
+            self.torch.cuda.current_stream().wait_event(self.ev[t % 2])
+
+    def code(self, t, o, vlc=None):
         """Step t's pictures (outputs o of the encode) into bits, then the
-        gather of step t-1 (code_gpu + code_host)."""
-        self.torch.cuda.current_stream().wait_stream(self.side)  # (the gather of step t-2 has read buffer t % 2)
-        self.code_gpu(t, o)
-        self.code_host(t)
+        gather of step t-1.  Forked (the default): the gather of step t-1 is
+        issued first on the side stream, then step t's coder behind an event
+        on the encode stream, so the coder of step t runs beside the encode
+        of step t+1 and the host's one wait (the gather's size read-back)
+        ends when step t-1's coder does.  Otherwise (P64_FEED_FORK=0) the
+        coder runs on the encode stream (code_gpu + code_host).
+        vlc: a prepared coder launch (stream.prepare_vlc on the side stream)
+        and its bits, instead of code_gpu's call."""
+        torch = self.torch
+        if not self.fork:
+            torch.cuda.current_stream().wait_stream(self.side)  # (the gather of step t-2 has read buffer t % 2)
+            if vlc is None:
+                self.code_gpu(t, o)
+            else:
+                vlc[0]()
+                self.bits[t % 2] = vlc[1]
+            self.code_host(t)
+            return
+        self.enc_ev[t % 2].record(torch.cuda.current_stream())
+        if self.pending is not None:
+            self._gather(self.pending)
+            self.pending = None
+        with torch.cuda.stream(self.side):
+            self.side.wait_event(self.enc_ev[t % 2])
+            if vlc is None:
+                self.code_gpu(t, o)
+            else:
+                vlc[0]()
+                self.bits[t % 2] = vlc[1]
+            self.ev[t % 2].record(self.side)
+        if self.world == 1:
+            # no size read-back at one rank, so step t's gather follows its
+            # coder at once: issued before it (one step late), its small
+            # kernels waited ~90 us for the CUs the encode held and delayed
+            # the coder behind them (profiles/r06n_fed_trace.txt)
+            self._gather(t)
+        else:
+            self.pending = t
 
     def code_gpu(self, t, o):
         """The device work of step t's coding on the current stream (no host
@@ -331,10 +382,18 @@ class CodedFeed:
         k = t % 2
         with torch.cuda.stream(self.side):
             self.side.wait_event(self.ev[k])
-            got = gather_coded(self.world, self.rank, self.bufs[k][0], self.bits[k], mx=self.mx[k])
+            if self.world == 1:
+                # one rank: its pictures are already resident on rank 0 (the
+                # gather is the identity), so no size is read back -- the kept
+                # pieces below are whole buffer rows
+                got = ([self.bufs[k][0]], [self.bits[k]])
+            else:
+                got = gather_coded(self.world, self.rank, self.bufs[k][0], self.bits[k], mx=self.mx[k])
             if got is not None and self.keep:
                 pays, bls = got
-                self.kept.append({g: (pays[r][i].clone(), bls[r][i].clone()) for g, (r, i) in self.keep.items()})
+                # one indexing op per rank for the kept sequences' pieces
+                self.kept.append([(gs, pays[r].index_select(0, ix), bls[r].index_select(0, ix))
+                                  for r, (gs, ix) in self.keep_rows.items()])
                 self.steps.append(t)
 
     def streams(self, fmt, end_tr):
@@ -342,13 +401,16 @@ class CodedFeed:
         ({global sequence: bytes}, closed like p64seq_finish) and bit counts."""
         self.torch.cuda.synchronize()
         writers = {g: self.p64s.Writer(fmt) for g in self.keep}
-        if os.environ.get("P64_FEED_SYNC", "0") != "0":  # (diagnostic)
-            for t, per in zip(self.steps, self.kept):
-                print(f"kept step {t}: " + " ".join(f"{g}:{int(per[g][1].item()) & 0xFFFFFFFF}" for g in per),
+        for t, per in zip(self.steps, self.kept):
+            pieces, bits = {}, {}
+            for gs, pay, bl in per:
+                pay, bl = pay.cpu().numpy(), bl.cpu().numpy()
+                for j, g in enumerate(gs):
+                    pieces[g] = pay[j].tobytes()
+                    bits[g] = int(bl[j]) & 0xFFFFFFFF
+            if os.environ.get("P64_FEED_SYNC", "0") != "0":  # (diagnostic)
+                print(f"kept step {t}: " + " ".join(f"{g}:{bits[g]}" for g in sorted(bits)),
                       file=sys.stderr, flush=True)
-        for per in self.kept:
-            pieces = {g: per[g][0].cpu().numpy().tobytes() for g in writers}
-            bits = {g: int(per[g][1].item()) & 0xFFFFFFFF for g in writers}
             stitch_pieces(writers, pieces, bits)
         out = {}
         for g, wr in writers.items():
@@ -911,7 +973,11 @@ def main(argv=None):
         # stores exactly the blocks its nonzero-block mask names
         # (include/p64gpu.h), so every other block must still hold it.
         vt, last = args.warmup, args.warmup + args.steps
-        ncoef = nslots if keep else 3
+        # --feed root --gather coded: the unchecked steps alternate between two
+        # output sets (0 and 3), so step t's coder (on the feed's side stream)
+        # reads a set step t+1's encode does not write
+        alt = root and args.gather == "coded"
+        ncoef = nslots if keep else (4 if alt else 3)
         coef_all = torch.full((ncoef, S, nmb, 6, 64), LEVEL_SENTINEL, dtype=torch.int16, device="cuda")
         nz_all = torch.empty((ncoef, S, nmb), dtype=torch.uint8, device="cuda")
         mb_all = torch.empty((ncoef, S, nmb, 4), dtype=torch.int8, device="cuda")
@@ -920,7 +986,7 @@ def main(argv=None):
         vb_root = None  # (--feed root codes with the coder's own counts: with_vlc measures it faster)
 
         def out_of(t):
-            i = slot(t) if keep else (1 if t == vt else (2 if t == last else 0))
+            i = slot(t) if keep else (1 if t == vt else (2 if t == last else (3 * (t % 2) if alt else 0)))
             return p64_amd.FrameBatchOut(coef=coef_all[i], mb=mb_all[i], me=me, nz=nz_all[i], vlc_bits=vb_root)
         # the checked pictures' buffers were written by no earlier step
         fresh = {t: (not keep) or (1 + args.warmup + args.steps <= nslots) for t in (vt, last)}
@@ -954,6 +1020,8 @@ def main(argv=None):
         def step(t, vlc_bits=None):
             if root:
                 pre(t)
+            if feed is not None:
+                feed.before_encode(t)
             launch(t, vlc_bits)
             if root:
                 post(t)
@@ -1012,18 +1080,18 @@ def main(argv=None):
                                              search_limit=args.search_limit, out=o)
                 vlc, vbits = p64s.prepare_vlc(o.mb, o.coef, feed.gq, feed.trs[t % 32], width=w, height=h,
                                               buffers=feed.bufs[t % 2], blk_bits=o.vlc_bits,
-                                              seq_bits=feed.seq_bits, max_bits=feed.mx[t % 2])
+                                              seq_bits=feed.seq_bits, max_bits=feed.mx[t % 2],
+                                              stream=feed.side if feed.fork else None)
                 prep[t] = (enc, vlc, vbits)
 
             def timed_launch(t):
+                feed.before_encode(t)
                 prep[t][0]()
 
             def timed_post(t):
-                torch.cuda.current_stream().wait_stream(feed.side)
-                prep[t][1]()
-                feed.bits[t % 2] = prep[t][2]
-                feed.code_host(t)
+                feed.code(t, None, vlc=(prep[t][1], prep[t][2]))
         if feed_graphs:
+            feed.fork = False  # (the coder inside each step's graph, on the encode stream)
             # --feed root, coded: each timed step's device work (encode + coder
             # + the phase bookkeeping) captured as its own HIP graph before the
             # region and replayed in the step, so the host issues four calls a
@@ -1070,28 +1138,51 @@ def main(argv=None):
                     print(f"feed step {t}: gather ok", file=sys.stderr, flush=True)
             timed_post = None
         if feed is not None:
-            # the scatter of step t+1's pictures is issued during step t on the
-            # feed's side stream (slots differ between consecutive steps); the
-            # first timed step scatters in place, so the region holds exactly
-            # K scatters.  (Not a stream of its own: a fourth stream shares a
-            # hardware queue with the encode stream -- GPU_MAX_HW_QUEUES = 4 --
-            # and serialised the gathers behind the encodes: 579 against 298
-            # us per step.)  Two events, created once, alternate.
-            pf_ev = [torch.cuda.Event(), torch.cuda.Event()]
+            # the scatters of steps t+1 and t+2 are issued during step t on the
+            # feed's side stream (at most 3 slots live, all distinct), so a step's
+            # pictures were queued two steps ahead -- behind the coder of step
+            # t-1, which shares the GPU with step t's encode and finishes late
+            # (one step ahead, the encode of t+1 waited for that coder and the
+            # scatter behind it: 68 us idle per step, profiles/r06m_fed_trace.txt);
+            # the first timed step scatters in place, so the region holds
+            # exactly K scatters.  (Not a stream of its own: a fourth stream
+            # shares a hardware queue with the encode stream -- GPU_MAX_HW_QUEUES
+            # = 4 -- and serialised the gathers behind the encodes: 579 against
+            # 298 us per step.)  Three events, created once, rotate.
+            assert nslots >= 3
+            pf_ev = [torch.cuda.Event() for _ in range(3)]
             pf_done = set()
             t_last = args.warmup + args.steps
+            ahead = int(os.environ.get("P64_FEED_AHEAD", "2"))  # (1: round 6's first form)
 
             def timed_pre(t):
                 if t not in pf_done:
                     pre(t)
                 else:
-                    torch.cuda.current_stream().wait_event(pf_ev[t % 2])
+                    torch.cuda.current_stream().wait_event(pf_ev[t % 3])
                     pf_done.discard(t)
-                if t + 1 <= t_last:
-                    with torch.cuda.stream(feed.side):
-                        pre(t + 1)
-                        pf_ev[(t + 1) % 2].record(feed.side)
-                    pf_done.add(t + 1)
+                for u in range(t + 1, min(t + ahead, t_last) + 1):
+                    if u not in pf_done:
+                        with torch.cuda.stream(feed.side):
+                            pre(u)
+                            pf_ev[u % 3].record(feed.side)
+                        pf_done.add(u)
+        feed_host = None
+        if feed is not None:  # host seconds spent issuing each part of the fed step (incl. its waits)
+            feed_host = {"pre": 0.0, "launch": 0.0, "post": 0.0}
+
+            def host_timed(fn, key):
+                if fn is None:
+                    return None
+
+                def f(t):
+                    a = time.perf_counter()
+                    fn(t)
+                    feed_host[key] += time.perf_counter() - a
+                return f
+            timed_pre = host_timed(timed_pre, "pre")
+            timed_launch = host_timed(timed_launch, "launch")
+            timed_post = host_timed(timed_post, "post")
         # the checked sequences (VERIFY_SEQS: one of each synth seed class) after
         # the warmup, checked against the oracle after the timed region
         seqs = [i for i in VERIFY_SEQS if i < S]
@@ -1230,6 +1321,10 @@ def main(argv=None):
             **({"other_content": other} if other else {}),
             "verified_vs_oracle": verified,
         }
+        if feed_host is not None:
+            result["feed_host_us_per_step"] = {k: round(v / args.steps * 1e6, 1) for k, v in feed_host.items()}
+            result["feed_host_note"] = ("host time per timed step in each part of the fed step (Python wrappers, "
+                                        "launches, event waits and, at N>1, the gather's size read-back)")
         if extra:
             result["configs"] = extra
 
