@@ -156,7 +156,15 @@ int p64gpu_motion_estimation(int width, int height, int nframes,
  * the encode reads them.  The reference's own order: MotionEstimation() for
  * the picture first (p64.c:652, me.c:340), then the MDU loop reads MeVAR,
  * MeVAROR, MeX/MeY... (p64.c:734-756). */
-enum { P64GPU_FLAG_ME_GIVEN = 1 };
+/* P64GPU_FLAG_SEARCH_ONLY -- inter pictures only, with args->me: the search
+ * alone (the first half of the encode), each record's mx, my, sad and sad0
+ * written (its var / varor / mwor are not: the ME_GIVEN encode that follows
+ * computes them itself); nothing else is read or written.  The two halves
+ * in order -- SEARCH_ONLY, then ME_GIVEN over the same arguments -- are the
+ * encode (the same outputs), with a point between them where the caller can
+ * place stream work (bench.py's entropy coder of the previous picture runs
+ * beside the second half).  Added in ABI version 3 (no layout change). */
+enum { P64GPU_FLAG_ME_GIVEN = 1, P64GPU_FLAG_SEARCH_ONLY = 2 };
 typedef struct {
   int32_t width, height;  /* picture size, multiples of 16, 32..4096         */
   int32_t nframes;        /* independent pictures in this launch (>= 1)      */
@@ -165,7 +173,7 @@ typedef struct {
   int32_t quant;          /* GQuant 1..31 (UseQuant without -r)              */
   int32_t me_mode;        /* P64GPU_ME_TSS | P64GPU_ME_FULL                  */
   int32_t search_limit;   /* FULL: 1..31 (SearchLimit, me.c:62, -i flag)     */
-  int32_t flags;          /* 0 or P64GPU_FLAG_ME_GIVEN                       */
+  int32_t flags;          /* 0, P64GPU_FLAG_ME_GIVEN or _SEARCH_ONLY         */
   int64_t frame_stride;   /* bytes between pictures in cur/ref/recon        */
   const uint8_t *cur;     /* [nframes] current pictures                       */
   const uint8_t *ref;     /* [nframes] previous reconstructions (CFS);

@@ -81,6 +81,7 @@ class EncodeArgs(ctypes.Structure):
 
 # numpy views of the record arrays (field order matches include/p64gpu.h)
 P64GPU_FLAG_ME_GIVEN = 1  # include/p64gpu.h
+P64GPU_FLAG_SEARCH_ONLY = 2
 ME_DTYPE = np.dtype([(n, "<i4") for n in ("mx", "my", "sad", "sad0", "var", "varor", "mwor")])
 MB_DTYPE = np.dtype([(n, "i1") for n in ("mtype", "cbp", "mvx", "mvy")])
 
@@ -380,11 +381,13 @@ class FrameBatchOut:
 def encode_frames(cur, ref, recon, last_intra, *, width: int, height: int, intra: bool,
                   quant: int = 8, me_mode: int = ME_TSS, search_limit: int = 15,
                   quant_mb=None, mtype_override=None, out: FrameBatchOut | None = None,
-                  want_me: bool = True, me_given: bool = False) -> FrameBatchOut:
+                  want_me: bool = True, me_given: bool = False, search_only: bool = False) -> FrameBatchOut:
     """One picture of each of `nframes` independent sequences (p64.c:622-1013).
     me_given: out.me already holds the batch's ME records (MotionEstimation
     over the same pictures, search mode and limit): the search is not run
-    again (P64GPU_FLAG_ME_GIVEN)."""
+    again (P64GPU_FLAG_ME_GIVEN).  search_only: the search alone into out.me
+    (P64GPU_FLAG_SEARCH_ONLY; then the same call with me_given finishes the
+    encode)."""
     torch = _torch()
     stride = picture_bytes(width, height)
     nframes = cur.numel() // stride
@@ -436,11 +439,13 @@ def encode_frames(cur, ref, recon, last_intra, *, width: int, height: int, intra
     me = out.me
     if me_given and (intra or me is None):
         raise P64GpuError("me_given needs an inter batch and out.me holding its records")
+    if search_only and (intra or me is None or me_given):
+        raise P64GpuError("search_only needs an inter batch with out.me (and not me_given)")
     if me is None and not intra:
         me = torch.empty((nframes, nmb, 7), dtype=torch.int32, device=dev)
     a = EncodeArgs(width=width, height=height, nframes=nframes, intra=int(bool(intra)),
                    quant=quant, me_mode=me_mode, search_limit=search_limit,
-                   flags=P64GPU_FLAG_ME_GIVEN if me_given else 0,
+                   flags=(P64GPU_FLAG_ME_GIVEN if me_given else 0) | (P64GPU_FLAG_SEARCH_ONLY if search_only else 0),
                    frame_stride=stride, cur=cur.data_ptr(),
                    ref=(ref.data_ptr() if ref is not None else None), recon=recon.data_ptr(),
                    last_intra=last_intra.data_ptr(),
@@ -455,7 +460,8 @@ def encode_frames(cur, ref, recon, last_intra, *, width: int, height: int, intra
 
 
 def prepare_encode(cur, ref, recon, last_intra, *, width: int, height: int, intra: bool, quant: int = 8,
-                   me_mode: int = ME_TSS, search_limit: int = 15, out: FrameBatchOut, stream=None):
+                   me_mode: int = ME_TSS, search_limit: int = 15, out: FrameBatchOut, stream=None,
+                   me_given: bool = False, search_only: bool = False):
     """encode_frames' launch with its arguments checked and packed once: the
     returned function issues it again with the same buffers (no per-call
     Python checks -- for host loops that relaunch the same step shapes, e.g.
@@ -474,8 +480,11 @@ def prepare_encode(cur, ref, recon, last_intra, *, width: int, height: int, intr
         raise P64GpuError("prepare_encode: buffer sizes do not match nframes x picture geometry")
     if out.me is None and not intra:
         raise P64GpuError("prepare_encode: inter batches need out.me")
+    if (me_given or search_only) and (intra or (me_given and search_only)):
+        raise P64GpuError("prepare_encode: me_given / search_only: one of them, inter batches only")
+    flags = (P64GPU_FLAG_ME_GIVEN if me_given else 0) | (P64GPU_FLAG_SEARCH_ONLY if search_only else 0)
     a = EncodeArgs(width=width, height=height, nframes=nframes, intra=int(bool(intra)), quant=quant,
-                   me_mode=me_mode, search_limit=search_limit, flags=0, frame_stride=stride,
+                   me_mode=me_mode, search_limit=search_limit, flags=flags, frame_stride=stride,
                    cur=cur.data_ptr(), ref=(ref.data_ptr() if ref is not None else None), recon=recon.data_ptr(),
                    last_intra=last_intra.data_ptr(), quant_mb=None, mtype_override=None,
                    coef=out.coef.data_ptr(), mb=out.mb.data_ptr(),

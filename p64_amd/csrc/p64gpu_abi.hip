@@ -199,7 +199,8 @@ int encode_launch(const p64gpu_encode_args *a, const int32_t *mb_list, int count
     return fail(P64GPU_E_INVALID, "me mode %d", a->me_mode);
   if (a->search_limit < 1 || a->search_limit > 31)
     return fail(P64GPU_E_INVALID, "search_limit %d not in 1..31", a->search_limit);
-  if (a->flags & ~P64GPU_FLAG_ME_GIVEN) return fail(P64GPU_E_INVALID, "flags 0x%x: unknown bits", a->flags);
+  if (a->flags & ~(P64GPU_FLAG_ME_GIVEN | P64GPU_FLAG_SEARCH_ONLY))
+    return fail(P64GPU_E_INVALID, "flags 0x%x: unknown bits", a->flags);
   if (a->vlc_bits && (mb_list || !aligned(a->vlc_bits, 16)))
     return fail(P64GPU_E_INVALID, "vlc_bits: 16-byte aligned, and not with an MB list");
   const uint32_t *vlc_len = nullptr;  // the count's code lengths, device copy (p64vlc.hip)
@@ -210,6 +211,14 @@ int encode_launch(const p64gpu_encode_args *a, const int32_t *mb_list, int count
     return fail(P64GPU_E_INVALID, "P64GPU_FLAG_ME_GIVEN needs an inter picture batch with args->me");
   hipStream_t st = (hipStream_t)stream;
   const int mode = a->intra ? 0 : (a->me_mode == P64GPU_ME_FULL ? 2 : 1);
+  if (a->flags & P64GPU_FLAG_SEARCH_ONLY) {  // the first half: the search into args->me
+    if (me_given || a->intra || !a->me || mb_list)
+      return fail(P64GPU_E_INVALID, "P64GPU_FLAG_SEARCH_ONLY needs an inter picture batch with args->me "
+                                    "(and not ME_GIVEN)");
+    HIP_TRY(p64k::motion(mode, a->width, a->height, a->nframes, a->frame_stride, a->ref, a->cur,
+                         a->search_limit, a->me, /*stats: the ME_GIVEN half's*/ false, st));
+    return P64GPU_OK;
+  }
   if (!mb_list && (!fused_forced() || me_given)) {
     const int nmb = (a->width / 16) * (a->height / 16);
     // inter: ME for the whole batch into the caller's records or the scratch

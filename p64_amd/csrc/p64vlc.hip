@@ -396,9 +396,24 @@ __global__ __launch_bounds__(64 * VLC_WAVES) void k_vlc_blk(VlcArgs a) {
   const int g = j / 33, m = j - g * 33, k = raster(a.format, g, m);
   const bool act = lane < 6 * VLC_MBS && mb0 + l / 6 < a.nmb;
   const size_t base = (size_t)fi * a.nmb;
-  // every lane's block is loaded, coded or not: the loads need not wait for the record
+  const p64_mb_rec r = a.mb[base + k];
+  const p64_mb_rec rp = a.mb[base + (m % 11 ? k - 1 : k)];  // MVD predictor (same GOB row)
+  const int mq = a.mquant ? (int)a.mquant[base + k] : 0;
+  const int mt = r.mtype;
+  const bool valid = mt >= 0 && mt <= 9;
+  const bool cbpt = valid && mt_cbp(mt);
+  const int cbp = cbpt ? r.cbp : 0x3f;
+  const bool coded = act && valid && mt_tc(mt) && ((cbp >> (5 - b)) & 1);
+  // the levels of the coded blocks only (an inter picture's uncoded blocks
+  // hold nothing the coder reads; -DVLC_LOAD_ALL: every lane's block, not
+  // waiting for the record -- the round-5/6 form)
   const uint32_t co = (uint32_t)(((base + k) * 6 + b) * 128);
   uint32_t lv[32];
+#pragma unroll
+  for (int i = 0; i < 32; i++) lv[i] = 0u;
+#ifndef VLC_LOAD_ALL
+  if (coded)
+#endif
   {
     const __amdgpu_buffer_rsrc_t cr = __builtin_amdgcn_make_buffer_rsrc(
         (void *)a.coef, (short)0, (int)((size_t)a.nframes * a.nmb * 768), 0x00020000);  // < 2 GiB (host split)
@@ -411,14 +426,6 @@ __global__ __launch_bounds__(64 * VLC_WAVES) void k_vlc_blk(VlcArgs a) {
       lv[4 * i + 3] = v[3];
     }
   }
-  const p64_mb_rec r = a.mb[base + k];
-  const p64_mb_rec rp = a.mb[base + (m % 11 ? k - 1 : k)];  // MVD predictor (same GOB row)
-  const int mq = a.mquant ? (int)a.mquant[base + k] : 0;
-  const int mt = r.mtype;
-  const bool valid = mt >= 0 && mt <= 9;
-  const bool cbpt = valid && mt_cbp(mt);
-  const int cbp = cbpt ? r.cbp : 0x3f;
-  const bool coded = act && valid && mt_tc(mt) && ((cbp >> (5 - b)) & 1);
   // the block's nonzero positions (the DC of an intra block is coded apart),
   // its levels as int8 in LDS for the indexed reads of the code loops, and
   // whether one of them does not fit (+128 per int16 half: a byte or not)
@@ -537,11 +544,13 @@ __global__ __launch_bounds__(64 * VLC_WAVES) void k_vlc_blk(VlcArgs a) {
   if (!big) {
     reinterpret_cast<uint4 *>(wb)[lane] = make_uint4(0, 0, 0, 0);
     wave_lds_sync();
+#ifndef VLC_NOEMIT  // (timing experiment only: no codes)
     if (tot > 0) {
       LdsBitWriter bw;
       bw.w0 = 0;
       emit(bw, wb, 0);
     }
+#endif
   }
   // the start (wave 0): the phase for the first workgroup, else the end of the
   // previous one -- 64 workgroups at a time, lane i reading the one i places
@@ -551,6 +560,10 @@ __global__ __launch_bounds__(64 * VLC_WAVES) void k_vlc_blk(VlcArgs a) {
     bool bad_all = wbad;
     if (G == 0) {
       first = a.seq_bits ? (a.seq_bits[fi] & 7) : (a.phase ? a.phase[fi] : 0);
+#ifdef VLC_NOSYNC  // (timing experiment only: wrong bits) no look-back
+    } else if (true) {
+      first = (int64_t)G * 12000;
+#endif
     } else {
       for (int v = G - 1;;) {
         const uint64_t inc = __ballot((s >> 62) == 2), zero = __ballot(s == 0);
@@ -651,7 +664,9 @@ __global__ __launch_bounds__(64 * VLC_WAVES) void k_vlc_blk(VlcArgs a) {
   // workgroup's
   if (wt == 0 || w0 == wl) {  // (one word: the previous workgroup's tail and ours)
     uint32_t v = wt > 0 ? firstv : 0u;
+#ifndef VLC_NOSYNC
     if (sh_first) v |= (uint32_t)st_wait(stw + 2 * (G - 1) + 1);
+#endif
     if (sh_last) {
       if (lane == 0) st_store(stw + 2 * G + 1, (1ull << 63) | v);
     } else if ((wt > 0 || sh_first) && lane == 0 && VLC_OK(w0 >= 0 && w0 < a.out_words, 3)) {
@@ -660,7 +675,11 @@ __global__ __launch_bounds__(64 * VLC_WAVES) void k_vlc_blk(VlcArgs a) {
   } else {
     if (sh_last && lane == 0) st_store(stw + 2 * G + 1, (1ull << 63) | lastv);
     if (sh_first) {
+#ifdef VLC_NOSYNC
+      const uint32_t pv = 0;
+#else
       const uint32_t pv = (uint32_t)st_wait(stw + 2 * (G - 1) + 1);
+#endif
       if (lane == 0 && VLC_OK(w0 >= 0 && w0 < a.out_words, 3)) out[w0] = firstv | pv;
     }
   }

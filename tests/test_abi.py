@@ -88,9 +88,17 @@ def test_invalid_arguments_rejected_without_device(p64):
     # flags: unknown bits, and P64GPU_FLAG_ME_GIVEN without an inter batch with records
     a = p64.EncodeArgs(width=176, height=144, nframes=1, quant=8, frame_stride=38016, me_mode=1,
                        search_limit=31, cur=16, ref=16, recon=16, last_intra=16, coef=16, mb=16,
-                       flags=2)
+                       flags=4)
     assert L.p64gpu_encode_frames(ctypes.byref(a), None) == -1
     assert b"flags" in L.p64gpu_last_error()
+    a.flags = p64.P64GPU_FLAG_SEARCH_ONLY  # args.me is NULL
+    assert L.p64gpu_encode_frames(ctypes.byref(a), None) == -1
+    assert b"SEARCH_ONLY" in L.p64gpu_last_error()
+    a.flags = p64.P64GPU_FLAG_SEARCH_ONLY | p64.P64GPU_FLAG_ME_GIVEN
+    a.me = 16
+    assert L.p64gpu_encode_frames(ctypes.byref(a), None) == -1
+    assert b"SEARCH_ONLY" in L.p64gpu_last_error()
+    a.me = None
     a.flags = p64.P64GPU_FLAG_ME_GIVEN  # args.me is NULL
     assert L.p64gpu_encode_frames(ctypes.byref(a), None) == -1
     assert b"ME_GIVEN" in L.p64gpu_last_error()

@@ -380,6 +380,43 @@ def test_encode_with_given_me_records(p64, torch_dev, mode, sl):
                 np.testing.assert_array_equal(x, y, err_msg=f"picture {t}")
 
 
+@pytest.mark.parametrize("mode,sl", [(1, 31), (0, 15)])
+def test_encode_in_two_halves(p64, torch_dev, mode, sl):
+    """P64GPU_FLAG_SEARCH_ONLY then P64GPU_FLAG_ME_GIVEN over the same
+    arguments (prepare_encode's launches, as bench.py's with_vlc issues them)
+    is the encode: levels, records, ME vectors and SADs, reconstruction, over
+    a closed loop of 4 pictures."""
+    torch = torch_dev
+    w, h, S, T = 352, 288, 3, 4
+    nmb, pic = (w // 16) * (h // 16), w * h * 3 // 2
+    frames = [dev(torch, np.stack([p64.synth_frame(31 + s, t, w, h) for s in range(S)])).reshape(-1)
+              for t in range(T)]
+
+    def run(halves):
+        li = torch.zeros(S * nmb, dtype=torch.uint8, device="cuda")
+        bufs = [torch.zeros(S * pic, dtype=torch.uint8, device="cuda") for _ in range(2)]
+        got = []
+        for t in range(T):
+            ref, rec = bufs[t % 2], bufs[(t + 1) % 2]
+            o = p64.FrameBatchOut(coef=torch.zeros((S, nmb, 6, 64), dtype=torch.int16, device="cuda"),
+                                  mb=torch.empty((S, nmb, 4), dtype=torch.int8, device="cuda"),
+                                  me=torch.zeros((S, nmb, 7), dtype=torch.int32, device="cuda"))
+            kw = dict(width=w, height=h, intra=(t == 0), quant=8, me_mode=mode, search_limit=sl, out=o)
+            if halves and t > 0:
+                p64.prepare_encode(frames[t], ref, rec, li, search_only=True, **kw)()
+                p64.prepare_encode(frames[t], ref, rec, li, me_given=True, **kw)()
+            else:
+                p64.encode_frames(frames[t], ref, rec, li, **kw)
+            torch.cuda.synchronize()
+            got.append((host(o.coef), host(o.mb), host(o.me) if t > 0 else None, host(rec)))
+        return got
+
+    for t, (a, b) in enumerate(zip(run(False), run(True))):
+        for x, y in zip(a, b):
+            if x is not None:
+                np.testing.assert_array_equal(x, y, err_msg=f"picture {t}")
+
+
 def _raw_encode(p64, torch, cur, ref, recon, li, coef, mb, *, w, h, stream, me=None):
     """p64gpu_encode_frames straight through the C ABI (me = NULL unless given)."""
     import ctypes
