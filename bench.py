@@ -93,7 +93,7 @@ INTRA_BYTES_PER_MB = 384 + 768 + 384 + 4 + 1
 # per-kernel means over the timed region of the driver's command (rocprofv3
 # --kernel-trace of `bench.py --steps 20 --warmup 5 --no-cpu`, reduced by
 # tools/timed_region.py --json; the spin-up's replays are outside the region)
-PROFILE_TIMED = "profiles/r05_timed_region.json"  # {workload key: {kernel: mean us}}
+PROFILE_TIMED = "profiles/r06_timed_region.json"  # {workload key: {kernel: mean us}}
 # executed v_sad_u8 work of k_motion per launch (tools/sad_count.py side build)
 PROFILE_SAD = "profiles/sad_executed.json"
 VALU_BUSY_NOTE = ("derived, not a busy counter: SQ_INSTS_VALU (PMC) x the kernel's mean VALU issue cost "
