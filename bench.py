@@ -1786,9 +1786,9 @@ def run_decode(args, torch, dist, np, p64_amd, world, enc, S, nmb, pic):
         lv, n, ix = p64_amd.pack_levels_device(enc["coef"][t], enc["mb"][t], mask, w, h)
         pk[t] = (lv if n else torch.zeros((1, 64), dtype=torch.int16, device="cuda"), n, ix)
     nbytes = []
-    ngr = (6 * nmb + 63) // 64
+    ngr = (S * 6 * nmb + 63) // 64  # the index: 16 bytes per 64 blocks of the batch
     for t in range(first, last + 1):
-        nbytes.append(decode_bytes(torch, enc["mb"][t], S * nmb) + 16 * S * ngr)
+        nbytes.append(decode_bytes(torch, enc["mb"][t], S * nmb) + 16 * ngr)
 
     def measure(packed):
         dec = [torch.zeros(S * pic, dtype=torch.uint8, device="cuda") for _ in range(2)]

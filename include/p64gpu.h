@@ -251,11 +251,12 @@ int p64gpu_decode_recon(int width, int height, int nframes, int64_t frame_stride
  * blocks' 64 zigzag levels each (nlevels blocks: MB present in coded_mask,
  * MTYPE with coefficients, its CBP bit set -- what the stream carries),
  * contiguous in (picture, MB, block) raster order; `index` holds, for each
- * group of 64 consecutive blocks of a picture (group j of picture f covers
- * its blocks 64j .. 64j+63, block = 6*mb + b; ceil(6*nmb/64) groups per
- * picture), four uint32: the index in `levels` of the group's first
- * transmitted block, 0, and the group's 64-bit transmitted-block mask (bit i
- * = block 64j + i), low word first.  p64s_pack_levels (p64stream.h) builds
+ * group of 64 consecutive blocks of the batch (the pictures' blocks back to
+ * back, block = 6*(nmb*f + mb) + b; group j covers blocks 64j .. 64j+63, a
+ * group may straddle two pictures; ceil(nframes*6*nmb/64) groups), four
+ * uint32: the index in `levels` of the group's first transmitted block, 0,
+ * and the group's 64-bit transmitted-block mask (bit i = block 64j + i), low
+ * word first.  p64s_pack_levels (p64stream.h) builds
  * both from p64s_read_picture's output.  The kernel loads a group's levels
  * from its index entry without waiting for the records.
  * levels and index 16-byte aligned; nlevels < 2^24 per call. */

@@ -126,7 +126,8 @@ int p64s_read_picture(p64s_reader *r, p64s_picture_info *info, p64_mb_rec *mb,
  * nframes pictures of p64s_read_picture output (mb, coded, coef as that
  * call writes them, pictures consecutive): the transmitted blocks' levels
  * into `levels` (room for up to nframes*nmb*6 blocks), contiguous in raster
- * order, and the per-group index (nframes * ceil(6*nmb/64) * 4 uint32).
+ * order, and the per-group index (ceil(nframes*6*nmb/64) * 4 uint32: groups
+ * of 64 consecutive blocks of the batch, pictures back to back).
  * Returns the number of blocks written (>= 0) or a negative status. */
 int64_t p64s_pack_levels(int format, int nframes, const p64_mb_rec *mb, const uint8_t *coded,
                          const int16_t *coef, int16_t *levels, uint32_t *index);

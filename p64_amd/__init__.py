@@ -534,9 +534,9 @@ def decode_recon_packed(ref, recon, levels, nlevels: int, index, mb, quant_mb, c
     nframes = recon.numel() // stride
     nmb = (width // 16) * (height // 16)
     nmb_all = nframes * nmb
-    ngr = (6 * nmb + 63) // 64
+    ngr = (nframes * 6 * nmb + 63) // 64  # groups of 64 blocks over the batch
     if nframes < 1 or ref.numel() < nframes * stride or levels.numel() < nlevels * 64 or \
-            index.numel() < nframes * ngr * 4 or mb.numel() < nmb_all * 4 or quant_mb.numel() < nmb_all or \
+            index.numel() < ngr * 4 or mb.numel() < nmb_all * 4 or quant_mb.numel() < nmb_all or \
             coded_mask.numel() < nmb_all:
         raise P64GpuError("buffer sizes do not match nframes x picture geometry")
     _check(lib().p64gpu_decode_recon_packed(width, height, nframes, stride, ref.data_ptr(), recon.data_ptr(),
@@ -560,17 +560,17 @@ def pack_levels_device(coef, mb, coded_mask, width: int, height: int):
     hc = torch.tensor(CBP_MTYPE, device=mb.device)[mt]
     cbp = torch.where(hc == 1, mbr[..., 1].long() & 63, torch.full_like(mt, 63))
     bits = (cbp[..., None] >> (5 - torch.arange(6, device=mb.device))) & 1  # [nf, nmb, 6]
-    tx = (bits * tc[..., None] * (coded_mask.reshape(nf, nmb)[..., None] != 0)).reshape(nf, 6 * nmb)
-    ngr = (6 * nmb + 63) // 64
-    pad = torch.zeros((nf, ngr * 64), dtype=torch.long, device=mb.device)
-    pad[:, :6 * nmb] = tx
-    g = pad.reshape(nf, ngr, 64)
-    cnt = g.sum(dim=2).reshape(-1)
+    tx = (bits * tc[..., None] * (coded_mask.reshape(nf, nmb)[..., None] != 0)).reshape(-1)
+    ngr = (nf * 6 * nmb + 63) // 64  # groups of 64 consecutive blocks of the batch
+    pad = torch.zeros(ngr * 64, dtype=torch.long, device=mb.device)
+    pad[:tx.numel()] = tx
+    g = pad.reshape(ngr, 64)
+    cnt = g.sum(dim=1)
     start = torch.cumsum(cnt, 0) - cnt
     w = (g.reshape(-1, 64) << torch.arange(64, device=mb.device)).sum(dim=1)  # (int64 wraps: bit 63 fine)
     index = torch.stack([start, torch.zeros_like(start), w & 0xFFFFFFFF, (w >> 32) & 0xFFFFFFFF], dim=1)
     index = index.to(torch.int64).to(torch.int32)
-    sel = tx.reshape(-1).nonzero().squeeze(1)
+    sel = tx.nonzero().squeeze(1)
     levels = coef.reshape(-1, 64).index_select(0, sel).contiguous()
     return levels, int(sel.numel()), index.contiguous()
 

@@ -1147,25 +1147,29 @@ __global__ __launch_bounds__(64) OCC4 void k_recon_mbg(int w, int h, int64_t str
 
 // Decoder reconstruction from PACKED levels (p64gpu_decode_recon_packed, ABI
 // v3): the transmitted blocks' levels contiguous in raster order, and per
-// group of 64 blocks of a picture (a wave) its first transmitted block's index
-// and its transmitted-block mask, {start, 0, mask lo, mask hi}
+// group of 64 consecutive blocks of the batch (a wave, as k_recon_mbg's: an
+// MB and a group may straddle two pictures) its first transmitted block's
+// index and its transmitted-block mask, {start, 0, mask lo, mask hi}
 // (p64s_pack_levels).  The wave reads its group's entry with one scalar load
 // while its records are in flight and issues its level loads at once from
 // start + (the lane's rank among the set bits) -- the levels no longer wait
 // for the record (in k_recon_mbg a lane learns from its record whether, and
-// so where, to load); only the prediction source does.  Waves map to
-// pictures: nwpp = ceil(6 nmb / 64) per picture, the last one partly idle.
+// so where, to load); only the prediction source does.  (Round 6's first
+// form gave each picture ceil(6 nmb / 64) groups of its own: 2.4% more waves
+// at CIF, the last of each picture 8/64 full -- 36.5 against 35.2 us.)
 typedef unsigned su4 __attribute__((ext_vector_type(4)));
 __global__ __launch_bounds__(64) OCC4 void k_recon_pk(int w, int h, int64_t stride, const uint8_t *refp,
                                                           uint8_t *recp, const int16_t *levels, uint32_t nlev,
                                                           const uint32_t *index, const p64_mb_rec *mbr,
                                                           const uint8_t *quant_mb, const uint8_t *coded_mask,
-                                                          BlkDiv kd, unsigned nmbs, unsigned nwpp) {
+                                                          BlkDiv kd, unsigned nmbs) {
   const int lane = threadIdx.x & 63;
-  const unsigned wv = xcd_remap(blockIdx.x, gridDim.x);  // (grid = nframes x nwpp)
+  const unsigned nblk = 6u * nmbs;
+  const unsigned wv = xcd_remap(blockIdx.x, gridDim.x);  // the wave's group
+  const unsigned g0 = wv * 64u;                           // its first block
+  if (g0 >= nblk) return;  // whole wave
   PRIO_HIGH();
   const int nmb = (w >> 4) * (h >> 4), nfr = (int)mdiv(nmbs, kd.mn, kd.sn);
-  const unsigned fi = wv / nwpp, j = wv - fi * nwpp;  // (scalar, once per wave)
   RecBufs B;
   B.ref = __builtin_amdgcn_make_buffer_rsrc((void *)refp, (short)0, (int)(nfr * stride), BUF_RSRC_W3);
   B.coef = __builtin_amdgcn_make_buffer_rsrc((void *)levels, (short)0, (int)(nlev * 128u), BUF_RSRC_W3);
@@ -1174,9 +1178,8 @@ __global__ __launch_bounds__(64) OCC4 void k_recon_pk(int w, int h, int64_t stri
   B.mask = __builtin_amdgcn_make_buffer_rsrc((void *)coded_mask, (short)0, nfr * nmb, BUF_RSRC_W3);
   const __amdgpu_buffer_rsrc_t rec =
       __builtin_amdgcn_make_buffer_rsrc((void *)recp, (short)0, (int)(nfr * stride), BUF_RSRC_W3);
-  const unsigned nb = 6u * (unsigned)nmb, bl = 64u * j + (unsigned)lane;  // block within the picture
-  const bool valid = bl < nb;
-  const unsigned g = fi * nb + min(bl, nb - 1);
+  const bool valid = g0 + (unsigned)lane < nblk;
+  const unsigned g = min(g0 + (unsigned)lane, nblk - 1);
   const unsigned gmb = __umulhi(g, 0xAAAAAAABu) >> 2;  // g / 6
   RecStageA A;
   A.p = blk_pos_mb(gmb, (int)(g - 6u * gmb), w, h, kd);
@@ -1201,6 +1204,10 @@ __global__ __launch_bounds__(64) OCC4 void k_recon_pk(int w, int h, int64_t stri
     lq[k][2] = v[2];
     lq[k][3] = v[3];
   }
+  // (the compiler otherwise hoists the coded-flag test of rec_stage_b above
+  // these loads, with an s_waitcnt vmcnt(0) for the record: the levels would
+  // wait for it again)
+  __builtin_amdgcn_sched_barrier(0);
   RecStageB S = rec_stage_b<false>(B, w, h, stride, A);
 #pragma unroll
   for (int k = 0; k < 8; k++)
@@ -1643,9 +1650,9 @@ hipError_t recon_mbg(int w, int h, int nframes, int64_t stride, const uint8_t *r
 hipError_t recon_pk(int w, int h, int nframes, int64_t stride, const uint8_t *ref, uint8_t *recon,
                     const int16_t *levels, uint32_t nlev, const uint32_t *index, const p64_mb_rec *mb,
                     const uint8_t *quant_mb, const uint8_t *coded_mask, hipStream_t st) {
-  const unsigned nmb = (unsigned)((w / 16) * (h / 16)), nwpp = (6u * nmb + 63u) / 64u;
-  hipLaunchKernelGGL(k_recon_pk, dim3((unsigned)nframes * nwpp), dim3(64), 0, st, w, h, stride, ref, recon, levels,
-                     nlev, index, mb, quant_mb, coded_mask, blk_div(w, h), (unsigned)nframes * nmb, nwpp);
+  const unsigned nm = (unsigned)((int64_t)nframes * (w / 16) * (h / 16));
+  hipLaunchKernelGGL(k_recon_pk, dim3((6u * nm + 63u) / 64u), dim3(64), 0, st, w, h, stride, ref, recon, levels,
+                     nlev, index, mb, quant_mb, coded_mask, blk_div(w, h), nm);
   return hipGetLastError();
 }
 

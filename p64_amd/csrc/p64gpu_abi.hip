@@ -418,13 +418,20 @@ int p64gpu_decode_recon_packed(int w, int h, int nframes, int64_t stride, const 
     return fail(P64GPU_E_INVALID, "nlevels %lld: 0 .. 2^24-1 blocks per call", (long long)nlevels);
   if (!aligned(ref, 16) || !aligned(recon, 16) || !aligned(levels, 16) || !aligned(index, 16) || !aligned(mb, 4))
     return fail(P64GPU_E_INVALID, "ref/recon/levels/index must be 16-byte aligned, mb 4-byte aligned");
-  const size_t nmb = (size_t)(w / 16) * (h / 16), nwpp = (6 * nmb + 63) / 64;
-  const int chunk = pictures_per_launch(w, h, stride);
+  const size_t nmb = (size_t)(w / 16) * (h / 16);
+  // the index's groups run over the whole batch (64 blocks each, across
+  // picture boundaries): a launch split starts on a group boundary, i.e. at a
+  // multiple of 32 pictures (32 * 6 * nmb blocks = 3 * nmb groups)
+  int chunk = pictures_per_launch(w, h, stride);
+  if (chunk < nframes) {
+    if (32 * stride >= ((int64_t)1 << 31)) return fail(P64GPU_E_INVALID, "decode_recon_packed: frame_stride");
+    chunk = std::max(32, chunk & ~31);  // (32 pictures are always within range: 4096x4096 is ~805 MB)
+  }
   for (int f0 = 0; f0 < nframes; f0 += chunk) {
     const int nf = nframes - f0 < chunk ? nframes - f0 : chunk;
     const size_t m0 = (size_t)f0 * nmb;
     HIP_TRY(p64k::recon_pk(w, h, nf, stride, ref + (size_t)f0 * stride, recon + (size_t)f0 * stride, levels,
-                           (uint32_t)nlevels, index + (size_t)f0 * nwpp * 4, mb + m0, quant_mb + m0,
+                           (uint32_t)nlevels, index + m0 * 6 / 64 * 4, mb + m0, quant_mb + m0,
                            coded_mask + m0, (hipStream_t)stream));
   }
   return P64GPU_OK;

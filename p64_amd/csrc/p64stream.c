@@ -783,29 +783,27 @@ int64_t p64s_pack_levels(int format, int nframes, const p64_mb_rec *mb, const ui
     return fail(P64GPU_E_INVALID, "pack_levels: bad arguments");
   int ngob = 0;
   p64s_geometry(format, NULL, NULL, &ngob);
-  const int64_t nmb = (int64_t)ngob * 33, nb = 6 * nmb, ngr = (nb + 63) / 64;
+  const int64_t nmb = (int64_t)ngob * 33, nball = 6 * nmb * nframes, ngr = (nball + 63) / 64;
   int64_t n = 0;
-  for (int64_t f = 0; f < nframes; f++) {
-    for (int64_t j = 0; j < ngr; j++) {
-      uint64_t m = 0;
-      const int64_t start = n;
-      for (int i = 0; i < 64 && 64 * j + i < nb; i++) {
-        const int64_t blk = 64 * j + i, k = f * nmb + blk / 6;
-        const int b = (int)(blk % 6), mt = mb[k].mtype;
-        if (mt < 0 || mt > 9) return fail(P64GPU_E_INVALID, "pack_levels: MTYPE %d at MB %lld", mt, (long long)k);
-        const int cbp = CBP_MT[mt] ? mb[k].cbp : 0x3f;
-        if (coded[k] && TC_MT[mt] && ((cbp >> (5 - b)) & 1)) {
-          memcpy(levels + n * 64, coef + (k * 6 + b) * 64, 64 * sizeof *levels);
-          m |= 1ull << i;
-          n++;
-        }
+  for (int64_t j = 0; j < ngr; j++) {  // groups of 64 consecutive blocks of the batch
+    uint64_t m = 0;
+    const int64_t start = n;
+    for (int i = 0; i < 64 && 64 * j + i < nball; i++) {
+      const int64_t blk = 64 * j + i, k = blk / 6;  // (k: the MB over the batch)
+      const int b = (int)(blk % 6), mt = mb[k].mtype;
+      if (mt < 0 || mt > 9) return fail(P64GPU_E_INVALID, "pack_levels: MTYPE %d at MB %lld", mt, (long long)k);
+      const int cbp = CBP_MT[mt] ? mb[k].cbp : 0x3f;
+      if (coded[k] && TC_MT[mt] && ((cbp >> (5 - b)) & 1)) {
+        memcpy(levels + n * 64, coef + (k * 6 + b) * 64, 64 * sizeof *levels);
+        m |= 1ull << i;
+        n++;
       }
-      uint32_t *e = index + 4 * (f * ngr + j);
-      e[0] = (uint32_t)start;
-      e[1] = 0;
-      e[2] = (uint32_t)m;
-      e[3] = (uint32_t)(m >> 32);
     }
+    uint32_t *e = index + 4 * j;
+    e[0] = (uint32_t)start;
+    e[1] = 0;
+    e[2] = (uint32_t)m;
+    e[3] = (uint32_t)(m >> 32);
   }
   return n;
 }

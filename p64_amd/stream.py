@@ -367,7 +367,7 @@ def pack_levels(fmt: int, mb, coded, coef):
     if mbv.size != n * nmb or cf.size != n * nmb * 384:
         raise P64GpuError("pack_levels: arrays do not match the picture format")
     levels = np.empty((n * nmb * 6, 64), np.int16)
-    index = np.empty((n * ((6 * nmb + 63) // 64), 4), np.uint32)
+    index = np.empty(((n * 6 * nmb + 63) // 64, 4), np.uint32)  # groups of 64 blocks of the batch
     k = int(lib().p64s_pack_levels(fmt, n, mbv.ctypes.data, cd.ctypes.data, cf.ctypes.data,
                                    levels.ctypes.data, index.ctypes.data))
     _check(k if k < 0 else 0)

@@ -660,6 +660,44 @@ def test_split_launches_match_single_launch(p64, torch_dev, monkeypatch):
     np.testing.assert_array_equal(whole[6], whole[5])  # decoder == encoder reconstruction
 
 
+def test_packed_decode_split_launches(p64, torch_dev, monkeypatch):
+    """p64gpu_decode_recon_packed over 40 QCIF pictures: its index groups run
+    across picture boundaries, so a split launch (P64GPU_CHUNK_BYTES: the
+    smallest split, at 32 pictures) starts on a group boundary; one launch,
+    the split launches and the dense entry give the same reconstructions,
+    which equal the encoder's."""
+    torch = torch_dev
+    w, h, S = 176, 144, 40
+    nmb, pic = (w // 16) * (h // 16), w * h * 3 // 2
+    frames = [dev(torch, np.stack([p64.synth_frame(51 + s, t, w, h) for s in range(S)])) for t in range(2)]
+    li = torch.zeros(S * nmb, dtype=torch.uint8, device="cuda")
+    r0 = torch.zeros(S * pic, dtype=torch.uint8, device="cuda")
+    r1 = torch.zeros_like(r0)
+    p64.encode_frames(frames[0], None, r0, li, width=w, height=h, intra=True, quant=6)
+    o1 = p64.encode_frames(frames[1], r0, r1, li, width=w, height=h, intra=False, quant=6,
+                           me_mode=p64.ME_FULL, search_limit=31)
+    qmb = torch.full((S * nmb,), 6, dtype=torch.uint8, device="cuda")
+    mask = torch.ones_like(qmb)
+    mask[::5] = 0  # some MBs not coded: their prediction only
+    lv, n, ix = p64.pack_levels_device(o1.coef, o1.mb, mask, w, h)
+    assert ix.shape[0] == (S * 6 * nmb + 63) // 64
+    dense = torch.zeros_like(r0)
+    p64.decode_recon(r0, dense, o1.coef, o1.mb, qmb, mask, width=w, height=h)
+    whole = torch.zeros_like(r0)
+    p64.decode_recon_packed(r0, whole, lv, n, ix, o1.mb, qmb, mask, width=w, height=h)
+    monkeypatch.setenv("P64GPU_CHUNK_BYTES", "20000")
+    split = torch.zeros_like(r0)
+    p64.decode_recon_packed(r0, split, lv, n, ix, o1.mb, qmb, mask, width=w, height=h)
+    torch.cuda.synchronize()
+    assert torch.equal(whole, dense)
+    assert torch.equal(split, dense)
+    full = torch.zeros_like(r0)
+    p64.decode_recon_packed(r0, full, *p64.pack_levels_device(o1.coef, o1.mb, torch.ones_like(qmb), w, h),
+                            o1.mb, qmb, torch.ones_like(qmb), width=w, height=h)
+    torch.cuda.synchronize()
+    assert torch.equal(full, r1)  # decoder == encoder reconstruction
+
+
 @pytest.mark.parametrize("content,mode", [("pan15", 1), ("noise", 1), ("flat", 1), ("pan15", 0)])
 def test_stress_contents_vs_oracle(p64, oracle_mod, torch_dev, content, mode):
     """The bench's stress inputs (+-15-px pans, uniform noise,

@@ -346,7 +346,8 @@ def test_pack_levels_matches_restatement(p64):
     the reader's output of short.p64 and on a golden sequence's records:
     exactly the blocks DecompressMDU reads (p64.c:1200-1217: MB present,
     MTYPE with coefficients, CBP bit) in raster order, and per 64-block
-    group its first block's index and mask."""
+    group of the batch (groups straddle pictures) its first block's index
+    and mask."""
     import numpy as np
     from p64_amd import stream
     from test_oracle_golden import load
@@ -358,14 +359,14 @@ def test_pack_levels_matches_restatement(p64):
         mt = mb["mtype"].astype(int).reshape(n, nmb)
         cbp = np.where(CB[mt] == 1, mb["cbp"].astype(int).reshape(n, nmb) & 63, 63)
         bits = (cbp[..., None] >> (5 - np.arange(6))) & 1
-        tx = (bits * TC[mt][..., None] * (coded.reshape(n, nmb)[..., None] != 0)).reshape(n, 6 * nmb)
-        ngr = (6 * nmb + 63) // 64
-        pad = np.zeros((n, ngr * 64), np.int64)
-        pad[:, :6 * nmb] = tx
+        tx = (bits * TC[mt][..., None] * (coded.reshape(n, nmb)[..., None] != 0)).reshape(n * 6 * nmb)
+        ngr = (n * 6 * nmb + 63) // 64  # groups of 64 consecutive blocks of the batch
+        pad = np.zeros(ngr * 64, np.int64)
+        pad[:n * 6 * nmb] = tx
         g = pad.reshape(-1, 64)
         cnt = g.sum(1)
         m = (g.astype(np.uint64) << np.arange(64, dtype=np.uint64)).sum(1, dtype=np.uint64)
-        return coef.reshape(n, 6 * nmb, 64)[tx == 1], np.cumsum(cnt) - cnt, m
+        return coef.reshape(n * 6 * nmb, 64)[tx == 1], np.cumsum(cnt) - cnt, m
 
     r = stream.Reader(open(os.path.join(GOLDEN, "short.p64"), "rb").read())
     pics = list(r)
@@ -384,3 +385,27 @@ def test_pack_levels_matches_restatement(p64):
         np.testing.assert_array_equal(ix[:, 0], start)
         assert not ix[:, 1].any()
         np.testing.assert_array_equal(ix[:, 2].astype(np.uint64) | (ix[:, 3].astype(np.uint64) << np.uint64(32)), m)
+
+
+def test_pack_levels_device_matches_host_packer(p64, monkeypatch):
+    """p64_amd.pack_levels_device (the bench's packer, torch ops -- run here
+    on CPU tensors) writes the same levels and index as p64s_pack_levels, for
+    QCIF and CIF batches whose groups straddle pictures."""
+    import numpy as np
+    import torch
+    from p64_amd import stream
+    monkeypatch.setattr(p64, "_torch", lambda: torch)
+    rng = np.random.default_rng(1)
+    for w, h in ((176, 144), (352, 288)):
+        nmb, S = (w // 16) * (h // 16), 7
+        mb = np.zeros((S, nmb, 4), np.int8)
+        mb[..., 0] = rng.integers(0, 10, (S, nmb))
+        mb[..., 1] = rng.integers(1, 64, (S, nmb))
+        coef = rng.integers(-5, 5, (S, nmb, 6, 64)).astype(np.int16)
+        coded = (rng.random((S, nmb)) > 0.2).astype(np.uint8)
+        lv, n, ix = p64.pack_levels_device(torch.tensor(coef), torch.tensor(mb), torch.tensor(coded), w, h)
+        lv2, ix2 = stream.pack_levels(stream.format_of(w, h), mb.reshape(-1, 4).view(p64.MB_DTYPE).reshape(-1),
+                                      coded, coef)
+        assert n == len(lv2)
+        np.testing.assert_array_equal(lv.numpy(), lv2)
+        np.testing.assert_array_equal(ix.numpy().view(np.uint32), ix2)

@@ -3,7 +3,7 @@
 #   tools/lease.sh TAG step [step ...]
 # steps (run in order; the first failure ends the lease, each GPU step under
 # its own time limit; everything lands under gpurun_out/TAG/):
-#   tests[=pytest -k expr]   pytest -m gpu (all, or the -k selection)
+#   tests[=a,b,...]          pytest -m gpu (all, or -k "a or b or ...")
 #   smoke                    __graft_entry__.smoke()
 #   bench[=args,comma,sep]   bench.py --gpus 1 --steps 20 --warmup 5 [args] -> bench[_args].json
 #   prof[=args]              rocprofv3 --kernel-trace --stats of the bench (--no-cpu) + timed region
@@ -29,7 +29,7 @@ for st in "$@"; do
   case $name in
     tests)
       sel=()
-      [ -n "$arg" ] && sel=(-k "$arg")
+      [ -n "$arg" ] && sel=(-k "$(echo "$arg" | sed 's/,/ or /g')")  # a,b: -k "a or b"
       timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread "${sel[@]}" \
         > $O/gpu_tests$sfx.log 2>&1 || { tail -40 $O/gpu_tests$sfx.log; exit 1; }
       tail -1 $O/gpu_tests$sfx.log | tee -a $O/summary.txt ;;
