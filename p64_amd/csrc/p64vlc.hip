@@ -232,6 +232,42 @@ struct LdsBitWriter {
   }
 };
 
+// The block's codes from its bit 0 into the lane's scratch (VLC_SCR words in
+// registers, left-aligned, MSB first), counting them: the one pass of VLC_ONE
+// (the count and the codes together; the emission then copies the words to
+// the lane's start).  The words shift through r[0..VLC_SCR-1] as they
+// complete (r[0] the newest, static register indices: no LDS spent on it);
+// a block of more than 32 VLC_SCR bits is coded again at the emission.
+// (Measured, tools/vlc_time.py: 6 words 42.7 us, 5: 50.4, 7: 45.1, 8: 44.0;
+// the same scratch in LDS, 8 words: 45.7 -- one workgroup less per CU.)
+#ifndef VLC_SCR_N
+#define VLC_SCR_N 6
+#endif
+constexpr int VLC_SCR = VLC_SCR_N;  // scratch words per lane (192 bits)
+struct RegScrWriter {
+  uint64_t acc = 0;
+  int nacc = 0, nw = 0, bits = 0;
+  uint32_t r[VLC_SCR];
+  __device__ __forceinline__ void push(uint32_t x) {
+#pragma unroll
+    for (int k = VLC_SCR - 1; k > 0; k--) r[k] = r[k - 1];
+    r[0] = x;
+    nw++;
+  }
+  __device__ __forceinline__ void put(uint32_t v, int n) {
+    acc = (acc << n) | v;
+    nacc += n;
+    bits += n;
+    if (nacc >= 32) {
+      push((uint32_t)(acc >> (nacc - 32)));
+      nacc -= 32;
+    }
+  }
+  __device__ __forceinline__ void finish() {
+    if (nacc > 0) push((uint32_t)(acc << (32 - nacc)));
+  }
+};
+
 // the scan positions of a block holding a nonzero level, as two 32-bit masks
 // (bit p of m0: position p; of m1: position 32 + p) from its 32 packed level
 // pairs: v_pk_min_u16 against 1 (a nonzero int16 is >= 1 as u16), v_dot2
@@ -278,32 +314,37 @@ __device__ __forceinline__ void code_of(const VlcTables &T, uint32_t e, bool fir
 template <typename L, class W>  // L: the level copy, int8 in LDS (the common case) or the int16 levels themselves
 __device__ __forceinline__ void block_codes(const VlcTables &T, const L *lvs, uint32_t m0, uint32_t m1, bool cbpt,
                                             W &bw) {
-  uint64_t m = ((uint64_t)m1 << 32) | m0;
-  if (cbpt && !m) return;
+  if (cbpt && !(m0 | m1)) return;
   int last = cbpt ? -1 : 0;
   bool first = cbpt;
-  while (m) {
-    const int p1 = (int)__builtin_ctzll(m);
-    m &= m - 1u;
-    const bool two = m != 0;
-    const int p2 = two ? (int)__builtin_ctzll(m | (1ull << 63)) : p1;
-    m &= m - 1u;
-    const int l1 = (int)lvs[p1], l2 = (int)lvs[p2];
-    const int r1 = p1 - last - 1, r2 = p2 - p1 - 1;
-    last = p2;
-    const int a1 = l1 < 0 ? -l1 : l1, a2 = l2 < 0 ? -l2 : l2;
-    const uint32_t e1 = T.t[T_TC + min(r1, 26) * 16 + min(a1, 15)];
-    const uint32_t e2 = T.t[T_TC + min(r2, 26) * 16 + min(a2, 15)];
-    uint32_t v;
-    int n;
-    code_of(T, e1, first, r1, l1, v, n);
-    bw.put(v, n);
-    if (two) {
-      code_of(T, e2, false, r2, l2, v, n);
+  // the two 32-position halves one after the other (32-bit find-first-set
+  // and clear: three VALU per position instead of seven on the 64-bit mask)
+  auto half = [&](uint32_t mh, int pb) {
+    while (mh) {
+      const int p1 = pb + (int)__builtin_ctz(mh);
+      mh &= mh - 1u;
+      const bool two = mh != 0;
+      const int p2 = two ? pb + (int)__builtin_ctz(mh) : p1;
+      mh &= mh - 1u;
+      const int l1 = (int)lvs[p1], l2 = (int)lvs[p2];
+      const int r1 = p1 - last - 1, r2 = p2 - p1 - 1;
+      last = p2;
+      const int a1 = l1 < 0 ? -l1 : l1, a2 = l2 < 0 ? -l2 : l2;
+      const uint32_t e1 = T.t[T_TC + min(r1, 26) * 16 + min(a1, 15)];
+      const uint32_t e2 = T.t[T_TC + min(r2, 26) * 16 + min(a2, 15)];
+      uint32_t v;
+      int n;
+      code_of(T, e1, first, r1, l1, v, n);
       bw.put(v, n);
+      if (two) {
+        code_of(T, e2, false, r2, l2, v, n);
+        bw.put(v, n);
+      }
+      first = false;
     }
-    first = false;
-  }
+  };
+  half(m0, 0);
+  half(m1, 32);
   const Code eob = tab(T, T_EOB);
   bw.put(eob.v, eob.len);
 }
@@ -336,7 +377,10 @@ __device__ __forceinline__ void block_codes(const VlcTables &T, const L *lvs, ui
 // it.  A wave with a coded level outside -128..127 (which the reference's
 // quantiser never makes, but the ABI takes) reads the int16 levels from
 // memory instead: the codes stay the host writer's for every int16 value.
-constexpr int VLC_STAGE = 80;
+#ifndef VLC_STAGE_N
+#define VLC_STAGE_N 64  // bytes of LDS per lane for its levels (80, 16 of them padding: one workgroup less per CU)
+#endif
+constexpr int VLC_STAGE = VLC_STAGE_N;
 enum { VLC_COUNT = 0, VLC_ONE = 1, VLC_GIVEN = 2 };
 // status words, two per workgroup of a picture (zeroed before the launch):
 // [0] the look-back word: flag (bits 62-63: 1 = the workgroup's own total,
@@ -380,10 +424,12 @@ __global__ __launch_bounds__(64 * VLC_WAVES) void k_vlc_blk(VlcArgs a) {
   const p64k::VlcLenTab &Lg = d_tabs.l;
   constexpr bool EMIT = MODE != VLC_COUNT, COUNT = MODE != VLC_GIVEN;
   __shared__ VlcTables T;  // per-lane table lookups from LDS, loaded once per workgroup
-  __shared__ uint32_t vlen[COUNT ? p64k::VLC_LEN_WORDS : 1];  // the count's code lengths (vlc_count.h)
-  if (COUNT && threadIdx.x < 64) p64k::load_vlc_len(Lg, vlen, threadIdx.x);
+  __shared__ uint32_t vlen[COUNT && MODE != VLC_ONE ? p64k::VLC_LEN_WORDS : 1];  // the count's code lengths (vlc_count.h)
+  if (COUNT && MODE != VLC_ONE && threadIdx.x < 64) p64k::load_vlc_len(Lg, vlen, threadIdx.x);
   __shared__ __align__(16) uint8_t stage[VLC_WAVES * 64 * VLC_STAGE];  // each lane's levels, scan order
   __shared__ __align__(16) uint32_t wbits[EMIT ? VLC_WAVES * VLC_EMIT_WORDS : 4];
+  constexpr bool ONEPASS = MODE == VLC_ONE;  // the count pass writes the codes (RegScrWriter)
+  RegScrWriter sw;
   for (int i = threadIdx.x; i < T_N; i += 64 * VLC_WAVES) T.t[i] = Tg.t[i];
   __syncthreads();
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -453,7 +499,21 @@ __global__ __launch_bounds__(64 * VLC_WAVES) void k_vlc_blk(VlcArgs a) {
   const int16_t *lvg = reinterpret_cast<const int16_t *>(a.coef) + ((base + k) * 6 + b) * 64;
   uint16_t *bk = a.blk_bits + (base + k) * 8;
   int bb = 0;  // the block's bits (an intra block's DC included)
-  if (COUNT) {
+  if (ONEPASS) {
+    if (coded) {
+      if (!cbpt) {  // EncodeDC codec.c:343-352
+        const int dc0 = (int)(int16_t)(lv[0] & 0xffffu);
+        const int dc = dc0 < 1 ? 1 : (dc0 > 254 ? 254 : dc0);
+        sw.put((uint32_t)(dc == 128 ? 255 : dc), 8);
+      }
+      if (narrow)
+        block_codes(T, lvs, m0, m1, cbpt, sw);
+      else
+        block_codes(T, lvg, m0, m1, cbpt, sw);
+      sw.finish();
+      bb = sw.bits;
+    }
+  } else if (COUNT) {
     const uint8_t *len = reinterpret_cast<const uint8_t *>(vlen);
     if (narrow) {
       if (coded) bb = p64k::block_vlc_bits(len, lvs, m0, m1, cbpt);
@@ -480,7 +540,7 @@ __global__ __launch_bounds__(64 * VLC_WAVES) void k_vlc_blk(VlcArgs a) {
   const int tot = __builtin_amdgcn_readlane(incl, 63);
   const bool bad = __any(hbad);
   const uint32_t trv = (uint32_t)a.tr[fi] & 31u, gqv = a.gquant[(size_t)fi * a.ngob + g] & 31u;
-  auto emit = [&](auto &bw, uint32_t *dst, int64_t base) {
+  auto emit = [&](auto &bw, uint32_t *dst, int64_t base, bool block) {
     if (act && b == 0) {
       bw.start(dst, base + rel);
       if (j == 0) {  // WritePictureHeader marker.c:103-135
@@ -499,7 +559,7 @@ __global__ __launch_bounds__(64 * VLC_WAVES) void k_vlc_blk(VlcArgs a) {
         if (hd.c[i].len) bw.put(hd.c[i].v, hd.c[i].len);
       bw.finish();
     }
-    if (coded) {
+    if (coded && block) {
       bw.start(dst, base + rel + hbits);
       if (!cbpt) {  // EncodeDC codec.c:343-352
         const int dc0 = (int)(int16_t)(lv[0] & 0xffffu);
@@ -548,7 +608,23 @@ __global__ __launch_bounds__(64 * VLC_WAVES) void k_vlc_blk(VlcArgs a) {
     if (tot > 0) {
       LdsBitWriter bw;
       bw.w0 = 0;
-      emit(bw, wb, 0);
+      // VLC_ONE: a block whose codes fit the scratch is copied from it to the
+      // lane's start (word by word, shifted, ORed where lanes share a word);
+      // the others are coded again here
+      const bool scr = ONEPASS && bb <= 32 * VLC_SCR;
+      emit(bw, wb, 0, !scr);
+      if (ONEPASS && coded && scr) {
+        const int p = rel + hbits, sh = p & 31, wi = p >> 5;
+#pragma unroll
+        for (int k = 0; k < VLC_SCR; k++) {
+          const int i = sw.nw - 1 - k;  // r[k] is word i of the block
+          if (i >= 0) {
+            const uint32_t sv = sw.r[k];
+            atomicOr(wb + wi + i, __builtin_bswap32(sv >> sh));
+            if (sh) atomicOr(wb + wi + i + 1, __builtin_bswap32(sv << (32 - sh)));
+          }
+        }
+      }
     }
 #endif
   }
@@ -650,7 +726,7 @@ __global__ __launch_bounds__(64 * VLC_WAVES) void k_vlc_blk(VlcArgs a) {
       bw.sh = s_shw;
       bw.wlo = w0;
       bw.whi = wl;
-      emit(bw, out, first + off[wv]);
+      emit(bw, out, first + off[wv], true);
     }
     __threadfence();
     __syncthreads();

@@ -5,9 +5,11 @@ XCD in bits 56..59), levels and records arrived, tables in LDS (barrier),
 blocks counted, codes in the LDS copy, start known (barrier after the
 look-back), words stored, end -- into a device array read back through
 p64dbg_vlc_stamps(); builds abtest/lib_vlcstamp.so from it (the other objects
-from the current build).  Run tools/vlc_timeline.py on the GPU box."""
+from the current build; extra hipcc flags from the command line, e.g.
+-DVLC_STAGE_N=64).  Run tools/vlc_timeline.py on the GPU box."""
 import os
 import subprocess
+import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 s = open(os.path.join(REPO, "p64_amd/csrc/p64vlc.hip")).read()
@@ -78,8 +80,8 @@ open(src, "w").write(s)
 try:
     os.makedirs(os.path.join(REPO, "abtest"), exist_ok=True)
     obj = os.path.join(REPO, "abtest/vlcstamp.o")
-    subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-c", src, "-o", obj],
-                   check=True)
+    subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", *sys.argv[1:], "-c",
+                    src, "-o", obj], check=True)
 finally:
     os.remove(src)
 c = os.path.join(REPO, "p64_amd/csrc")
