@@ -1474,8 +1474,8 @@ def measure_vlc(args, torch, p64_amd, enc, S, nmb, w, h):
     t's pictures into the FrameBatchOut o (the caller's closed loop).  Per
     step: the encode launches on the main stream, then the entropy coder's
     launch (counting the blocks' bits itself, or taking the encoder's counts:
-    both measured) and a copy of every picture's bit count to pinned host
-    memory FORKED onto a side stream, so step t's coder runs concurrently
+    both measured), storing every picture's bit count straight into pinned
+    host memory, FORKED onto a side stream, so step t's coder runs concurrently
     with step t+1's encode (round 6: the coder reads only step t's records
     and levels; two output sets alternate, and an encode waits for the coder
     that read its set two steps before); the side stream joins at the end.
@@ -1506,9 +1506,11 @@ def measure_vlc(args, torch, p64_amd, enc, S, nmb, w, h):
         side = torch.cuda.Stream()
 
         def coder(k, o, given):
-            _, bits = p64s.vlc_pictures(o.mb, o.coef, gq, trs[k], width=w, height=h, buffers=bufs,
-                                        host_bits=False, blk_bits=o.vlc_bits if given else None)
-            host[k].copy_(bits, non_blocking=True)
+            # each picture's bit count stored by the coder straight into the
+            # pinned host row (device-addressable: p64gpu_vlc_args, ABI v3) --
+            # no copy launch after it
+            p64s.vlc_pictures(o.mb, o.coef, gq, trs[k], width=w, height=h, buffers=(bufs[0], host[k], bufs[2]),
+                              host_bits=False, blk_bits=o.vlc_bits if given else None)
 
         def run(given, split):
             def out(k):
@@ -1600,9 +1602,10 @@ def measure_vlc(args, torch, p64_amd, enc, S, nmb, w, h):
                                 "ok": True}
         res["note"] = ("encode launches + GPU entropy coding (one launch after the status words' zeroing "
                        "kernel: each workgroup of 40 MBs counts or takes its bits, finds its start by a "
-                       "decoupled look-back, writes its words) per step, the coder and the bit-count copy to "
-                       "pinned host memory forked onto a side stream (concurrent with the next step's encode, "
-                       "or with its second half when split: P64GPU_FLAG_SEARCH_ONLY + ME_GIVEN), the steps "
+                       "decoupled look-back, writes its words) per step, the coder -- its bit counts "
+                       "stored straight into pinned host memory -- forked onto a side stream (concurrent "
+                       "with the next step's encode, or with its second half when split: "
+                       "P64GPU_FLAG_SEARCH_ONLY + ME_GIVEN), the steps "
                        "replayed as one HIP graph after a spin-up; the fastest of four paths (path / "
                        "other_paths); not part of `value`")
         return res
