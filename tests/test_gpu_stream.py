@@ -468,14 +468,16 @@ def test_gpu_vlc_big_path_stress(p64, torch_dev, given):
             assert gpu >> (hb - 8 * len(full)) == int.from_bytes(full, "big"), (rep, t)
 
 
-@pytest.mark.parametrize("given", [False, True])
-def test_fed_path_stitched_streams(p64, torch_dev, tmp_path, given):
+@pytest.mark.parametrize("given,fork", [(False, True), (True, True), (False, False)])
+def test_fed_path_stitched_streams(p64, torch_dev, tmp_path, given, fork):
     """bench.py --feed root --gather coded at world 1: each step's pictures
-    coded on the GPU at their sequences' bit phases (bench.CodedFeed), gathered
-    one step late on the side stream, stitched on rank 0 (stitch_pieces):
-    byte-identical to the host writer over the same records
-    (p64s_write_picture) and to the .p64 the CLI writes for those pictures
-    (p64.c:524-613, stream.c:142-150, 193)."""
+    coded on the GPU at their sequences' bit phases (bench.CodedFeed: the
+    coder forked onto the side stream beside the next step's encode, the
+    output sets alternating -- or, fork=False, on the encode stream), gathered
+    on the side stream, stitched on rank 0 (stitch_pieces): byte-identical to
+    the host writer over the same records (p64s_write_picture) and to the
+    .p64 the CLI writes for those pictures (p64.c:524-613, stream.c:142-150,
+    193)."""
     import sys
     sys.path.insert(0, REPO)
     import bench
@@ -486,22 +488,26 @@ def test_fed_path_stitched_streams(p64, torch_dev, tmp_path, given):
     fr = p64.synth_frames_device(w, h, 3, S, 0, n, content=p64.SYNTH_SURVEY)
     rec = [torch.zeros(S * pic, dtype=torch.uint8, device="cuda") for _ in range(2)]
     li = torch.zeros(S * nmb, dtype=torch.uint8, device="cuda")
-    out = p64.FrameBatchOut(coef=torch.zeros((S, nmb, 6, 64), dtype=torch.int16, device="cuda"),
-                            mb=torch.empty((S, nmb, 4), dtype=torch.int8, device="cuda"),
-                            me=torch.empty((S, nmb, 7), dtype=torch.int32, device="cuda"),
-                            vlc_bits=(torch.empty((S, nmb, 8), dtype=torch.int16, device="cuda")
-                                      if given else None))
+    outs = [p64.FrameBatchOut(coef=torch.zeros((S, nmb, 6, 64), dtype=torch.int16, device="cuda"),
+                              mb=torch.empty((S, nmb, 4), dtype=torch.int8, device="cuda"),
+                              me=torch.empty((S, nmb, 7), dtype=torch.int32, device="cuda"),
+                              vlc_bits=(torch.empty((S, nmb, 8), dtype=torch.int16, device="cuda")
+                                        if given else None)) for _ in range(2)]
     feed = bench.CodedFeed(torch, stream, 1, 0, S, w, h, 8, keep=range(S))
+    assert feed.fork  # (the default)
+    feed.fork = fork
     fmt = stream.format_of(w, h)
     host = [stream.Writer(fmt) for _ in range(S)]
     for t in range(n):
+        out = outs[t % 2]
+        feed.before_encode(t)  # (the coder of step t-2 read this set)
+        out.coef.zero_()  # (inter pictures store only their nonzero blocks)
         p64.encode_frames(fr[t].reshape(-1), rec[(t + 1) % 2], rec[t % 2], li, width=w, height=h,
                           intra=(t == 0), quant=8, me_mode=p64.ME_FULL, search_limit=31, out=out)
         feed.code(t, out)
         mb, coef = out.mb.cpu().numpy(), out.coef.cpu().numpy()
         for s in range(S):
             host[s].write_picture(t % 32, mb[s], coef[s], 8)
-        out.coef.zero_()  # (inter pictures store only their nonzero blocks)
     feed.finish()
     got = feed.streams(fmt, n % 32)
     for s in range(S):
