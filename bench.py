@@ -260,15 +260,20 @@ def stitch_pieces(writers, pieces, bits):
 class CodedFeed:
     """--feed root --gather coded: the rank's pictures entropy-coded on its
     GPU each step, every picture at its sequence's running bit phase
-    (p64gpu_vlc_pictures; p64EncodeSequence's continuous stream, p64.c:524-613),
-    and the coded pictures gathered to rank 0 -- one step LATE, on a side
-    stream: step t's coder writes buffer t % 2 and records the step's longest
-    picture on the device; the gather of step t-1 then waits for that event on
-    the side stream, MAX-reduces the size there and reads it back with a
-    side-stream sync, so the encode stream never waits for the host and the
-    gather overlaps step t's encode (round 6: no per-step .item() on the
-    encode stream).  Before the coder reuses a buffer the encode stream waits
-    for the side stream.  finish() gathers the last step.
+    (p64gpu_vlc_pictures with seq_bits / max_bits: the coder continues each
+    sequence's stream on the device; p64EncodeSequence's continuous stream,
+    p64.c:524-613), and the coded pictures gathered to rank 0 on a side
+    stream.  Forked (the default): step t's coder runs on the side stream
+    behind an event on the encode stream, beside step t+1's encode; the
+    encode outputs alternate between two sets, and before_encode(t) makes the
+    encode stream wait for the coder that read its set (step t-2's).  At N>1
+    the gather of step t-1 (a MAX all-reduce of the longest picture, its size
+    read back on the side stream, then the payloads) is issued before step
+    t's coder, so the host's only wait ends with step t-1's coder and the
+    encode stream never waits for the host; at one rank the gather is the
+    identity and follows each coder at once (no size read back).  finish()
+    gathers the last step.  (P64_FEED_FORK=0: the coder on the encode
+    stream, the gather one step late -- round 6's first form.)
     Rank 0 keeps the pieces of the sequences in `keep` (global indices) for
     stitch_pieces; verification happens after the timed region."""
 
