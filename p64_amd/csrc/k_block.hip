@@ -1151,12 +1151,14 @@ __global__ __launch_bounds__(64) OCC4 void k_recon_mbg(int w, int h, int64_t str
 // MB and a group may straddle two pictures) its first transmitted block's
 // index and its transmitted-block mask, {start, 0, mask lo, mask hi}
 // (p64s_pack_levels).  The wave reads its group's entry with one scalar load
-// while its records are in flight and issues its level loads at once from
-// start + (the lane's rank among the set bits) -- the levels no longer wait
-// for the record (in k_recon_mbg a lane learns from its record whether, and
-// so where, to load); only the prediction source does.  (Round 6's first
-// form gave each picture ceil(6 nmb / 64) groups of its own: 2.4% more waves
-// at CIF, the last of each picture 8/64 full -- 36.5 against 35.2 us.)
+// while its records are in flight; the prediction source's loads go out as
+// soon as the record is in, then the level loads from start + (the lane's
+// rank among the set bits) -- they need no record (in k_recon_mbg a lane
+// learns from its record whether, and so where, to load).  Measured: levels
+// issued before the prediction source 35.6-35.8 us, after it 34.9 (HBM 0.497,
+// A/B in one lease, r06ar).  (Round 6's first form gave each picture
+// ceil(6 nmb / 64) groups of its own: 2.4% more waves at CIF, the last of
+// each picture 8/64 full.)
 typedef unsigned su4 __attribute__((ext_vector_type(4)));
 __global__ __launch_bounds__(64) OCC4 void k_recon_pk(int w, int h, int64_t stride, const uint8_t *refp,
                                                           uint8_t *recp, const int16_t *levels, uint32_t nlev,
@@ -1186,33 +1188,24 @@ __global__ __launch_bounds__(64) OCC4 void k_recon_pk(int w, int h, int64_t stri
   A.m = __builtin_amdgcn_raw_buffer_load_b32(B.mb, 4 * gmb, 0, 0);
   A.q = __builtin_amdgcn_raw_buffer_load_b8(B.q, gmb, 0, 0);
   A.coded = __builtin_amdgcn_raw_buffer_load_b8(B.mask, valid ? gmb : BUF_OOB, 0, 0);
-  // the group's entry by a scalar load (its wait is on the scalar counter:
-  // the record loads above stay in flight), then the level loads
+  // the group's entry by a scalar load issued now and waited for only after
+  // the prediction source's loads are out (rec_stage_b waits for the record
+  // alone), then the level loads
   su4 ix;
-  asm volatile("s_load_dwordx4 %0, %1, %2\n s_waitcnt lgkmcnt(0)"
-               : "=s"(ix)
-               : "s"(index), "s"(16u * wv));
+  asm volatile("s_load_dwordx4 %0, %1, %2" : "=s"(ix) : "s"(index), "s"(16u * wv));
+  RecStageB S = rec_stage_b<false>(B, w, h, stride, A);
+  asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(ix));
   const uint64_t msk = (uint64_t)ix.z | ((uint64_t)ix.w << 32);
   const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(msk >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)msk, 0u));
   const uint32_t lo = ((msk >> lane) & 1) && valid ? (ix.x + rank) * 128u : BUF_OOB;
-  uint32_t lq[8][4];
 #pragma unroll
   for (int k = 0; k < 8; k++) {
     const auto v = __builtin_amdgcn_raw_buffer_load_b128(B.coef, lo + 16 * k, 0, 0);
-    lq[k][0] = v[0];
-    lq[k][1] = v[1];
-    lq[k][2] = v[2];
-    lq[k][3] = v[3];
+    S.lq[k][0] = v[0];
+    S.lq[k][1] = v[1];
+    S.lq[k][2] = v[2];
+    S.lq[k][3] = v[3];
   }
-  // (the compiler otherwise hoists the coded-flag test of rec_stage_b above
-  // these loads, with an s_waitcnt vmcnt(0) for the record: the levels would
-  // wait for it again)
-  __builtin_amdgcn_sched_barrier(0);
-  RecStageB S = rec_stage_b<false>(B, w, h, stride, A);
-#pragma unroll
-  for (int k = 0; k < 8; k++)
-#pragma unroll
-    for (int i = 0; i < 4; i++) S.lq[k][i] = lq[k][i];
   PRIO_LOW();
   __shared__ uint32_t slots[RSLOT * (64 / LPB)];
   rec_wave_compact<false>(w, h, stride, rec, A, S, slots, lane);  // (DIRECT: 119 VGPRs, 4 waves: 39.6 vs 36.1 us, r06f)
