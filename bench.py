@@ -1789,10 +1789,21 @@ def run_decode(args, torch, dist, np, p64_amd, world, enc, S, nmb, pic):
     mask = torch.ones(S * nmb, dtype=torch.uint8, device="cuda")
     first = last - args.steps + 1
     # the packed layout of every picture (the reader's job in a decoder)
-    pk = {}
+    # (every picture's levels in one buffer, as a reader filling a batch
+    # would: separately allocated per picture they measured up to 2 us
+    # apart run to run)
+    pk, parts = {}, []
     for t in range(last + 1):
         lv, n, ix = p64_amd.pack_levels_device(enc["coef"][t], enc["mb"][t], mask, w, h)
-        pk[t] = (lv if n else torch.zeros((1, 64), dtype=torch.int16, device="cuda"), n, ix)
+        parts.append((lv, n, ix))
+    lv_all = torch.zeros((max(1, sum(n for _, n, _ in parts)), 64), dtype=torch.int16, device="cuda")
+    off = 0
+    for t, (lv, n, ix) in enumerate(parts):
+        if n:
+            lv_all[off:off + n].copy_(lv)
+        pk[t] = (lv_all[off:] if n else lv_all[:1], n, ix)
+        off += n
+    del parts
     nbytes = []
     ngr = (S * 6 * nmb + 63) // 64  # the index: 16 bytes per 64 blocks of the batch
     for t in range(first, last + 1):
@@ -1829,8 +1840,12 @@ def run_decode(args, torch, dist, np, p64_amd, world, enc, S, nmb, pic):
         ok = bool(torch.equal(dec[last % 2], enc["recon_last"]))
         return elapsed, kavg, clk, ok
 
-    elapsed, kavg, clk, ok = measure(True)
-    d_el, d_kavg, _, d_ok = measure(False)
+    if os.environ.get("P64_DECODE_DENSE_FIRST", "0") != "0":  # (diagnostic: order effects)
+        d_el, d_kavg, _, d_ok = measure(False)
+        elapsed, kavg, clk, ok = measure(True)
+    else:
+        elapsed, kavg, clk, ok = measure(True)
+        d_el, d_kavg, _, d_ok = measure(False)
     tmax = max_over_ranks(elapsed, world, device="cuda")
     if not all_ranks_ok(ok and d_ok, world, device="cuda"):
         raise SystemExit("bench: decoded pictures differ from the encoder's reconstruction")
