@@ -1,3 +1,9 @@
+"""Per-kernel timeline of a few timed steps from a rocprofv3 kernel trace
+(development aid; how profiles/r06m_fed_trace.txt .. r06o were made):
+    python3 tools/fed_trace.py <kernel_trace.csv> <first step> <last step>
+Steps count the last 20 k_motion dispatches before the final k_clock probe
+(the timed region); each line: start, end, duration (us from the first
+shown), hardware queue, kernel."""
 import csv,sys
 rows=list(csv.DictReader(open(sys.argv[1])))
 rows.sort(key=lambda r:int(r['Start_Timestamp']))
