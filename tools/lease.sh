@@ -7,7 +7,7 @@
 #   smoke                    __graft_entry__.smoke()
 #   bench[=args,comma,sep]   bench.py --gpus 1 --steps 20 --warmup 5 [args] -> bench[_args].json
 #   prof[=args]              rocprofv3 --kernel-trace --stats of the bench (--no-cpu) + timed region
-#   pmc=content              tools/pmc_bench.sh passes for that content
+#   pmc                      tools/pmc_bench.sh: its PMC passes over every content (into gpurun_out/pmcb)
 #   probe[=args]             tools/vlc_fault_probe.py with the bounds-checked coder
 #   sadcount=content         executed v_sad_u8 work of k_motion (abtest/lib_sadcount.so, tools/sad_count.py)
 #   py=script.py[,args]      any tracked python tool, e.g. py=tools/stream_time.py
@@ -52,7 +52,7 @@ for st in "$@"; do
       done
       cat $O/timed_region$sfx.txt >> $O/summary.txt ;;
     pmc)
-      CONTENT=$arg O=$O timeout -k 10 900 bash tools/pmc_bench.sh > $O/pmc_$arg.log 2>&1 || { tail -20 $O/pmc_$arg.log; exit 1; } ;;
+      timeout -k 10 900 bash tools/pmc_bench.sh > $O/pmc.log 2>&1 || { tail -20 $O/pmc.log; exit 1; } ;;
     probe)
       P64GPU_LIB=$R/abtest/lib_vlccheck.so timeout -k 10 300 python3 -u tools/vlc_fault_probe.py $(echo $arg | tr ',' ' ') \
         > $O/probe$sfx.log 2>&1 || { cat $O/probe$sfx.log; exit 1; }
