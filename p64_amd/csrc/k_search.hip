@@ -669,8 +669,15 @@ __device__ __forceinline__ void me_full(const Sx &S, const uint8_t *cur_blk, int
                                                                __builtin_amdgcn_mbcnt_lo((uint32_t)bl, 0u));
         // the entry: ord | Sbot << 16 (finish_halves; acc's high half is
         // Sbot).  Past ME_LIST_MAX entries the dense pass takes over and the
-        // list is not read: the index is clamped rather than tested
-        if (sv) list[min(idx, ME_LIST_MAX - 1)] = (accb[d] << 16) | (base + d);
+        // list is not read: the index is clamped rather than tested -- only
+        // once the list may reach its end (a scalar test: the clamp's VALU
+        // is one of ~8 per candidate row here)
+        const uint32_t e = (accb[d] << 16) | (base + d);
+        if (nsurv <= ME_LIST_MAX - 64) {
+          if (sv) list[idx] = e;
+        } else {
+          if (sv) list[min(idx, ME_LIST_MAX - 1)] = e;
+        }
         nsurv += __popcll(bl);
       }
     }
