@@ -228,9 +228,14 @@ __device__ __forceinline__ int rlevel(int l, int q) {
 // Wave reductions without the LDS crossbar: DPP folds each 16-lane row
 // (quad_perm [1,0,3,2], [2,3,0,1], row_half_mirror, row_mirror), then the four
 // row results are combined in scalar registers.  The result is wave-uniform.
+// (CTRL: full permutations only -- quad_perm, row_half_mirror, row_mirror --
+// so every lane has a source and bound_ctrl changes nothing; with it the
+// compiler needs no zeroed destination first: one v_mov fewer per use that
+// is not fused into its consumer)
 template <int CTRL>
 __device__ __forceinline__ unsigned dpp(unsigned v) {
-  return (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xf, 0xf, false);
+  static_assert((CTRL >= 0 && CTRL <= 0xFF) || CTRL == 0x140 || CTRL == 0x141, "full permutations only");
+  return (unsigned)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xf, 0xf, true);
 }
 // after the row folds every lane of a row holds the row's result; row_bcast:15
 // (rows 1 and 3 take lane 15 of rows 0 and 2) and row_bcast:31 (rows 2 and 3
