@@ -381,9 +381,11 @@ def ctypes_ptr(t):
 
 
 def test_gpu_vlc_graph_replay(p64, torch_dev):
-    """The coder's launch (a memset of its status words + one kernel) captured
-    in a HIP graph and replayed twice gives the eager call's bits: the
-    look-back state is reset by the captured memset, not by the host."""
+    """The coder's launch (a zeroing kernel for its status words + the coder
+    kernel; a captured hipMemsetAsync was seen not to order before the coder
+    on replay) captured in a HIP graph and replayed
+    twice gives the eager call's bits: the look-back state is reset inside
+    the graph, not by the host."""
     from p64_amd import stream
     torch = torch_dev
     z = load("seq_qcif_full31.npz")
@@ -409,6 +411,71 @@ def test_gpu_vlc_graph_replay(p64, torch_dev):
         for t in range(mb.shape[0]):
             nb = (bits[t] + 7) // 8
             np.testing.assert_array_equal(out[t, :nb], out0[t, :nb])
+
+
+def test_gpu_encode_with_forked_coder_graph(p64, torch_dev):
+    """bench.py's with_vlc pattern: each step's encode on the capturing
+    stream, its coder forked onto a side stream behind an event (beside the
+    next step's encode), the bit counts stored straight into pinned host rows,
+    the side stream joined at the end -- one HIP graph, replayed twice from
+    the same closed-loop state.  Every step's pictures equal the host writer
+    over that step's records, bit counts and bytes, on both replays."""
+    from p64_amd import stream
+    torch = torch_dev
+    w, h, S, T = 176, 144, 6, 4
+    nmb, pic = 99, 176 * 144 * 3 // 2
+    fmt = stream.format_of(w, h)
+    fr = p64.synth_frames_device(w, h, 7, S, 0, T + 1, content=p64.SYNTH_SURVEY)
+    rec = [torch.zeros(S * pic, dtype=torch.uint8, device="cuda") for _ in range(2)]
+    li = torch.zeros(S * nmb, dtype=torch.uint8, device="cuda")
+    outs = [p64.FrameBatchOut(coef=torch.zeros((S, nmb, 6, 64), dtype=torch.int16, device="cuda"),
+                              mb=torch.empty((S, nmb, 4), dtype=torch.int8, device="cuda"),
+                              me=torch.empty((S, nmb, 7), dtype=torch.int32, device="cuda")) for _ in range(T)]
+    p64.encode_frames(fr[0].reshape(-1), None, rec[1], li, width=w, height=h, intra=True, quant=8,
+                      out=outs[0])  # picture 0 (intra), then T inter steps in the graph
+    gq = torch.full((S, 3), 8, dtype=torch.uint8, device="cuda")
+    trs = [torch.full((S,), 1 + k, dtype=torch.int32, device="cuda") for k in range(T)]
+    vb = [stream.vlc_buffers(S, w, h) for _ in range(T)]
+    host = torch.empty((T, S), dtype=torch.int32, pin_memory=True)
+    stream.vlc_pictures(outs[0].mb, outs[0].coef, gq, trs[0], width=w, height=h, buffers=vb[0],
+                        host_bits=False)  # (tables uploaded before the capture)
+    saved = [r.clone() for r in rec] + [li.clone()]
+    torch.cuda.synchronize()
+    side = torch.cuda.Stream()
+    ev = [torch.cuda.Event() for _ in range(T)]
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        main = torch.cuda.current_stream()
+        for k in range(T):
+            t = 1 + k
+            p64.encode_frames(fr[t].reshape(-1), rec[t % 2], rec[(t + 1) % 2], li, width=w, height=h,
+                              intra=False, quant=8, me_mode=p64.ME_FULL, search_limit=31, out=outs[k])
+            ev[k].record(main)
+            side.wait_event(ev[k])
+            with torch.cuda.stream(side):
+                stream.vlc_pictures(outs[k].mb, outs[k].coef, gq, trs[k], width=w, height=h,
+                                    buffers=(vb[k][0], host[k], vb[k][2]), host_bits=False)
+        main.wait_stream(side)
+    for rep in range(2):
+        for a, b in zip(rec + [li], saved):
+            a.copy_(b)
+        host.zero_()
+        for b in vb:
+            b[0].zero_()
+        torch.cuda.synchronize()
+        g.replay()
+        torch.cuda.synchronize()
+        for k in range(T):
+            mb, coef, data = outs[k].mb.cpu().numpy(), outs[k].coef.cpu().numpy(), vb[k][0].cpu().numpy()
+            for s in range(S):
+                wr = stream.Writer(fmt)
+                wr.write_picture(1 + k, mb[s], coef[s], 8)
+                nb, bits = wr.bits(), int(host[k, s]) & 0xFFFFFFFF
+                assert bits == nb, (rep, k, s)
+                full = wr.data()
+                nbytes = (bits + 7) // 8
+                gpu = int.from_bytes(data[s, :nbytes].tobytes(), "big") >> (nbytes * 8 - bits)
+                assert gpu >> (nb - 8 * len(full)) == int.from_bytes(full, "big"), (rep, k, s)
 
 
 @pytest.mark.parametrize("given", [False, True])
